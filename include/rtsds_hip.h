@@ -1,0 +1,176 @@
+/*
+ * rtsds_hip.h -- C ABI of librtsds_hip.so, the MI355X (gfx950 / CDNA4) kernels behind the
+ * RTSDS hot path (BiSeNet / DeepLabV2 forward+backward + adversarial DA discriminator step).
+ *
+ * The reference (sina-behnam/RTSDS @ 2024-08-07) is pure PyTorch: every kernel on its hot
+ * path is an implicit ATen op reached through torch.nn.  Each entry point below names the
+ * reference call site(s) whose ATen kernel it replaces.
+ *
+ * Conventions:
+ *  - Activations are NHWC ("channels_last"), dtype RTSDS_F32 or RTSDS_BF16; weights are
+ *    [Cout][KH][KW][Cin] in the same dtype; statistics, biases, losses and optimizer state
+ *    are fp32.
+ *  - Pointers are device pointers owned by the caller (PyTorch caching allocator).  The
+ *    library never allocates or frees; scratch comes in as (ws, ws_bytes).
+ *  - `stream` is a hipStream_t passed as void*.  Every call is stream-ordered, stateless,
+ *    re-entrant and performs no host synchronisation (graph-capture safe).
+ *  - Return value: RTSDS_OK or one of the RTSDS_ERR_* codes; the Python layer raises.
+ */
+#ifndef RTSDS_HIP_H
+#define RTSDS_HIP_H
+#include <stddef.h>
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum { RTSDS_F32 = 0, RTSDS_BF16 = 1 };
+enum {
+  RTSDS_OK = 0,
+  RTSDS_ERR_SHAPE = 1,        /* inconsistent / out-of-range shape */
+  RTSDS_ERR_UNSUPPORTED = 2,  /* configuration the kernels do not implement */
+  RTSDS_ERR_LAUNCH = 3,       /* HIP launch failure */
+  RTSDS_ERR_WORKSPACE = 4     /* ws_bytes smaller than the *_workspace() query */
+};
+enum { RTSDS_ACT_NONE = 0, RTSDS_ACT_RELU = 1, RTSDS_ACT_LEAKY = 2, RTSDS_ACT_SIGMOID = 3 };
+#define RTSDS_ACCUMULATE 0x100 /* conv fwd flag: y += conv(...) (ASPP sum, deeplabv2.py:62-66) */
+
+typedef struct {
+  int n, h, w, c;   /* input  [n][h][w][c]                                     */
+  int ho, wo, k;    /* output [n][ho][wo][k]                                   */
+  int kh, kw;       /* filter size                                             */
+  int sh, sw;       /* stride                                                  */
+  int ph, pw;       /* zero padding                                            */
+  int dh, dw;       /* dilation                                                */
+  int dtype;        /* RTSDS_F32 / RTSDS_BF16 for x, w, y                      */
+} rtsds_conv_desc;
+
+/* ---------------------------------------------------------------- convolution
+ * Replaces nn.Conv2d (ATen convolution fwd / grad_input / grad_weight) at
+ * build_bisenet.py:11-12,38,65,67,99-100,109-110,117; torchvision ResNet convs reached via
+ * build_contextpath.py:19-24; deeplabv2.py:13,19,24,56,73,99; model.py:54-58,69-70.
+ * Implicit GEMM on MFMA (bf16: v_mfma_f32_16x16x32_bf16, f32: v_mfma_f32_16x16x4_f32).  */
+
+/* y = act(conv(x, w) + bias [+ y if act & RTSDS_ACCUMULATE]).  bias may be NULL (fp32 [k]). */
+int rtsds_conv2d_fwd(const rtsds_conv_desc* d, const void* x, const void* w, const float* bias,
+                     void* y, int act, void* stream);
+/* dx (+)= conv_transpose(dy, w) (accumulate != 0: dx += ...).  Needs ws >=
+ * rtsds_conv2d_dgrad_workspace(d).  Strides 1 and 2 only.                               */
+size_t rtsds_conv2d_dgrad_workspace(const rtsds_conv_desc* d);
+int rtsds_conv2d_dgrad(const rtsds_conv_desc* d, const void* dy, const void* w, void* dx,
+                       int accumulate, void* ws, size_t ws_bytes, void* stream);
+/* dw (fp32 [k][kh][kw][c], overwritten) = sum_pixels dy (x) patch(x);
+ * dbias (fp32 [k], overwritten, may be NULL) = sum_pixels dy.                            */
+size_t rtsds_conv2d_wgrad_workspace(const rtsds_conv_desc* d);
+int rtsds_conv2d_wgrad(const rtsds_conv_desc* d, const void* x, const void* dy, float* dw,
+                       float* dbias, void* ws, size_t ws_bytes, void* stream);
+
+/* ---------------------------------------------------------------- batch norm (train/eval)
+ * Replaces nn.BatchNorm2d at build_bisenet.py:13,39; torchvision ResNet bn*; deeplabv2.py:14-27,
+ * 75,101 (frozen affine, train-mode batch statistics).  x, y, res, dy, dx: NHWC [rows][c]
+ * with rows = n*h*w.
+ * Forward (training): mean/invstd of the batch are written to save_mean / save_invstd and
+ * the running buffers are updated in place with the unbiased variance, momentum m
+ * (PyTorch semantics).  Forward (eval): running stats are used, save_* untouched.
+ * y = act(gamma * (x - mean) * invstd + beta [+ res]).  gamma/beta may be NULL (1 / 0).   */
+size_t rtsds_bn_workspace(long rows, int c);
+int rtsds_bn_fwd(const void* x, const void* res, void* y, long rows, int c, const float* gamma,
+                 const float* beta, float* running_mean, float* running_var, float* save_mean,
+                 float* save_invstd, float momentum, float eps, int training, int act, int dtype,
+                 void* ws, size_t ws_bytes, void* stream);
+/* Backward of the fused BN(+res)(+act) above, given y (post-activation output) for the
+ * activation mask.  dx, dres (may be NULL), dgamma/dbeta (fp32, overwritten, may be NULL).
+ * training=0 gives the eval-mode backward (constant statistics).                         */
+int rtsds_bn_bwd(const void* dy, const void* x, const void* y, void* dx, void* dres,
+                 float* dgamma, float* dbeta, long rows, int c, const float* gamma,
+                 const float* save_mean, const float* save_invstd, int training, int act,
+                 int dtype, void* ws, size_t ws_bytes, void* stream);
+
+/* ---------------------------------------------------------------- layout / dtype
+ * Input images arrive NCHW fp32 from the reference's loaders (datasets/cityscapes.py:62,
+ * main.py:69-72).  cast: weight shadows (fp32 master -> bf16) and dtype round trips.
+ * copy_channels: torch.cat along channels and its backward split (build_bisenet.py:72,153). */
+int rtsds_nchw_to_nhwc(const float* x, void* y, int n, int c, int h, int w, int dtype, void* stream);
+int rtsds_cast(const void* src, int src_dtype, void* dst, int dst_dtype, long n, void* stream);
+int rtsds_copy_channels(const void* src, int src_ld, int src_off, void* dst, int dst_ld, int dst_off,
+                        long rows, int cnt, int dtype, void* stream);
+
+/* ---------------------------------------------------------------- pointwise activations
+ * act 1 ReLU (build_bisenet.py:77), 2 LeakyReLU(0.2) (model.py:62,73), 3 sigmoid
+ * (build_bisenet.py:49,78).  Backward from the forward output y; act 0 = dx = alpha*dy
+ * (GradientReversalFunction, model.py:9-17).                                              */
+int rtsds_act_fwd(const void* x, void* y, long n, int act, int dtype, void* stream);
+int rtsds_act_bwd(const void* dy, const void* y, void* dx, long n, int act, float alpha, int dtype,
+                  void* stream);
+
+/* ---------------------------------------------------------------- pooling
+ * MaxPool2d (build_contextpath.py:21 via torchvision; deeplabv2.py:79 ceil_mode -- the
+ * caller sizes ho/wo).  idx: uint8 tap index per output, consumed by the backward.       */
+int rtsds_maxpool_fwd(const void* x, void* y, uint8_t* idx, int n, int h, int w, int c, int ho,
+                      int wo, int k, int s, int p, int dtype, void* stream);
+int rtsds_maxpool_bwd(const void* dy, const uint8_t* idx, void* dx, int n, int h, int w, int c,
+                      int ho, int wo, int k, int s, int p, int dtype, void* stream);
+/* Global average pool over H*W (build_bisenet.py:46,75; build_contextpath.py:27-28;
+ * model.py:63,82).  y: [n][c].                                                            */
+int rtsds_gap_fwd(const void* x, void* y, int n, long hw, int c, int dtype, void* stream);
+int rtsds_gap_bwd(const void* dy, void* dx, int n, long hw, int c, int dtype, void* stream);
+
+/* ---------------------------------------------------------------- channel attention
+ * mode 0: y = x*a[n][c] (build_bisenet.py:52,149); mode 1: y = x*a + x (build_bisenet.py:79-80).
+ * Backward: dx (may be NULL), da[n][c] = sum_hw dy*x (may be NULL).                       */
+int rtsds_chscale_fwd(const void* x, const void* a, void* y, int n, long hw, int c, int mode,
+                      int dtype, void* stream);
+int rtsds_chscale_bwd(const void* dy, const void* x, const void* a, void* dx, void* da, int n,
+                      long hw, int c, int mode, int dtype, void* stream);
+
+/* ---------------------------------------------------------------- bilinear resize
+ * F.interpolate(mode='bilinear', align_corners=False) (build_bisenet.py:151-152,158-159,166;
+ * deeplabv2.py:126; model.py:23).  scale = in/out (size=) or 1/scale_factor, in fp32 as
+ * ATen computes it.  The output (forward) / incoming grad (backward) may be a channel slice
+ * of a wider NHWC tensor: pixel pitch *_ld (0 = c), channel offset *_off.               */
+int rtsds_bilinear_fwd(const void* x, void* y, int n, int hi, int wi, int c, int ho, int wo,
+                       float scale_h, float scale_w, int y_ld, int y_off, int dtype, void* stream);
+int rtsds_bilinear_bwd(const void* dy, void* dx, int n, int hi, int wi, int c, int ho, int wo,
+                       float scale_h, float scale_w, int dy_ld, int dy_off, int dtype, void* stream);
+
+/* ---------------------------------------------------------------- softmax / losses
+ * Logits addressed by element strides (sn, sc, shw) per (image, channel, pixel): NHWC and
+ * NCHW both work.  Softmax over channels (train.py:225,245,256) writes NHWC with pitch
+ * y_ld >= c (extra channels zeroed).                                                      */
+int rtsds_softmax_fwd(const void* x, long sn, long sc, long shw, void* y, int y_ld, int n, long hw,
+                      int c, int dtype, void* stream);
+int rtsds_softmax_bwd(const void* dy, const void* y, int ld, void* dx, long sn, long sc, long shw,
+                      int n, long hw, int c, int dtype, void* stream);
+/* nn.CrossEntropyLoss(ignore_index) mean over valid pixels (main.py:124-130).  The forward
+ * leaves the valid count at ((float*)ws)[2048]; pass that pointer as `count` to the bwd.  */
+size_t rtsds_ce_workspace(void);
+int rtsds_ce_fwd(const void* x, long sn, long sc, long shw, const int64_t* target, float* loss, int n,
+                 long hw, int c, int ignore_index, int dtype, void* ws, size_t ws_bytes, void* stream);
+int rtsds_ce_bwd(const void* x, long sn, long sc, long shw, const int64_t* target,
+                 const float* grad_loss, const float* count, void* dx, int n, long hw, int c,
+                 int ignore_index, int dtype, void* stream);
+/* nn.BCEWithLogitsLoss() mean (main.py:131-132), fp32.                                  */
+int rtsds_bce_fwd(const float* x, const float* target, float* loss, int n, void* stream);
+int rtsds_bce_bwd(const float* x, const float* target, const float* grad_loss, float* dx, int n,
+                  void* stream);
+
+/* ---------------------------------------------------------------- optimizer
+ * torch.optim.Adam step (main.py:116-117) over flat fp32 arenas; grad is multiplied by
+ * grad_scale first (data-parallel 1/world).  bf16_shadow (may be NULL) receives bf16(param). */
+int rtsds_adam_step(float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
+                    void* bf16_shadow, long n, float lr, float beta1, float beta2, float eps,
+                    float weight_decay, int step, float grad_scale, void* stream);
+
+/* ---------------------------------------------------------------- metrics
+ * argmax over channels, first maximum wins (train.py:102-106,272-275; validation.py:51).
+ * out (int64 [n*hw]) may be NULL; if target and correct are given, *correct += #matches.
+ * confusion: hist[nc*nc] += bincount(nc*label + pred) for 0 <= label < nc (utils.py:52-58). */
+int rtsds_argmax(const void* x, long sn, long sc, long shw, int64_t* out, const int64_t* target,
+                 unsigned long long* correct, int n, long hw, int c, int dtype, void* stream);
+int rtsds_confusion(const int64_t* label, const int64_t* pred, unsigned long long* hist, long total,
+                    int nc, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RTSDS_HIP_H */

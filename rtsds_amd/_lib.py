@@ -1,0 +1,103 @@
+"""ctypes binding of librtsds_hip.so (the C ABI declared in include/rtsds_hip.h).
+
+The HIP library is the only compute path: if it is missing, cannot be loaded, or no HIP
+device is present, every op raises -- there is no CPU / eager-PyTorch fallback.
+``torch`` is imported first so that the process-wide HIP runtime is torch's own
+``libamdhip64.so.7`` (same SONAME as the one the library links against).
+"""
+import ctypes
+import os
+
+import torch  # noqa: F401  (must precede the dlopen below)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "librtsds_hip.so")
+
+F32, BF16 = 0, 1
+ACT_NONE, ACT_RELU, ACT_LEAKY = 0, 1, 2
+ACCUMULATE = 0x100
+ERRORS = {1: "bad shape", 2: "unsupported configuration", 3: "HIP launch failure", 4: "workspace too small"}
+
+c_int, c_long, c_float, c_size_t, c_void_p = (ctypes.c_int, ctypes.c_long, ctypes.c_float,
+                                              ctypes.c_size_t, ctypes.c_void_p)
+
+
+class ConvDesc(ctypes.Structure):
+    _fields_ = [(n, c_int) for n in ("n", "h", "w", "c", "ho", "wo", "k", "kh", "kw", "sh", "sw",
+                                     "ph", "pw", "dh", "dw", "dtype")]
+
+
+P = c_void_p
+# name -> (restype, argtypes)
+SIGNATURES = {
+    "rtsds_conv2d_fwd": (c_int, [ctypes.POINTER(ConvDesc), P, P, P, P, c_int, P]),
+    "rtsds_conv2d_dgrad_workspace": (c_size_t, [ctypes.POINTER(ConvDesc)]),
+    "rtsds_conv2d_dgrad": (c_int, [ctypes.POINTER(ConvDesc), P, P, P, c_int, P, c_size_t, P]),
+    "rtsds_conv2d_wgrad_workspace": (c_size_t, [ctypes.POINTER(ConvDesc)]),
+    "rtsds_conv2d_wgrad": (c_int, [ctypes.POINTER(ConvDesc), P, P, P, P, P, c_size_t, P]),
+    "rtsds_bn_workspace": (c_size_t, [c_long, c_int]),
+    "rtsds_bn_fwd": (c_int, [P, P, P, c_long, c_int, P, P, P, P, P, P, c_float, c_float, c_int,
+                             c_int, c_int, P, c_size_t, P]),
+    "rtsds_bn_bwd": (c_int, [P, P, P, P, P, P, P, c_long, c_int, P, P, P, c_int, c_int, c_int, P,
+                             c_size_t, P]),
+    "rtsds_nchw_to_nhwc": (c_int, [P, P, c_int, c_int, c_int, c_int, c_int, P]),
+    "rtsds_cast": (c_int, [P, c_int, P, c_int, c_long, P]),
+    "rtsds_copy_channels": (c_int, [P, c_int, c_int, P, c_int, c_int, c_long, c_int, c_int, P]),
+    "rtsds_act_fwd": (c_int, [P, P, c_long, c_int, c_int, P]),
+    "rtsds_act_bwd": (c_int, [P, P, P, c_long, c_int, c_float, c_int, P]),
+    "rtsds_maxpool_fwd": (c_int, [P, P, P] + [c_int] * 10 + [P]),
+    "rtsds_maxpool_bwd": (c_int, [P, P, P] + [c_int] * 10 + [P]),
+    "rtsds_gap_fwd": (c_int, [P, P, c_int, c_long, c_int, c_int, P]),
+    "rtsds_gap_bwd": (c_int, [P, P, c_int, c_long, c_int, c_int, P]),
+    "rtsds_chscale_fwd": (c_int, [P, P, P, c_int, c_long, c_int, c_int, c_int, P]),
+    "rtsds_chscale_bwd": (c_int, [P, P, P, P, P, c_int, c_long, c_int, c_int, c_int, P]),
+    "rtsds_bilinear_fwd": (c_int, [P, P] + [c_int] * 6 + [c_float, c_float, c_int, c_int, c_int, P]),
+    "rtsds_bilinear_bwd": (c_int, [P, P] + [c_int] * 6 + [c_float, c_float, c_int, c_int, c_int, P]),
+    "rtsds_softmax_fwd": (c_int, [P, c_long, c_long, c_long, P, c_int, c_int, c_long, c_int, c_int, P]),
+    "rtsds_softmax_bwd": (c_int, [P, P, c_int, P, c_long, c_long, c_long, c_int, c_long, c_int, c_int,
+                                  P]),
+    "rtsds_ce_workspace": (c_size_t, []),
+    "rtsds_ce_fwd": (c_int, [P, c_long, c_long, c_long, P, P, c_int, c_long, c_int, c_int, c_int, P,
+                             c_size_t, P]),
+    "rtsds_ce_bwd": (c_int, [P, c_long, c_long, c_long, P, P, P, P, c_int, c_long, c_int, c_int, c_int,
+                             P]),
+    "rtsds_bce_fwd": (c_int, [P, P, P, c_int, P]),
+    "rtsds_bce_bwd": (c_int, [P, P, P, P, c_int, P]),
+    "rtsds_adam_step": (c_int, [P, P, P, P, P, c_long, c_float, c_float, c_float, c_float, c_float,
+                                c_int, c_float, P]),
+    "rtsds_argmax": (c_int, [P, c_long, c_long, c_long, P, P, P, c_int, c_long, c_int, c_int, P]),
+    "rtsds_confusion": (c_int, [P, P, P, c_long, c_int, P]),
+}
+
+_lib = None
+
+
+def load(path=LIB_PATH):
+    """dlopen the library and attach signatures (no GPU needed).  Raises if absent."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(path):
+            raise RuntimeError(f"rtsds_amd: HIP library not built ({path}); run __graft_entry__.build()")
+        lib = ctypes.CDLL(path)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype, fn.argtypes = res, args
+        _lib = lib
+    return _lib
+
+
+class _Lib:
+    def __getattr__(self, name):
+        fn = getattr(load(), name)
+
+        def call(*args):
+            rc = fn(*args)
+            if name.endswith("_workspace"):
+                return rc
+            if rc != 0:
+                raise RuntimeError(f"rtsds_amd: {name} failed: {ERRORS.get(rc, rc)}")
+            return rc
+        return call
+
+
+lib = _Lib()

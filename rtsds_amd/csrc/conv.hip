@@ -1,0 +1,677 @@
+// Implicit-GEMM convolution (forward, data-grad, weight-grad) for gfx950 / CDNA4.
+//
+// One kernel template serves the three GEMMs of nn.Conv2d training:
+//   FWD   C[m = (n,oh,ow)][co]          = sum_{k=(r,s,ci)} X[n, oh*s-p+r*d, ...][ci] * W[co][r][s][ci]
+//   DGRAD C[m = (n,ih,iw)][ci]          = sum_{k=(r,s,co)} dY[n, (ih+p-r*d)/s, ...][co] * W[co][r][s][ci]
+//   WGRAD C[co][(r,s,ci)]               = sum_{pixels q} dY[q][co] * X[patch(q, r, s)][ci]
+// NHWC activations make the FWD/DGRAD reduction axis (ci / co) contiguous in memory, so those
+// tiles are staged "k-contiguous" (KC) and read with ds_read_b128 fragments.  WGRAD reduces
+// over pixels, which are strided in NHWC: its tiles are staged pixel-major (RC, one row per
+// pixel, channels contiguous -> coalesced 16-B global loads) and the MFMA fragments are
+// read transposed with gfx950's ds_read_b64_tr_b16 (bf16) or plain b32 reads (f32).
+//
+// Tile: BM x BN x BK per 256-thread workgroup (4 waves, WM x WN), register-staged double
+// buffer, one barrier per K-step.  bf16 uses v_mfma_f32_16x16x32_bf16, f32 (parity mode)
+// v_mfma_f32_16x16x4_f32 (exact f32 FMA chain).
+#include "common.h"
+#include <algorithm>
+
+enum { MODE_FWD = 0, MODE_DGRAD = 1, MODE_WGRAD = 2 };
+
+struct ConvArgs {
+  const void* a;      // FWD: x   DGRAD: dy  WGRAD: dy
+  const void* b;      // FWD: w   DGRAD: w^T (repacked [ci][r][s][co])  WGRAD: x
+  const float* bias;  // FWD only
+  void* out;          // FWD: y (T)  DGRAD: dx (T)  WGRAD: fp32 partials [split][M][N]
+  int M, N, K;        // GEMM extents; K = reduction length
+  int n, h, w, c, ho, wo, k, kh, kw, sh, sw, ph, pw, dh, dw;
+  FastDiv f_howo, f_wo, f_hw, f_w, f_c, f_k, f_kw;
+  int tiles_per_split;
+  int act;
+  int accum;          // FWD/DGRAD: y += result
+  long split_stride;  // elements between WGRAD split slabs
+};
+
+template <typename T> struct Mma;
+template <> struct Mma<bf16> {
+  static constexpr int KS = 32;
+  typedef bf16x8 frag;
+  RT_DEV static f32x4 run(frag a, frag b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+  }
+};
+template <> struct Mma<float> {
+  static constexpr int KS = 4;
+  typedef float frag;
+  RT_DEV static f32x4 run(frag a, frag b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+  }
+};
+
+// LDS pitches (elements).  KC: [rows][BK+pad]; bf16 pad 8 -> 80-B rows (16 consecutive rows
+// hit 16 distinct 16-B slots); f32 pad 1.  RC: [BK][cols+16]: bf16 rows are 32 B mod 256 apart
+// so a half-wave's 8 tr-read rows cover all 64 banks; f32 rows are 16 dwords mod 32 apart.
+template <typename T, int BK> struct KCPitch { static constexpr int v = BK + (sizeof(T) == 2 ? 8 : 1); };
+template <int COLS> struct RCPitch { static constexpr int v = COLS + 16; };
+
+// ---- fragment reads --------------------------------------------------------------
+// KC: lane l holds row (l&15), k-chunk (l>>4) of a 16-row block.
+RT_DEV bf16x8 frag_kc(const bf16* s, int pitch, int row0, int ks, int lane) {
+  return *(const bf16x8*)(s + (row0 + (lane & 15)) * pitch + ks * 32 + 8 * (lane >> 4));
+}
+RT_DEV float frag_kc(const float* s, int pitch, int row0, int ks, int lane) {
+  return s[(row0 + (lane & 15)) * pitch + ks * 4 + (lane >> 4)];
+}
+// RC: tile stored [k][col].  bf16 via two ds_read_b64_tr_b16: lane 16g+4q+p addresses row
+// (base + 4g + q), columns 4p..4p+3; it receives column (l&15) of those 4 rows.  Fragment
+// element j <-> k row  4g+j (j<4)  /  16+4g+(j-4) (j>=4): a permutation of k shared by both
+// operands, which the MFMA's k-sum does not see.
+RT_DEV bf16x8 frag_rc(const bf16* s, int pitch, int col0, int ks, int lane) {
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  const bf16* p0 = s + (ks * 32 + 4 * g + q) * pitch + col0 + 4 * p;
+  const bf16* p1 = p0 + 16 * pitch;
+  s16x4 t0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)p0);
+  s16x4 t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)p1);
+  typedef __attribute__((ext_vector_type(8))) short s16x8;
+  s16x8 r = {t0[0], t0[1], t0[2], t0[3], t1[0], t1[1], t1[2], t1[3]};
+  return __builtin_bit_cast(bf16x8, r);
+}
+RT_DEV float frag_rc(const float* s, int pitch, int col0, int ks, int lane) {
+  return s[(ks * 4 + (lane >> 4)) * pitch + col0 + (lane & 15)];
+}
+
+template <typename T> RT_DEV typename VecT<T>::v16 vzero() {
+  typename VecT<T>::v16 z;
+#pragma unroll
+  for (int j = 0; j < VecT<T>::N; ++j) z[j] = (T)0.0f;
+  return z;
+}
+
+// ---- main kernel -------------------------------------------------------------------
+// ALA / ALB: alignment class of the A / B gathers.
+//   KC A: 2 = channel count % BK == 0 (one filter tap per K-tile), 1 = % V == 0 (16-B chunks
+//         never straddle a tap), 0 = scalar gather.
+//   KC B: 1 = K % V == 0 (vector rows), 0 = scalar.
+//   RC A/B: 1 = channel count % V == 0, 0 = scalar.
+template <typename T, int MODE, int BM, int BN, int BK, int WM, int WN, int ALA, int ALB>
+__global__ void __launch_bounds__(256) conv_gemm_kernel(const ConvArgs P) {
+  typedef typename VecT<T>::v16 V16;
+  constexpr int V = VecT<T>::N;
+  constexpr bool RC = (MODE == MODE_WGRAD);
+  constexpr int KCP = KCPitch<T, BK>::v;
+  constexpr int PA = RC ? RCPitch<BM>::v : KCP;
+  constexpr int PB = RC ? RCPitch<BN>::v : KCP;
+  constexpr int A_EL = RC ? BK * PA : BM * PA;
+  constexpr int B_EL = RC ? BK * PB : BN * PB;
+  constexpr int CA = BM * BK / V, CB = BN * BK / V;      // 16-B chunks per tile
+  constexpr int NA = (CA + 255) / 256, NB = (CB + 255) / 256;
+  constexpr int WTM = BM / WM, WTN = BN / WN, FM = WTM / 16, FN = WTN / 16;
+  constexpr int KS = Mma<T>::KS;
+  static_assert(WM * WN == 4, "4 waves");
+  static_assert(BK % KS == 0, "BK");
+  static_assert(!RC || BK == (sizeof(T) == 2 ? 32 : 16), "RC BK");
+
+  __shared__ __attribute__((aligned(16))) T smem[2 * (A_EL + B_EL)];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm0 = (wave / WN) * WTM, wn0 = (wave % WN) * WTN;
+  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  const T* __restrict__ ga = (const T*)P.a;
+  const T* __restrict__ gb = (const T*)P.b;
+
+  const int nk_total = (P.K + BK - 1) / BK;
+  const int kt0 = blockIdx.z * P.tiles_per_split;
+  const int kt1 = min(nk_total, kt0 + P.tiles_per_split);
+
+  // ---- per-thread invariant gather state
+  // KC-A rows (FWD / DGRAD): image base offset + spatial anchor of each staged row.
+  long a_off[NA];
+  int a_h[NA], a_w[NA];
+  bool a_ok[NA];
+  // RC-B column (WGRAD): fixed (tap, ci) for this thread's 16-B chunk.
+  int b_r = 0, b_s = 0, b_ci = 0;
+  bool b_colok = false;
+
+  if (!RC) {
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+      const int id = tid + 256 * i;
+      const int row = id / (BK / V);
+      const int m = m0 + row;
+      a_ok[i] = (id < CA) && (m < P.M);
+      const int mm = a_ok[i] ? m : 0;
+      if (MODE == MODE_FWD) {
+        const int img = fdiv(mm, P.f_howo), rem = mm - img * P.ho * P.wo;
+        const int oh = fdiv(rem, P.f_wo), ow = rem - oh * P.wo;
+        a_off[i] = (long)img * P.h * P.w * P.c;
+        a_h[i] = oh * P.sh - P.ph;
+        a_w[i] = ow * P.sw - P.pw;
+      } else {
+        const int img = fdiv(mm, P.f_hw), rem = mm - img * P.h * P.w;
+        const int ih = fdiv(rem, P.f_w), iw = rem - ih * P.w;
+        a_off[i] = (long)img * P.ho * P.wo * P.k;
+        a_h[i] = ih + P.ph;
+        a_w[i] = iw + P.pw;
+      }
+    }
+  } else {
+    const int cc = tid % (BN / V);
+    const int nn = n0 + cc * V;
+    b_colok = nn < P.N;
+    if (ALB == 1 && b_colok) {
+      const int tap = fdiv(nn, P.f_c);
+      b_ci = nn - tap * P.c;
+      b_r = fdiv(tap, P.f_kw);
+      b_s = tap - b_r * P.kw;
+    }
+  }
+
+  V16 ra[NA], rb[NB];
+
+  // ---- global -> register stage of K-tile kt
+  auto load_tile = [&](int kt) {
+    const int k0 = kt * BK;
+    if (!RC) {
+      // ---- A (KC gather)
+      const int Cr = (MODE == MODE_FWD) ? P.c : P.k;  // channels along the reduction
+      int tap_u = 0, r_u = 0, s_u = 0, ci_u = 0;
+      if (ALA == 2) {
+        tap_u = k0 / Cr;
+        ci_u = k0 - tap_u * Cr;
+        r_u = tap_u / P.kw;
+        s_u = tap_u - r_u * P.kw;
+      }
+#pragma unroll
+      for (int i = 0; i < NA; ++i) {
+        const int id = tid + 256 * i;
+        const int kc = id % (BK / V);
+        V16 v = vzero<T>();
+        if (ALA >= 1) {
+          int r, s, ci;
+          bool okk = true;
+          if (ALA == 2) {
+            r = r_u; s = s_u; ci = ci_u + kc * V;
+          } else {
+            const int kk = k0 + kc * V;
+            okk = kk < P.K;
+            const int tap = fdiv(kk, MODE == MODE_FWD ? P.f_c : P.f_k);
+            ci = kk - tap * Cr;
+            r = fdiv(tap, P.f_kw);
+            s = tap - r * P.kw;
+          }
+          int hh, ww;
+          bool ok = a_ok[i] && okk;
+          if (MODE == MODE_FWD) {
+            hh = a_h[i] + r * P.dh;
+            ww = a_w[i] + s * P.dw;
+            ok = ok && (unsigned)hh < (unsigned)P.h && (unsigned)ww < (unsigned)P.w;
+            if (ok) v = *(const V16*)(ga + a_off[i] + ((long)hh * P.w + ww) * P.c + ci);
+          } else {
+            int hn = a_h[i] - r * P.dh, wn = a_w[i] - s * P.dw;
+            if (P.sh == 2) { ok = ok && !(hn & 1); hn >>= 1; }
+            if (P.sw == 2) { ok = ok && !(wn & 1); wn >>= 1; }
+            ok = ok && (unsigned)hn < (unsigned)P.ho && (unsigned)wn < (unsigned)P.wo;
+            if (ok) v = *(const V16*)(ga + a_off[i] + ((long)hn * P.wo + wn) * P.k + ci);
+          }
+        } else {
+#pragma unroll
+          for (int j = 0; j < V; ++j) {
+            const int kk = k0 + kc * V + j;
+            if (!a_ok[i] || kk >= P.K) continue;
+            const int tap = kk / Cr;
+            const int ci = kk - tap * Cr;
+            const int r = tap / P.kw, s = tap - r * P.kw;
+            if (MODE == MODE_FWD) {
+              const int hh = a_h[i] + r * P.dh, ww = a_w[i] + s * P.dw;
+              if ((unsigned)hh < (unsigned)P.h && (unsigned)ww < (unsigned)P.w)
+                v[j] = ga[a_off[i] + ((long)hh * P.w + ww) * P.c + ci];
+            } else {
+              int hn = a_h[i] - r * P.dh, wn = a_w[i] - s * P.dw;
+              bool ok = true;
+              if (P.sh == 2) { ok = !(hn & 1); hn >>= 1; }
+              if (P.sw == 2) { ok = ok && !(wn & 1); wn >>= 1; }
+              if (ok && (unsigned)hn < (unsigned)P.ho && (unsigned)wn < (unsigned)P.wo)
+                v[j] = ga[a_off[i] + ((long)hn * P.wo + wn) * P.k + ci];
+            }
+          }
+        }
+        ra[i] = v;
+      }
+      // ---- B (KC rows of the [N][K] weight matrix)
+#pragma unroll
+      for (int i = 0; i < NB; ++i) {
+        const int id = tid + 256 * i;
+        const int row = id / (BK / V), kc = id % (BK / V);
+        const int nrow = n0 + row, kk = k0 + kc * V;
+        V16 v = vzero<T>();
+        if (id < CB && nrow < P.N) {
+          const T* src = gb + (long)nrow * P.K + kk;
+          if (ALB == 1) {
+            if (kk < P.K) v = *(const V16*)src;
+          } else {
+#pragma unroll
+            for (int j = 0; j < V; ++j)
+              if (kk + j < P.K) v[j] = src[j];
+          }
+        }
+        rb[i] = v;
+      }
+    } else {
+      // ---- WGRAD A: dY rows (pixels) x Cout columns
+#pragma unroll
+      for (int i = 0; i < NA; ++i) {
+        const int id = tid + 256 * i;
+        const int kk = id / (BM / V), cc = id % (BM / V);
+        const int q = k0 + kk, co = m0 + cc * V;
+        V16 v = vzero<T>();
+        if (id < CA && q < P.K) {
+          const T* src = ga + (long)q * P.k + co;
+          if (ALA == 1) {
+            if (co < P.M) v = *(const V16*)src;
+          } else {
+#pragma unroll
+            for (int j = 0; j < V; ++j)
+              if (co + j < P.M) v[j] = src[j];
+          }
+        }
+        ra[i] = v;
+      }
+      // ---- WGRAD B: input patches, rows = output pixels, columns = (r, s, ci)
+#pragma unroll
+      for (int i = 0; i < NB; ++i) {
+        const int id = tid + 256 * i;
+        const int kk = id / (BN / V), cc = id % (BN / V);
+        const int q = k0 + kk;
+        V16 v = vzero<T>();
+        if (id < CB && q < P.K) {
+          const int img = fdiv(q, P.f_howo), rem = q - img * P.ho * P.wo;
+          const int oh = fdiv(rem, P.f_wo), ow = rem - oh * P.wo;
+          const long base = (long)img * P.h * P.w * P.c;
+          const int hb = oh * P.sh - P.ph, wb = ow * P.sw - P.pw;
+          if (ALB == 1) {
+            const int hh = hb + b_r * P.dh, ww = wb + b_s * P.dw;
+            if (b_colok && (unsigned)hh < (unsigned)P.h && (unsigned)ww < (unsigned)P.w)
+              v = *(const V16*)(gb + base + ((long)hh * P.w + ww) * P.c + b_ci);
+          } else {
+#pragma unroll
+            for (int j = 0; j < V; ++j) {
+              const int nn = n0 + cc * V + j;
+              if (nn >= P.N) continue;
+              const int tap = nn / P.c, ci = nn - tap * P.c;
+              const int r = tap / P.kw, s = tap - r * P.kw;
+              const int hh = hb + r * P.dh, ww = wb + s * P.dw;
+              if ((unsigned)hh < (unsigned)P.h && (unsigned)ww < (unsigned)P.w)
+                v[j] = gb[base + ((long)hh * P.w + ww) * P.c + ci];
+            }
+          }
+        }
+        rb[i] = v;
+      }
+    }
+  };
+
+  // ---- register -> LDS stage
+  auto store_tile = [&](int buf) {
+    T* sa = smem + buf * (A_EL + B_EL);
+    T* sb = sa + A_EL;
+    if (!RC) {
+#pragma unroll
+      for (int i = 0; i < NA; ++i) {
+        const int id = tid + 256 * i;
+        if (id >= CA) break;
+        const int row = id / (BK / V), kc = id % (BK / V);
+        T* dst = sa + row * PA + kc * V;
+        if (sizeof(T) == 2) *(V16*)dst = ra[i];
+        else {
+#pragma unroll
+          for (int j = 0; j < V; ++j) dst[j] = ra[i][j];
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < NB; ++i) {
+        const int id = tid + 256 * i;
+        if (id >= CB) break;
+        const int row = id / (BK / V), kc = id % (BK / V);
+        T* dst = sb + row * PB + kc * V;
+        if (sizeof(T) == 2) *(V16*)dst = rb[i];
+        else {
+#pragma unroll
+          for (int j = 0; j < V; ++j) dst[j] = rb[i][j];
+        }
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < NA; ++i) {
+        const int id = tid + 256 * i;
+        if (id >= CA) break;
+        const int kk = id / (BM / V), cc = id % (BM / V);
+        *(V16*)(sa + kk * PA + cc * V) = ra[i];
+      }
+#pragma unroll
+      for (int i = 0; i < NB; ++i) {
+        const int id = tid + 256 * i;
+        if (id >= CB) break;
+        const int kk = id / (BN / V), cc = id % (BN / V);
+        *(V16*)(sb + kk * PB + cc * V) = rb[i];
+      }
+    }
+  };
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (kt0 < kt1) {
+    load_tile(kt0);
+    store_tile(0);
+    __syncthreads();
+    for (int kt = kt0; kt < kt1; ++kt) {
+      const int buf = (kt - kt0) & 1;
+      const bool more = kt + 1 < kt1;
+      if (more) load_tile(kt + 1);
+      const T* sa = smem + buf * (A_EL + B_EL);
+      const T* sb = sa + A_EL;
+#pragma unroll
+      for (int ks = 0; ks < BK / KS; ++ks) {
+        typename Mma<T>::frag fa[FM], fb[FN];
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+          fa[i] = RC ? frag_rc(sa, PA, wm0 + i * 16, ks, lane) : frag_kc(sa, PA, wm0 + i * 16, ks, lane);
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          fb[j] = RC ? frag_rc(sb, PB, wn0 + j * 16, ks, lane) : frag_kc(sb, PB, wn0 + j * 16, ks, lane);
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j) acc[i][j] = Mma<T>::run(fa[i], fb[j], acc[i][j]);
+      }
+      if (more) store_tile(buf ^ 1);
+      __syncthreads();
+    }
+  }
+
+  // ---- epilogue: C[row][col], row = (lane>>4)*4 + e, col = lane&15 within each 16x16 block
+  const int er = (lane >> 4) * 4, ec = lane & 15;
+  if (MODE == MODE_WGRAD) {
+    float* out = (float*)P.out + (long)blockIdx.z * P.split_stride;
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int gn = n0 + wn0 + j * 16 + ec;
+        if (gn >= P.N) continue;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int gm = m0 + wm0 + i * 16 + er + e;
+          if (gm < P.M) out[(long)gm * P.N + gn] = acc[i][j][e];
+        }
+      }
+  } else {
+    T* out = (T*)P.out;
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int gn = n0 + wn0 + j * 16 + ec;
+      if (gn >= P.N) continue;
+      const float bv = P.bias ? P.bias[gn] : 0.f;
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int gm = m0 + wm0 + i * 16 + er + e;
+          if (gm >= P.M) continue;
+          float v = acc[i][j][e] + bv;
+          if (P.accum) v += to_f(out[(long)gm * P.N + gn]);
+          if (P.act == RTSDS_ACT_RELU) v = fmaxf(v, 0.f);
+          else if (P.act == RTSDS_ACT_LEAKY) v = v > 0.f ? v : 0.2f * v;
+          else if (P.act == RTSDS_ACT_SIGMOID) v = 1.f / (1.f + expf(-v));
+          out[(long)gm * P.N + gn] = from_f<T>(v);
+        }
+    }
+  }
+}
+
+// ---- small helper kernels -------------------------------------------------------------
+// W[co][r][s][ci] -> Wt[ci][r][s][co]   (DGRAD's B operand)
+template <typename T>
+__global__ void repack_wt_kernel(const T* __restrict__ w, T* __restrict__ wt, int co_n, int taps, int ci_n) {
+  const long total = (long)co_n * taps * ci_n;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int co = (int)(i % co_n);
+    const long rest = i / co_n;
+    const int tap = (int)(rest % taps);
+    const int ci = (int)(rest / taps);
+    wt[i] = w[((long)co * taps + tap) * ci_n + ci];
+  }
+}
+
+// dw[i] = sum_s partial[s][i]
+__global__ void split_reduce_kernel(const float* __restrict__ part, float* __restrict__ out, long n, int splits) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    float s = 0.f;
+    for (int k = 0; k < splits; ++k) s += part[(long)k * n + i];
+    out[i] = s;
+  }
+}
+
+// dbias: two-stage deterministic column sum of dy[rows][c].
+// Stage 1: grid (ceil(c/64), RB); block sums rows blockIdx.y*4+rw (+= 4*RB) -> part[RB][c].
+template <typename T>
+__global__ void colsum_part_kernel(const T* __restrict__ dy, float* __restrict__ part, long rows, int c) {
+  __shared__ float red[4][64];
+  const int cc = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int rw = threadIdx.x >> 6;
+  float s = 0.f;
+  if (cc < c)
+    for (long r = (long)blockIdx.y * 4 + rw; r < rows; r += 4L * gridDim.y) s += to_f(dy[r * c + cc]);
+  red[rw][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (rw == 0 && cc < c)
+    part[(long)blockIdx.y * c + cc] = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+}
+__global__ void colsum_final_kernel(const float* __restrict__ part, float* __restrict__ out, int rb, int c) {
+  const int cc = blockIdx.x * blockDim.x + threadIdx.x;
+  if (cc >= c) return;
+  float s = 0.f;
+  for (int i = 0; i < rb; ++i) s += part[(long)i * c + cc];
+  out[cc] = s;
+}
+static const int kColsumRB = 256;
+
+// ---- host side ---------------------------------------------------------------------------
+static ConvArgs make_args(const rtsds_conv_desc* d) {
+  ConvArgs p = {};
+  p.n = d->n; p.h = d->h; p.w = d->w; p.c = d->c; p.ho = d->ho; p.wo = d->wo; p.k = d->k;
+  p.kh = d->kh; p.kw = d->kw; p.sh = d->sh; p.sw = d->sw; p.ph = d->ph; p.pw = d->pw;
+  p.dh = d->dh; p.dw = d->dw;
+  p.f_howo = fastdiv_make(d->ho * d->wo);
+  p.f_wo = fastdiv_make(d->wo);
+  p.f_hw = fastdiv_make(d->h * d->w);
+  p.f_w = fastdiv_make(d->w);
+  p.f_c = fastdiv_make(d->c);
+  p.f_k = fastdiv_make(d->k);
+  p.f_kw = fastdiv_make(d->kw);
+  p.tiles_per_split = 1 << 30;
+  return p;
+}
+
+static int check_desc(const rtsds_conv_desc* d) {
+  if (d->n <= 0 || d->h <= 0 || d->w <= 0 || d->c <= 0 || d->k <= 0 || d->kh <= 0 || d->kw <= 0 ||
+      d->sh <= 0 || d->sw <= 0 || d->dh <= 0 || d->dw <= 0 || d->ph < 0 || d->pw < 0)
+    return RTSDS_ERR_SHAPE;
+  const int ho = (d->h + 2 * d->ph - d->dh * (d->kh - 1) - 1) / d->sh + 1;
+  const int wo = (d->w + 2 * d->pw - d->dw * (d->kw - 1) - 1) / d->sw + 1;
+  if (ho != d->ho || wo != d->wo || ho <= 0 || wo <= 0) return RTSDS_ERR_SHAPE;
+  if (d->dtype != RTSDS_F32 && d->dtype != RTSDS_BF16) return RTSDS_ERR_UNSUPPORTED;
+  if ((long)d->n * d->h * d->w * d->c >= (1L << 31) || (long)d->n * d->ho * d->wo * d->k >= (1L << 31))
+    return RTSDS_ERR_UNSUPPORTED;
+  return RTSDS_OK;
+}
+
+template <typename T, int MODE, int BM, int BN, int BK, int WM, int WN, int ALA, int ALB>
+static void launch(const ConvArgs& p, int splits, hipStream_t st) {
+  dim3 grid(rt_cdiv(p.M, BM), rt_cdiv(p.N, BN), splits);
+  hipLaunchKernelGGL((conv_gemm_kernel<T, MODE, BM, BN, BK, WM, WN, ALA, ALB>), grid, dim3(256), 0, st, p);
+}
+
+// Tile selection for FWD / DGRAD.  bf16: 128x128 (2x2 waves of 64x64) for wide outputs,
+// 128x64 for 64-channel outputs, 256x32 for the 19/1-channel heads; f32: 64x64 / 128x32.
+template <typename T, int MODE, int ALA, int ALB>
+static void dispatch_mn(const ConvArgs& p, hipStream_t st) {
+  constexpr int BK = sizeof(T) == 2 ? 32 : 16;
+  if (sizeof(T) == 2) {
+    if (p.N <= 32) launch<T, MODE, 256, 32, BK, 4, 1, ALA, ALB>(p, 1, st);
+    else if (p.N <= 64) launch<T, MODE, 128, 64, BK, 2, 2, ALA, ALB>(p, 1, st);
+    else launch<T, MODE, 128, 128, BK, 2, 2, ALA, ALB>(p, 1, st);
+  } else {
+    if (p.N <= 32) launch<T, MODE, 128, 32, BK, 4, 1, ALA, ALB>(p, 1, st);
+    else launch<T, MODE, 64, 64, BK, 2, 2, ALA, ALB>(p, 1, st);
+  }
+}
+
+template <typename T, int MODE>
+static void dispatch_align(const ConvArgs& p, int cr, hipStream_t st) {
+  constexpr int V = VecT<T>::N;
+  constexpr int BK = sizeof(T) == 2 ? 32 : 16;
+  const int alb = (p.K % V == 0) ? 1 : 0;
+  if (cr % BK == 0) {
+    if (alb) dispatch_mn<T, MODE, 2, 1>(p, st); else dispatch_mn<T, MODE, 2, 0>(p, st);
+  } else if (cr % V == 0) {
+    if (alb) dispatch_mn<T, MODE, 1, 1>(p, st); else dispatch_mn<T, MODE, 1, 0>(p, st);
+  } else {
+    if (alb) dispatch_mn<T, MODE, 0, 1>(p, st); else dispatch_mn<T, MODE, 0, 0>(p, st);
+  }
+}
+
+extern "C" int rtsds_conv2d_fwd(const rtsds_conv_desc* d, const void* x, const void* w, const float* bias,
+                                void* y, int act, void* stream) {
+  int e = check_desc(d);
+  if (e) return e;
+  ConvArgs p = make_args(d);
+  p.a = x; p.b = w; p.bias = bias; p.out = y;
+  p.act = act & 0xff;
+  p.accum = (act & RTSDS_ACCUMULATE) ? 1 : 0;
+  p.M = d->n * d->ho * d->wo;
+  p.N = d->k;
+  p.K = d->kh * d->kw * d->c;
+  hipStream_t st = (hipStream_t)stream;
+  if (d->dtype == RTSDS_BF16) dispatch_align<bf16, MODE_FWD>(p, d->c, st);
+  else dispatch_align<float, MODE_FWD>(p, d->c, st);
+  return hipGetLastError() == hipSuccess ? RTSDS_OK : RTSDS_ERR_LAUNCH;
+}
+
+extern "C" size_t rtsds_conv2d_dgrad_workspace(const rtsds_conv_desc* d) {
+  const size_t es = d->dtype == RTSDS_BF16 ? 2 : 4;
+  return ((size_t)d->k * d->kh * d->kw * d->c * es + 255) & ~(size_t)255;
+}
+
+extern "C" int rtsds_conv2d_dgrad(const rtsds_conv_desc* d, const void* dy, const void* w, void* dx,
+                                  int accumulate, void* ws, size_t ws_bytes, void* stream) {
+  int e = check_desc(d);
+  if (e) return e;
+  if (d->sh > 2 || d->sw > 2) return RTSDS_ERR_UNSUPPORTED;
+  if (ws_bytes < rtsds_conv2d_dgrad_workspace(d)) return RTSDS_ERR_WORKSPACE;
+  hipStream_t st = (hipStream_t)stream;
+  const int taps = d->kh * d->kw;
+  const long wn = (long)d->k * taps * d->c;
+  const int blocks = (int)std::min<long>(4096, (wn + 255) / 256);
+  if (d->dtype == RTSDS_BF16)
+    hipLaunchKernelGGL(repack_wt_kernel<bf16>, dim3(blocks), dim3(256), 0, st, (const bf16*)w, (bf16*)ws, d->k, taps, d->c);
+  else
+    hipLaunchKernelGGL(repack_wt_kernel<float>, dim3(blocks), dim3(256), 0, st, (const float*)w, (float*)ws, d->k, taps, d->c);
+  ConvArgs p = make_args(d);
+  p.a = dy; p.b = ws; p.bias = nullptr; p.out = dx; p.act = 0;
+  p.accum = accumulate ? 1 : 0;
+  p.M = d->n * d->h * d->w;
+  p.N = d->c;
+  p.K = taps * d->k;
+  if (d->dtype == RTSDS_BF16) dispatch_align<bf16, MODE_DGRAD>(p, d->k, st);
+  else dispatch_align<float, MODE_DGRAD>(p, d->k, st);
+  return hipGetLastError() == hipSuccess ? RTSDS_OK : RTSDS_ERR_LAUNCH;
+}
+
+// WGRAD split-K: enough (M/BM)*(N/BN)*splits workgroups to fill 256 CUs ~2x, each split at
+// least 8 K-tiles; fp32 partial slabs summed by split_reduce_kernel (deterministic).
+static void wgrad_plan(const rtsds_conv_desc* d, int& bm, int& bn, int& splits, int& tps) {
+  const bool b16 = d->dtype == RTSDS_BF16;
+  const int M = d->k, N = d->kh * d->kw * d->c;
+  const long R = (long)d->n * d->ho * d->wo;
+  const int BK = b16 ? 32 : 16;
+  bm = b16 ? (M <= 64 ? 64 : 128) : 64;
+  bn = b16 ? (N <= 64 ? 64 : 128) : 64;
+  const long tiles = (long)rt_cdiv(M, bm) * rt_cdiv(N, bn);
+  const long nk = (R + BK - 1) / BK;
+  long want = std::max<long>(1, 512 / tiles);
+  want = std::min<long>(want, std::max<long>(1, nk / 8));
+  want = std::min<long>(want, 256);
+  tps = (int)((nk + want - 1) / want);
+  splits = (int)((nk + tps - 1) / tps);
+}
+
+extern "C" size_t rtsds_conv2d_wgrad_workspace(const rtsds_conv_desc* d) {
+  int bm, bn, splits, tps;
+  wgrad_plan(d, bm, bn, splits, tps);
+  size_t slab = splits <= 1 ? 0 : ((size_t)splits * d->k * d->kh * d->kw * d->c * 4 + 255) & ~(size_t)255;
+  return slab + (((size_t)kColsumRB * d->k * 4 + 255) & ~(size_t)255);
+}
+
+template <typename T, int ALA, int ALB>
+static void wgrad_launch(const ConvArgs& p, int bm, int bn, int splits, hipStream_t st) {
+  constexpr int BK = sizeof(T) == 2 ? 32 : 16;
+  if (sizeof(T) == 2) {
+    if (bm == 64 && bn == 64) launch<T, MODE_WGRAD, 64, 64, BK, 2, 2, ALA, ALB>(p, splits, st);
+    else if (bm == 64) launch<T, MODE_WGRAD, 64, 128, BK, 2, 2, ALA, ALB>(p, splits, st);
+    else if (bn == 64) launch<T, MODE_WGRAD, 128, 64, BK, 2, 2, ALA, ALB>(p, splits, st);
+    else launch<T, MODE_WGRAD, 128, 128, BK, 2, 2, ALA, ALB>(p, splits, st);
+  } else {
+    launch<T, MODE_WGRAD, 64, 64, BK, 2, 2, ALA, ALB>(p, splits, st);
+  }
+}
+
+extern "C" int rtsds_conv2d_wgrad(const rtsds_conv_desc* d, const void* x, const void* dy, float* dw,
+                                  float* dbias, void* ws, size_t ws_bytes, void* stream) {
+  int e = check_desc(d);
+  if (e) return e;
+  if (ws_bytes < rtsds_conv2d_wgrad_workspace(d)) return RTSDS_ERR_WORKSPACE;
+  hipStream_t st = (hipStream_t)stream;
+  int bm, bn, splits, tps;
+  wgrad_plan(d, bm, bn, splits, tps);
+  ConvArgs p = make_args(d);
+  p.a = dy; p.b = x; p.bias = nullptr; p.act = 0;
+  p.M = d->k;
+  p.N = d->kh * d->kw * d->c;
+  p.K = d->n * d->ho * d->wo;
+  p.tiles_per_split = tps;
+  p.split_stride = (long)p.M * p.N;
+  p.out = splits > 1 ? ws : (void*)dw;
+  const bool b16 = d->dtype == RTSDS_BF16;
+  const int V = b16 ? 8 : 4;
+  const int ala = d->k % V == 0, alb = d->c % V == 0;
+  if (b16) {
+    if (ala && alb) wgrad_launch<bf16, 1, 1>(p, bm, bn, splits, st);
+    else if (ala) wgrad_launch<bf16, 1, 0>(p, bm, bn, splits, st);
+    else if (alb) wgrad_launch<bf16, 0, 1>(p, bm, bn, splits, st);
+    else wgrad_launch<bf16, 0, 0>(p, bm, bn, splits, st);
+  } else {
+    if (ala && alb) wgrad_launch<float, 1, 1>(p, bm, bn, splits, st);
+    else if (ala) wgrad_launch<float, 1, 0>(p, bm, bn, splits, st);
+    else if (alb) wgrad_launch<float, 0, 1>(p, bm, bn, splits, st);
+    else wgrad_launch<float, 0, 0>(p, bm, bn, splits, st);
+  }
+  if (splits > 1) {
+    const long n = p.split_stride;
+    const int blocks = (int)std::min<long>(2048, (n + 255) / 256);
+    hipLaunchKernelGGL(split_reduce_kernel, dim3(blocks), dim3(256), 0, st, (const float*)ws, dw, n, splits);
+  }
+  if (dbias) {
+    const long rows = (long)d->n * d->ho * d->wo;
+    const size_t slab = splits <= 1 ? 0 : ((size_t)splits * p.split_stride * 4 + 255) & ~(size_t)255;
+    float* part = (float*)((char*)ws + slab);
+    dim3 g1(rt_cdiv(d->k, 64), kColsumRB);
+    if (b16) hipLaunchKernelGGL(colsum_part_kernel<bf16>, g1, dim3(256), 0, st, (const bf16*)dy, part, rows, d->k);
+    else hipLaunchKernelGGL(colsum_part_kernel<float>, g1, dim3(256), 0, st, (const float*)dy, part, rows, d->k);
+    hipLaunchKernelGGL(colsum_final_kernel, dim3(rt_cdiv(d->k, 256)), dim3(256), 0, st, (const float*)part, dbias, kColsumRB, d->k);
+  }
+  return hipGetLastError() == hipSuccess ? RTSDS_OK : RTSDS_ERR_LAUNCH;
+}

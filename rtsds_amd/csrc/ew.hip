@@ -1,0 +1,636 @@
+// Memory-bound kernels of the RTSDS hot path (gfx950): layout/dtype conversion, max-pool,
+// global average pool, channel attention scaling, bilinear resize, channel softmax,
+// cross-entropy with ignore_index, BCE-with-logits, fused Adam, argmax / pixel accuracy.
+// All activations are NHWC; per-pixel channel vectors are contiguous.
+#include "common.h"
+#include <algorithm>
+
+static inline int ew_blocks(long work, int per_block = 256, int cap = 8192) {
+  return (int)std::max<long>(1, std::min<long>(cap, (work + per_block - 1) / per_block));
+}
+#define GRID_STRIDE(i, n) for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < (n); i += (long)gridDim.x * blockDim.x)
+#define DISPATCH_T(dtype, ...)                                \
+  do {                                                        \
+    if ((dtype) == RTSDS_BF16) { typedef bf16 T; __VA_ARGS__; } \
+    else if ((dtype) == RTSDS_F32) { typedef float T; __VA_ARGS__; } \
+    else return RTSDS_ERR_UNSUPPORTED;                        \
+  } while (0)
+#define RET_LAUNCH() return hipGetLastError() == hipSuccess ? RTSDS_OK : RTSDS_ERR_LAUNCH
+
+// ------------------------------------------------------------------ layout / dtype
+// NCHW fp32 (the reference's input tensors) -> NHWC T.
+template <typename T>
+__global__ void nchw_to_nhwc_kernel(const float* __restrict__ x, T* __restrict__ y, int n, int c, long hw) {
+  const long total = (long)n * c * hw;
+  GRID_STRIDE(i, total) {
+    const int ch = (int)(i % c);
+    const long p = i / c;
+    const long img = p / hw, s = p - img * hw;
+    y[i] = from_f<T>(x[(img * c + ch) * hw + s]);
+  }
+}
+extern "C" int rtsds_nchw_to_nhwc(const float* x, void* y, int n, int c, int h, int w, int dtype, void* stream) {
+  const long total = (long)n * c * h * w;
+  if (total <= 0) return RTSDS_ERR_SHAPE;
+  DISPATCH_T(dtype, hipLaunchKernelGGL(nchw_to_nhwc_kernel<T>, dim3(ew_blocks(total)), dim3(256), 0, (hipStream_t)stream, x, (T*)y, n, c, (long)h * w));
+  RET_LAUNCH();
+}
+
+// dst (dtype_dst) = src (dtype_src), elementwise.
+template <typename S, typename D>
+__global__ void cast_kernel(const S* __restrict__ s, D* __restrict__ d, long n) {
+  GRID_STRIDE(i, n) d[i] = from_f<D>(to_f(s[i]));
+}
+extern "C" int rtsds_cast(const void* src, int src_dtype, void* dst, int dst_dtype, long n, void* stream) {
+  if (n <= 0) return n == 0 ? RTSDS_OK : RTSDS_ERR_SHAPE;
+  hipStream_t st = (hipStream_t)stream;
+  const int b = ew_blocks(n);
+  if (src_dtype == RTSDS_F32 && dst_dtype == RTSDS_BF16) hipLaunchKernelGGL((cast_kernel<float, bf16>), dim3(b), dim3(256), 0, st, (const float*)src, (bf16*)dst, n);
+  else if (src_dtype == RTSDS_BF16 && dst_dtype == RTSDS_F32) hipLaunchKernelGGL((cast_kernel<bf16, float>), dim3(b), dim3(256), 0, st, (const bf16*)src, (float*)dst, n);
+  else if (src_dtype == RTSDS_F32 && dst_dtype == RTSDS_F32) hipLaunchKernelGGL((cast_kernel<float, float>), dim3(b), dim3(256), 0, st, (const float*)src, (float*)dst, n);
+  else if (src_dtype == RTSDS_BF16 && dst_dtype == RTSDS_BF16) hipLaunchKernelGGL((cast_kernel<bf16, bf16>), dim3(b), dim3(256), 0, st, (const bf16*)src, (bf16*)dst, n);
+  else return RTSDS_ERR_UNSUPPORTED;
+  RET_LAUNCH();
+}
+
+// Channel-slice copy: dst[r][doff + j] = src[r][soff + j], j < cnt  (torch.cat / its backward
+// split along channels, build_bisenet.py:72,153).
+template <typename T>
+__global__ void copy_channels_kernel(const T* __restrict__ s, int sld, int soff, T* __restrict__ d, int dld, int doff, long rows, int cnt) {
+  const long total = rows * cnt;
+  GRID_STRIDE(i, total) {
+    const long r = i / cnt;
+    const int j = (int)(i - r * cnt);
+    d[r * dld + doff + j] = s[r * sld + soff + j];
+  }
+}
+template <typename T>
+__global__ void copy_channels_vec_kernel(const T* __restrict__ s, int sld, int soff, T* __restrict__ d, int dld, int doff, long rows, int cnt) {
+  typedef typename VecT<T>::v16 V16;
+  constexpr int V = VecT<T>::N;
+  const int cv = cnt / V;
+  const long total = rows * cv;
+  GRID_STRIDE(i, total) {
+    const long r = i / cv;
+    const int j = (int)(i - r * cv) * V;
+    *(V16*)(d + r * dld + doff + j) = *(const V16*)(s + r * sld + soff + j);
+  }
+}
+extern "C" int rtsds_copy_channels(const void* src, int src_ld, int src_off, void* dst, int dst_ld, int dst_off, long rows,
+                                   int cnt, int dtype, void* stream) {
+  if (rows <= 0 || cnt <= 0) return RTSDS_ERR_SHAPE;
+  hipStream_t st = (hipStream_t)stream;
+  DISPATCH_T(dtype, {
+    constexpr int V = VecT<T>::N;
+    if (cnt % V == 0 && src_ld % V == 0 && dst_ld % V == 0 && src_off % V == 0 && dst_off % V == 0)
+      hipLaunchKernelGGL(copy_channels_vec_kernel<T>, dim3(ew_blocks(rows * cnt / V)), dim3(256), 0, st, (const T*)src, src_ld, src_off, (T*)dst, dst_ld, dst_off, rows, cnt);
+    else
+      hipLaunchKernelGGL(copy_channels_kernel<T>, dim3(ew_blocks(rows * cnt)), dim3(256), 0, st, (const T*)src, src_ld, src_off, (T*)dst, dst_ld, dst_off, rows, cnt);
+  });
+  RET_LAUNCH();
+}
+
+// ------------------------------------------------------------------ activations (pointwise)
+// act: 1 relu, 2 leaky(0.2), 3 sigmoid.  Backward uses the forward OUTPUT y.
+template <typename T>
+__global__ void act_fwd_kernel(const T* __restrict__ x, T* __restrict__ y, long n, int act) {
+  GRID_STRIDE(i, n) {
+    float v = to_f(x[i]);
+    if (act == 1) v = fmaxf(v, 0.f);
+    else if (act == 2) v = v > 0.f ? v : 0.2f * v;
+    else if (act == 3) v = 1.f / (1.f + expf(-v));
+    y[i] = from_f<T>(v);
+  }
+}
+template <typename T>
+__global__ void act_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ y, T* __restrict__ dx, long n, int act, float alpha) {
+  GRID_STRIDE(i, n) {
+    const float g = to_f(dy[i]);
+    float r;
+    if (act == 1) r = to_f(y[i]) > 0.f ? g : 0.f;
+    else if (act == 2) r = to_f(y[i]) > 0.f ? g : 0.2f * g;
+    else if (act == 3) { const float s = to_f(y[i]); r = g * s * (1.f - s); }
+    else r = alpha * g;  // act 0: scale (gradient reversal, model.py:9-17)
+    dx[i] = from_f<T>(r);
+  }
+}
+extern "C" int rtsds_act_fwd(const void* x, void* y, long n, int act, int dtype, void* stream) {
+  if (n <= 0) return RTSDS_ERR_SHAPE;
+  DISPATCH_T(dtype, hipLaunchKernelGGL(act_fwd_kernel<T>, dim3(ew_blocks(n)), dim3(256), 0, (hipStream_t)stream, (const T*)x, (T*)y, n, act));
+  RET_LAUNCH();
+}
+extern "C" int rtsds_act_bwd(const void* dy, const void* y, void* dx, long n, int act, float alpha, int dtype, void* stream) {
+  if (n <= 0) return RTSDS_ERR_SHAPE;
+  DISPATCH_T(dtype, hipLaunchKernelGGL(act_bwd_kernel<T>, dim3(ew_blocks(n)), dim3(256), 0, (hipStream_t)stream, (const T*)dy, (const T*)y, (T*)dx, n, act, alpha));
+  RET_LAUNCH();
+}
+
+// ------------------------------------------------------------------ max pool
+// torchvision / deeplab max pool (build_contextpath.py:21, deeplabv2.py:79): padded taps are
+// skipped, first maximum wins (ATen CPU scan order), NaN propagates.  idx = tap index.
+template <typename T>
+__global__ void maxpool_fwd_kernel(const T* __restrict__ x, T* __restrict__ y, uint8_t* __restrict__ idx, int n, int h, int w,
+                                   int c, int ho, int wo, int k, int s, int p) {
+  const long total = (long)n * ho * wo * c;
+  GRID_STRIDE(i, total) {
+    const int ch = (int)(i % c);
+    long q = i / c;
+    const int ow = (int)(q % wo); q /= wo;
+    const int oh = (int)(q % ho);
+    const int img = (int)(q / ho);
+    const int h0 = oh * s - p, w0 = ow * s - p;
+    float best = -INFINITY;
+    int bi = -1;
+    for (int a = 0; a < k; ++a) {
+      const int hh = h0 + a;
+      if (hh < 0 || hh >= h) continue;
+      for (int b = 0; b < k; ++b) {
+        const int ww = w0 + b;
+        if (ww < 0 || ww >= w) continue;
+        const float v = to_f(x[(((long)img * h + hh) * w + ww) * c + ch]);
+        if (bi < 0 || v > best || v != v) { best = v; bi = a * k + b; if (v != v) goto done; }
+      }
+    }
+  done:
+    y[i] = from_f<T>(best);
+    idx[i] = (uint8_t)(bi < 0 ? 0 : bi);
+  }
+}
+// Gather backward (deterministic): each input element sums the windows that chose it.
+template <typename T>
+__global__ void maxpool_bwd_kernel(const T* __restrict__ dy, const uint8_t* __restrict__ idx, T* __restrict__ dx, int n, int h,
+                                   int w, int c, int ho, int wo, int k, int s, int p) {
+  const long total = (long)n * h * w * c;
+  GRID_STRIDE(i, total) {
+    const int ch = (int)(i % c);
+    long q = i / c;
+    const int iw = (int)(q % w); q /= w;
+    const int ih = (int)(q % h);
+    const int img = (int)(q / h);
+    const int oh_lo = max(0, (ih + p - k + s) / s), oh_hi = min(ho - 1, (ih + p) / s);
+    const int ow_lo = max(0, (iw + p - k + s) / s), ow_hi = min(wo - 1, (iw + p) / s);
+    float acc = 0.f;
+    for (int oh = oh_lo; oh <= oh_hi; ++oh) {
+      const int a = ih - (oh * s - p);
+      if (a < 0 || a >= k) continue;
+      for (int ow = ow_lo; ow <= ow_hi; ++ow) {
+        const int b = iw - (ow * s - p);
+        if (b < 0 || b >= k) continue;
+        const long o = (((long)img * ho + oh) * wo + ow) * c + ch;
+        if (idx[o] == a * k + b) acc += to_f(dy[o]);
+      }
+    }
+    dx[i] = from_f<T>(acc);
+  }
+}
+extern "C" int rtsds_maxpool_fwd(const void* x, void* y, uint8_t* idx, int n, int h, int w, int c, int ho, int wo, int k, int s,
+                                 int p, int dtype, void* stream) {
+  if (k * k > 255 || n <= 0 || ho <= 0 || wo <= 0) return RTSDS_ERR_SHAPE;
+  const long total = (long)n * ho * wo * c;
+  DISPATCH_T(dtype, hipLaunchKernelGGL(maxpool_fwd_kernel<T>, dim3(ew_blocks(total)), dim3(256), 0, (hipStream_t)stream, (const T*)x, (T*)y, idx, n, h, w, c, ho, wo, k, s, p));
+  RET_LAUNCH();
+}
+extern "C" int rtsds_maxpool_bwd(const void* dy, const uint8_t* idx, void* dx, int n, int h, int w, int c, int ho, int wo, int k,
+                                 int s, int p, int dtype, void* stream) {
+  const long total = (long)n * h * w * c;
+  if (total <= 0) return RTSDS_ERR_SHAPE;
+  DISPATCH_T(dtype, hipLaunchKernelGGL(maxpool_bwd_kernel<T>, dim3(ew_blocks(total)), dim3(256), 0, (hipStream_t)stream, (const T*)dy, idx, (T*)dx, n, h, w, c, ho, wo, k, s, p));
+  RET_LAUNCH();
+}
+
+// ------------------------------------------------------------------ global average pool
+// y[img][c] = mean_hw x[img][hw][c]   (AdaptiveAvgPool2d(1) / torch.mean over H,W:
+// build_bisenet.py:46,75, build_contextpath.py:27-28, model.py:63,82).
+// grid (img, ceil(c/64)); 256 threads = 4 row groups x 64 channels.
+template <typename T>
+__global__ void gap_fwd_kernel(const T* __restrict__ x, T* __restrict__ y, long hw, int c) {
+  __shared__ float red[4][64];
+  const int img = blockIdx.x, ch = blockIdx.y * 64 + (threadIdx.x & 63), rg = threadIdx.x >> 6;
+  float s = 0.f;
+  if (ch < c)
+    for (long r = rg; r < hw; r += 4) s += to_f(x[((long)img * hw + r) * c + ch]);
+  red[rg][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (rg == 0 && ch < c) y[(long)img * c + ch] = from_f<T>((red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x]) / (float)hw);
+}
+template <typename T>
+__global__ void gap_bwd_kernel(const T* __restrict__ dy, T* __restrict__ dx, int n, long hw, int c) {
+  const long total = (long)n * hw * c;
+  const float inv = 1.f / (float)hw;
+  GRID_STRIDE(i, total) {
+    const int ch = (int)(i % c);
+    const long img = i / c / hw;
+    dx[i] = from_f<T>(to_f(dy[img * c + ch]) * inv);
+  }
+}
+extern "C" int rtsds_gap_fwd(const void* x, void* y, int n, long hw, int c, int dtype, void* stream) {
+  if (n <= 0 || hw <= 0 || c <= 0) return RTSDS_ERR_SHAPE;
+  DISPATCH_T(dtype, hipLaunchKernelGGL(gap_fwd_kernel<T>, dim3(n, rt_cdiv(c, 64)), dim3(256), 0, (hipStream_t)stream, (const T*)x, (T*)y, hw, c));
+  RET_LAUNCH();
+}
+extern "C" int rtsds_gap_bwd(const void* dy, void* dx, int n, long hw, int c, int dtype, void* stream) {
+  if (n <= 0 || hw <= 0 || c <= 0) return RTSDS_ERR_SHAPE;
+  DISPATCH_T(dtype, hipLaunchKernelGGL(gap_bwd_kernel<T>, dim3(ew_blocks((long)n * hw * c)), dim3(256), 0, (hipStream_t)stream, (const T*)dy, (T*)dx, n, hw, c));
+  RET_LAUNCH();
+}
+
+// ------------------------------------------------------------------ channel attention scale
+// mode 0: y = x * a[img][c]           (ARM x*sigmoid, cx2*tail: build_bisenet.py:52,149)
+// mode 1: y = x * a[img][c] + x       (FFM: build_bisenet.py:79-80)
+template <typename T>
+__global__ void chscale_fwd_kernel(const T* __restrict__ x, const T* __restrict__ a, T* __restrict__ y, int n, long hw, int c, int mode) {
+  const long total = (long)n * hw * c;
+  GRID_STRIDE(i, total) {
+    const int ch = (int)(i % c);
+    const long img = i / c / hw;
+    const float xv = to_f(x[i]), av = to_f(a[img * c + ch]);
+    y[i] = from_f<T>(mode ? fmaf(xv, av, xv) : xv * av);
+  }
+}
+template <typename T>
+__global__ void chscale_bwd_dx_kernel(const T* __restrict__ dy, const T* __restrict__ a, T* __restrict__ dx, int n, long hw, int c, int mode) {
+  const long total = (long)n * hw * c;
+  GRID_STRIDE(i, total) {
+    const int ch = (int)(i % c);
+    const long img = i / c / hw;
+    const float av = to_f(a[img * c + ch]) + (mode ? 1.f : 0.f);
+    dx[i] = from_f<T>(to_f(dy[i]) * av);
+  }
+}
+// da[img][c] = sum_hw dy * x   (grid (img, ceil(c/64)))
+template <typename T>
+__global__ void chscale_bwd_da_kernel(const T* __restrict__ dy, const T* __restrict__ x, T* __restrict__ da, long hw, int c) {
+  __shared__ float red[4][64];
+  const int img = blockIdx.x, ch = blockIdx.y * 64 + (threadIdx.x & 63), rg = threadIdx.x >> 6;
+  float s = 0.f;
+  if (ch < c)
+    for (long r = rg; r < hw; r += 4) {
+      const long o = ((long)img * hw + r) * c + ch;
+      s = fmaf(to_f(dy[o]), to_f(x[o]), s);
+    }
+  red[rg][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (rg == 0 && ch < c) da[(long)img * c + ch] = from_f<T>(red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x]);
+}
+extern "C" int rtsds_chscale_fwd(const void* x, const void* a, void* y, int n, long hw, int c, int mode, int dtype, void* stream) {
+  const long total = (long)n * hw * c;
+  if (total <= 0) return RTSDS_ERR_SHAPE;
+  DISPATCH_T(dtype, hipLaunchKernelGGL(chscale_fwd_kernel<T>, dim3(ew_blocks(total)), dim3(256), 0, (hipStream_t)stream, (const T*)x, (const T*)a, (T*)y, n, hw, c, mode));
+  RET_LAUNCH();
+}
+extern "C" int rtsds_chscale_bwd(const void* dy, const void* x, const void* a, void* dx, void* da, int n, long hw, int c, int mode,
+                                 int dtype, void* stream) {
+  const long total = (long)n * hw * c;
+  if (total <= 0) return RTSDS_ERR_SHAPE;
+  hipStream_t st = (hipStream_t)stream;
+  DISPATCH_T(dtype, {
+    if (dx) hipLaunchKernelGGL(chscale_bwd_dx_kernel<T>, dim3(ew_blocks(total)), dim3(256), 0, st, (const T*)dy, (const T*)a, (T*)dx, n, hw, c, mode);
+    if (da) hipLaunchKernelGGL(chscale_bwd_da_kernel<T>, dim3(n, rt_cdiv(c, 64)), dim3(256), 0, st, (const T*)dy, (const T*)x, (T*)da, hw, c);
+  });
+  RET_LAUNCH();
+}
+
+// ------------------------------------------------------------------ bilinear (align_corners=False)
+// ATen's source index: src = scale*(dst+0.5)-0.5 clamped at 0; i0 = floor, i1 = min(i0+1, in-1).
+// scale = in/out for size=..., 1/scale_factor for scale_factor=... (both computed by the host
+// in fp32 exactly as ATen's area_pixel_compute_scale does).
+RT_DEV void bil_src(int o, float scale, int in, int& i0, int& i1, float& l0, float& l1) {
+  float src = scale * ((float)o + 0.5f) - 0.5f;
+  if (src < 0.f) src = 0.f;
+  i0 = (int)src;
+  if (i0 > in - 1) i0 = in - 1;
+  i1 = i0 + (i0 < in - 1 ? 1 : 0);
+  l1 = src - (float)i0;
+  l0 = 1.f - l1;
+}
+template <typename T>
+__global__ void bilinear_fwd_kernel(const T* __restrict__ x, T* __restrict__ y, int n, int hi, int wi, int c, int ho, int wo,
+                                    float sh, float sw, int yld, int yoff) {
+  const long total = (long)n * ho * wo * c;
+  GRID_STRIDE(i, total) {
+    const int ch = (int)(i % c);
+    long q = i / c;
+    const int ow = (int)(q % wo); q /= wo;
+    const int oh = (int)(q % ho);
+    const int img = (int)(q / ho);
+    int h0, h1, w0, w1;
+    float lh0, lh1, lw0, lw1;
+    bil_src(oh, sh, hi, h0, h1, lh0, lh1);
+    bil_src(ow, sw, wi, w0, w1, lw0, lw1);
+    const T* b = x + (long)img * hi * wi * c + ch;
+    const float v00 = to_f(b[((long)h0 * wi + w0) * c]), v01 = to_f(b[((long)h0 * wi + w1) * c]);
+    const float v10 = to_f(b[((long)h1 * wi + w0) * c]), v11 = to_f(b[((long)h1 * wi + w1) * c]);
+    const float v = lh0 * (lw0 * v00 + lw1 * v01) + lh1 * (lw0 * v10 + lw1 * v11);
+    y[((((long)img * ho + oh) * wo) + ow) * yld + yoff + ch] = from_f<T>(v);
+  }
+}
+// Backward as a gather (deterministic): input pixel (ih, iw) collects every output pixel whose
+// (i0 | i1) equals it.  Candidate outputs span [(i-1.5)/scale, (i+1.5)/scale].
+template <typename T>
+__global__ void bilinear_bwd_kernel(const T* __restrict__ dy, T* __restrict__ dx, int n, int hi, int wi, int c, int ho, int wo,
+                                    float sh, float sw, int dyld, int dyoff) {
+  const long total = (long)n * hi * wi * c;
+  GRID_STRIDE(i, total) {
+    const int ch = (int)(i % c);
+    long q = i / c;
+    const int iw = (int)(q % wi); q /= wi;
+    const int ih = (int)(q % hi);
+    const int img = (int)(q / hi);
+    const int oh_lo = max(0, (int)floorf(((float)ih - 1.5f) / sh) - 1), oh_hi = min(ho - 1, (int)ceilf(((float)ih + 1.5f) / sh) + 1);
+    const int ow_lo = max(0, (int)floorf(((float)iw - 1.5f) / sw) - 1), ow_hi = min(wo - 1, (int)ceilf(((float)iw + 1.5f) / sw) + 1);
+    float acc = 0.f;
+    for (int oh = oh_lo; oh <= oh_hi; ++oh) {
+      int h0, h1;
+      float lh0, lh1;
+      bil_src(oh, sh, hi, h0, h1, lh0, lh1);
+      const float wh = (h0 == ih ? lh0 : 0.f) + (h1 == ih ? lh1 : 0.f);
+      if (wh == 0.f) continue;
+      float racc = 0.f;
+      for (int ow = ow_lo; ow <= ow_hi; ++ow) {
+        int w0, w1;
+        float lw0, lw1;
+        bil_src(ow, sw, wi, w0, w1, lw0, lw1);
+        const float ww = (w0 == iw ? lw0 : 0.f) + (w1 == iw ? lw1 : 0.f);
+        if (ww == 0.f) continue;
+        racc = fmaf(ww, to_f(dy[((((long)img * ho + oh) * wo) + ow) * dyld + dyoff + ch]), racc);
+      }
+      acc = fmaf(wh, racc, acc);
+    }
+    dx[i] = from_f<T>(acc);
+  }
+}
+extern "C" int rtsds_bilinear_fwd(const void* x, void* y, int n, int hi, int wi, int c, int ho, int wo, float scale_h, float scale_w,
+                                  int y_ld, int y_off, int dtype, void* stream) {
+  const long total = (long)n * ho * wo * c;
+  if (total <= 0 || hi <= 0 || wi <= 0) return RTSDS_ERR_SHAPE;
+  if (y_ld <= 0) y_ld = c;
+  DISPATCH_T(dtype, hipLaunchKernelGGL(bilinear_fwd_kernel<T>, dim3(ew_blocks(total)), dim3(256), 0, (hipStream_t)stream, (const T*)x, (T*)y, n, hi, wi, c, ho, wo, scale_h, scale_w, y_ld, y_off));
+  RET_LAUNCH();
+}
+extern "C" int rtsds_bilinear_bwd(const void* dy, void* dx, int n, int hi, int wi, int c, int ho, int wo, float scale_h, float scale_w,
+                                  int dy_ld, int dy_off, int dtype, void* stream) {
+  const long total = (long)n * hi * wi * c;
+  if (total <= 0 || ho <= 0 || wo <= 0) return RTSDS_ERR_SHAPE;
+  if (dy_ld <= 0) dy_ld = c;
+  DISPATCH_T(dtype, hipLaunchKernelGGL(bilinear_bwd_kernel<T>, dim3(ew_blocks(total)), dim3(256), 0, (hipStream_t)stream, (const T*)dy, (T*)dx, n, hi, wi, c, ho, wo, scale_h, scale_w, dy_ld, dy_off));
+  RET_LAUNCH();
+}
+
+// ------------------------------------------------------------------ channel softmax (dim=1)
+// train.py:225,245,256.  One thread per pixel; logits addressed by (sn, sc, shw) strides so
+// NHWC and NCHW tensors both work.  Output NHWC contiguous with row pitch yld (zero-padded
+// channels c..yld-1 so a padded discriminator input can be produced directly).
+template <typename T, typename O>
+__global__ void softmax_fwd_kernel(const T* __restrict__ x, O* __restrict__ y, int n, long hw, int c, long sn, long sc, long shw, int yld) {
+  const long total = (long)n * hw;
+  GRID_STRIDE(p, total) {
+    const long img = p / hw, s = p - img * hw;
+    const T* b = x + img * sn + s * shw;
+    float m = -INFINITY;
+    for (int k = 0; k < c; ++k) m = fmaxf(m, to_f(b[k * sc]));
+    float z = 0.f;
+    for (int k = 0; k < c; ++k) z += expf(to_f(b[k * sc]) - m);
+    const float iz = 1.f / z;
+    O* o = y + p * yld;
+    for (int k = 0; k < c; ++k) o[k] = from_f<O>(expf(to_f(b[k * sc]) - m) * iz);
+    for (int k = c; k < yld; ++k) o[k] = from_f<O>(0.f);
+  }
+}
+// dx = y * (dy - sum_k dy_k y_k); dy/y have row pitch ld (>= c), dx strided like the logits.
+template <typename T, typename O>
+__global__ void softmax_bwd_kernel(const O* __restrict__ dy, const O* __restrict__ y, T* __restrict__ dx, int n, long hw, int c, int ld,
+                                   long sn, long sc, long shw) {
+  const long total = (long)n * hw;
+  GRID_STRIDE(p, total) {
+    const long img = p / hw, s = p - img * hw;
+    const O* g = dy + p * ld;
+    const O* yy = y + p * ld;
+    float dot = 0.f;
+    for (int k = 0; k < c; ++k) dot = fmaf(to_f(g[k]), to_f(yy[k]), dot);
+    T* o = dx + img * sn + s * shw;
+    for (int k = 0; k < c; ++k) o[k * sc] = from_f<T>(to_f(yy[k]) * (to_f(g[k]) - dot));
+  }
+}
+extern "C" int rtsds_softmax_fwd(const void* x, long sn, long sc, long shw, void* y, int y_ld, int n, long hw, int c, int dtype,
+                                 void* stream) {
+  if (n <= 0 || hw <= 0 || c <= 0 || y_ld < c) return RTSDS_ERR_SHAPE;
+  DISPATCH_T(dtype, hipLaunchKernelGGL((softmax_fwd_kernel<T, T>), dim3(ew_blocks((long)n * hw)), dim3(256), 0, (hipStream_t)stream, (const T*)x, (T*)y, n, hw, c, sn, sc, shw, y_ld));
+  RET_LAUNCH();
+}
+extern "C" int rtsds_softmax_bwd(const void* dy, const void* y, int ld, void* dx, long sn, long sc, long shw, int n, long hw, int c,
+                                 int dtype, void* stream) {
+  if (n <= 0 || hw <= 0 || c <= 0 || ld < c) return RTSDS_ERR_SHAPE;
+  DISPATCH_T(dtype, hipLaunchKernelGGL((softmax_bwd_kernel<T, T>), dim3(ew_blocks((long)n * hw)), dim3(256), 0, (hipStream_t)stream, (const T*)dy, (const T*)y, (T*)dx, n, hw, c, ld, sn, sc, shw));
+  RET_LAUNCH();
+}
+
+// ------------------------------------------------------------------ cross entropy (ignore_index)
+// nn.CrossEntropyLoss(ignore_index=19) (main.py:124-130, train.py:86-92,202-204): mean over
+// non-ignored pixels of logsumexp(x) - x[t].  Two passes for the forward (per-block partial
+// (sum, count) -> final), one fused pass for the backward.
+// ws layout: [0, RB) partial sums, [RB, 2RB) partial counts, [2RB] total count.
+static const int kCeRB = 1024;
+template <typename T>
+__global__ void ce_fwd_part_kernel(const T* __restrict__ x, const int64_t* __restrict__ tgt, float* __restrict__ part, int n, long hw, int c,
+                                   long sn, long sc, long shw, int ignore) {
+  __shared__ float rs[4], rc[4];
+  const long total = (long)n * hw;
+  float ls = 0.f, lc = 0.f;
+  GRID_STRIDE(p, total) {
+    const long t = tgt[p];
+    if (t == ignore) continue;
+    const long img = p / hw, s = p - img * hw;
+    const T* b = x + img * sn + s * shw;
+    float m = -INFINITY;
+    for (int k = 0; k < c; ++k) m = fmaxf(m, to_f(b[k * sc]));
+    float z = 0.f;
+    for (int k = 0; k < c; ++k) z += expf(to_f(b[k * sc]) - m);
+    const float xt = (t >= 0 && t < c) ? to_f(b[t * sc]) : NAN;
+    ls += logf(z) + m - xt;
+    lc += 1.f;
+  }
+  ls = wave_sum(ls);
+  lc = wave_sum(lc);
+  if ((threadIdx.x & 63) == 0) { rs[threadIdx.x >> 6] = ls; rc[threadIdx.x >> 6] = lc; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    part[blockIdx.x] = rs[0] + rs[1] + rs[2] + rs[3];
+    part[kCeRB + blockIdx.x] = rc[0] + rc[1] + rc[2] + rc[3];
+  }
+}
+__global__ void ce_fwd_final_kernel(float* __restrict__ part, int nb, float* __restrict__ loss) {
+  __shared__ float rs[4], rc[4];
+  float s = 0.f, cn = 0.f;
+  for (int i = threadIdx.x; i < nb; i += blockDim.x) { s += part[i]; cn += part[kCeRB + i]; }
+  s = wave_sum(s);
+  cn = wave_sum(cn);
+  if ((threadIdx.x & 63) == 0) { rs[threadIdx.x >> 6] = s; rc[threadIdx.x >> 6] = cn; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float S = rs[0] + rs[1] + rs[2] + rs[3], C = rc[0] + rc[1] + rc[2] + rc[3];
+    part[2 * kCeRB] = C;
+    loss[0] = S / C;
+  }
+}
+template <typename T>
+__global__ void ce_bwd_kernel(const T* __restrict__ x, const int64_t* __restrict__ tgt, const float* __restrict__ gout,
+                              const float* __restrict__ count, T* __restrict__ dx, int n, long hw, int c, long sn, long sc, long shw,
+                              int ignore) {
+  const long total = (long)n * hw;
+  const float g = gout[0] / count[0];
+  GRID_STRIDE(p, total) {
+    const long t = tgt[p];
+    const long img = p / hw, s = p - img * hw;
+    const T* b = x + img * sn + s * shw;
+    T* o = dx + img * sn + s * shw;
+    if (t == ignore) {
+      for (int k = 0; k < c; ++k) o[k * sc] = from_f<T>(0.f);
+      continue;
+    }
+    float m = -INFINITY;
+    for (int k = 0; k < c; ++k) m = fmaxf(m, to_f(b[k * sc]));
+    float z = 0.f;
+    for (int k = 0; k < c; ++k) z += expf(to_f(b[k * sc]) - m);
+    const float iz = 1.f / z;
+    for (int k = 0; k < c; ++k) {
+      const float pr = expf(to_f(b[k * sc]) - m) * iz;
+      o[k * sc] = from_f<T>(g * (pr - (k == t ? 1.f : 0.f)));
+    }
+  }
+}
+extern "C" size_t rtsds_ce_workspace(void) { return (2 * kCeRB + 64) * sizeof(float); }
+extern "C" int rtsds_ce_fwd(const void* x, long sn, long sc, long shw, const int64_t* tgt, float* loss, int n, long hw, int c,
+                            int ignore_index, int dtype, void* ws, size_t ws_bytes, void* stream) {
+  if (n <= 0 || hw <= 0 || c <= 0) return RTSDS_ERR_SHAPE;
+  if (ws_bytes < rtsds_ce_workspace()) return RTSDS_ERR_WORKSPACE;
+  hipStream_t st = (hipStream_t)stream;
+  const int nb = std::min<int>(kCeRB, ew_blocks((long)n * hw, 256, kCeRB));
+  DISPATCH_T(dtype, hipLaunchKernelGGL(ce_fwd_part_kernel<T>, dim3(nb), dim3(256), 0, st, (const T*)x, tgt, (float*)ws, n, hw, c, sn, sc, shw, ignore_index));
+  hipLaunchKernelGGL(ce_fwd_final_kernel, dim3(1), dim3(256), 0, st, (float*)ws, nb, loss);
+  RET_LAUNCH();
+}
+// count = the valid-pixel count written by rtsds_ce_fwd into its workspace (ws + 2*1024 floats).
+extern "C" int rtsds_ce_bwd(const void* x, long sn, long sc, long shw, const int64_t* tgt, const float* grad_loss, const float* count,
+                            void* dx, int n, long hw, int c, int ignore_index, int dtype, void* stream) {
+  if (n <= 0 || hw <= 0 || c <= 0) return RTSDS_ERR_SHAPE;
+  DISPATCH_T(dtype, hipLaunchKernelGGL(ce_bwd_kernel<T>, dim3(ew_blocks((long)n * hw)), dim3(256), 0, (hipStream_t)stream, (const T*)x, tgt, grad_loss, count, (T*)dx, n, hw, c, sn, sc, shw, ignore_index));
+  RET_LAUNCH();
+}
+
+// ------------------------------------------------------------------ BCE with logits
+// nn.BCEWithLogitsLoss() (main.py:131-132, train.py:229,247,258): mean of
+// max(x,0) - x*t + log1p(exp(-|x|)).  Tiny (one logit per image): one block.
+__global__ void bce_fwd_kernel(const float* __restrict__ x, const float* __restrict__ t, float* __restrict__ loss, int n) {
+  __shared__ float r[4];
+  float s = 0.f;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const float v = x[i];
+    s += fmaxf(v, 0.f) - v * t[i] + log1pf(expf(-fabsf(v)));
+  }
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) r[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) loss[0] = (r[0] + r[1] + r[2] + r[3]) / (float)n;
+}
+__global__ void bce_bwd_kernel(const float* __restrict__ x, const float* __restrict__ t, const float* __restrict__ gout, float* __restrict__ dx, int n) {
+  const float g = gout[0] / (float)n;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const float s = 1.f / (1.f + expf(-x[i]));
+    dx[i] = g * (s - t[i]);
+  }
+}
+extern "C" int rtsds_bce_fwd(const float* x, const float* target, float* loss, int n, void* stream) {
+  if (n <= 0) return RTSDS_ERR_SHAPE;
+  hipLaunchKernelGGL(bce_fwd_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, x, target, loss, n);
+  RET_LAUNCH();
+}
+extern "C" int rtsds_bce_bwd(const float* x, const float* target, const float* grad_loss, float* dx, int n, void* stream) {
+  if (n <= 0) return RTSDS_ERR_SHAPE;
+  hipLaunchKernelGGL(bce_bwd_kernel, dim3(ew_blocks(n)), dim3(256), 0, (hipStream_t)stream, x, target, grad_loss, dx, n);
+  RET_LAUNCH();
+}
+
+// ------------------------------------------------------------------ Adam (flat, fused)
+// torch.optim.Adam (main.py:116-117; L2 weight decay folded into the gradient, as torch does
+// for weight_decay != 0 without decoupling).  One launch over the flat parameter arena;
+// optionally refreshes the bf16 shadow weights in the same pass.
+__global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m, float* __restrict__ v,
+                            bf16* __restrict__ shadow, long n, float lr, float b1, float b2, float eps, float wd, float bc1,
+                            float bc2_sqrt, float gscale) {
+  const float step = lr / bc1;
+  GRID_STRIDE(i, n) {
+    float gi = g[i] * gscale;
+    float pi = p[i];
+    if (wd != 0.f) gi = fmaf(wd, pi, gi);
+    float mi = m[i], vi = v[i];
+    mi = fmaf(1.f - b1, gi - mi, mi);
+    vi = fmaf(b2, vi, (1.f - b2) * gi * gi);
+    const float den = sqrtf(vi) / bc2_sqrt + eps;
+    pi -= step * (mi / den);
+    m[i] = mi;
+    v[i] = vi;
+    p[i] = pi;
+    if (shadow) shadow[i] = (bf16)pi;
+  }
+}
+extern "C" int rtsds_adam_step(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, void* bf16_shadow, long n, float lr,
+                               float beta1, float beta2, float eps, float weight_decay, int step, float grad_scale, void* stream) {
+  if (n <= 0 || step <= 0) return RTSDS_ERR_SHAPE;
+  const double bc1 = 1.0 - pow((double)beta1, step), bc2 = 1.0 - pow((double)beta2, step);
+  hipLaunchKernelGGL(adam_kernel, dim3(ew_blocks(n, 256, 4096)), dim3(256), 0, (hipStream_t)stream, param, grad, exp_avg, exp_avg_sq,
+                     (bf16*)bf16_shadow, n, lr, beta1, beta2, eps, weight_decay, (float)bc1, (float)sqrt(bc2), grad_scale);
+  RET_LAUNCH();
+}
+
+// ------------------------------------------------------------------ argmax / pixel accuracy
+// argmax over channels, first maximum wins (torch.argmax / max(1), train.py:102-106,272-275,
+// validation.py:51).  out_idx may be NULL; correct += #(argmax == target) (ignored pixels
+// count as wrong, exactly like the reference).
+template <typename T>
+__global__ void argmax_kernel(const T* __restrict__ x, int64_t* __restrict__ out, const int64_t* __restrict__ tgt,
+                              unsigned long long* __restrict__ correct, int n, long hw, int c, long sn, long sc, long shw) {
+  const long total = (long)n * hw;
+  unsigned long long cnt = 0;
+  GRID_STRIDE(p, total) {
+    const long img = p / hw, s = p - img * hw;
+    const T* b = x + img * sn + s * shw;
+    float best = to_f(b[0]);
+    int bi = 0;
+    for (int k = 1; k < c; ++k) {
+      const float v = to_f(b[k * sc]);
+      if (v > best || (v != v && best == best)) { best = v; bi = k; }
+    }
+    if (out) out[p] = bi;
+    if (tgt && tgt[p] == bi) ++cnt;
+  }
+  if (correct) {
+    for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
+    if ((threadIdx.x & 63) == 0 && cnt) atomicAdd(correct, cnt);
+  }
+}
+extern "C" int rtsds_argmax(const void* x, long sn, long sc, long shw, int64_t* out, const int64_t* target, unsigned long long* correct,
+                            int n, long hw, int c, int dtype, void* stream) {
+  if (n <= 0 || hw <= 0 || c <= 0) return RTSDS_ERR_SHAPE;
+  DISPATCH_T(dtype, hipLaunchKernelGGL(argmax_kernel<T>, dim3(ew_blocks((long)n * hw, 256, 4096)), dim3(256), 0, (hipStream_t)stream, (const T*)x, out, target, correct, n, hw, c, sn, sc, shw));
+  RET_LAUNCH();
+}
+
+// 19x19 confusion histogram (utils.fast_hist, utils.py:52-58): labels outside [0, nc) dropped.
+__global__ void confusion_kernel(const int64_t* __restrict__ label, const int64_t* __restrict__ pred, unsigned long long* __restrict__ hist,
+                                 long total, int nc) {
+  extern __shared__ unsigned int lh[];
+  for (int i = threadIdx.x; i < nc * nc; i += blockDim.x) lh[i] = 0;
+  __syncthreads();
+  GRID_STRIDE(p, total) {
+    const long a = label[p];
+    if (a >= 0 && a < nc) atomicAdd(&lh[a * nc + pred[p]], 1u);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < nc * nc; i += blockDim.x)
+    if (lh[i]) atomicAdd(&hist[i], (unsigned long long)lh[i]);
+}
+extern "C" int rtsds_confusion(const int64_t* label, const int64_t* pred, unsigned long long* hist, long total, int nc, void* stream) {
+  if (total <= 0 || nc <= 0 || nc > 64) return RTSDS_ERR_SHAPE;
+  hipLaunchKernelGGL(confusion_kernel, dim3(ew_blocks(total, 256, 1024)), dim3(256), nc * nc * 4, (hipStream_t)stream, label, pred, hist, total, nc);
+  RET_LAUNCH();
+}

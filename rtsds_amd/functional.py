@@ -1,0 +1,555 @@
+"""Autograd functions over the C ABI (include/rtsds_hip.h).
+
+Every forward and backward here is a call into librtsds_hip.so on the current HIP stream;
+PyTorch supplies only memory (caching allocator), the stream and the autograd graph.
+Activations are NHWC tensors of logical shape [N, C, H, W] (``torch.channels_last``) in the
+runtime compute dtype; parameters, statistics and losses are fp32.
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from ._lib import ConvDesc, lib
+from .runtime import CL, dcode, empty_nhwc, nhwc, require_hip, stream, workspace
+
+_P = lambda t: None if t is None else t.data_ptr()  # noqa: E731
+
+
+# ----------------------------------------------------------------------------- conv
+def _conv_desc(x, k, kh, kw, stride, padding, dilation):
+    n, c, h, w = x.shape
+    ho = (h + 2 * padding[0] - dilation[0] * (kh - 1) - 1) // stride[0] + 1
+    wo = (w + 2 * padding[1] - dilation[1] * (kw - 1) - 1) // stride[1] + 1
+    d = ConvDesc(n, h, w, c, ho, wo, k, kh, kw, stride[0], stride[1], padding[0], padding[1],
+                 dilation[0], dilation[1], dcode(x))
+    return d
+
+
+class ConvFn(torch.autograd.Function):
+    """nn.Conv2d forward / backward (bias and LeakyReLU/ReLU epilogue optionally fused).
+
+    ``wq`` is the weight in compute dtype and kernel layout [Cout][KH][KW][Cin] (the fp32
+    parameter itself or its bf16 shadow); gradients are returned for ``weight``."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, wq, stride, padding, dilation, act):
+        require_hip(x, weight)
+        x = nhwc(x)
+        k, _, kh, kw = weight.shape
+        d = _conv_desc(x, k, kh, kw, stride, padding, dilation)
+        y = empty_nhwc(d.n, k, d.ho, d.wo, x.dtype, x.device)
+        lib.rtsds_conv2d_fwd(ctypes.byref(d), _P(x), _P(wq), _P(bias), _P(y), act, stream())
+        ctx.d, ctx.act, ctx.has_bias = d, act, bias is not None
+        ctx.save_for_backward(x, wq, y if act else None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, wq, y = ctx.saved_tensors
+        d = ctx.d
+        dy = nhwc(dy)
+        if dy.dtype != x.dtype:
+            dy = cast(dy, x.dtype)
+        if ctx.act:
+            g = torch.empty_like(dy)
+            lib.rtsds_act_bwd(_P(dy), _P(y), _P(g), dy.numel(), ctx.act, 1.0, dcode(dy), stream())
+        else:
+            g = dy
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = empty_nhwc(d.n, d.c, d.h, d.w, x.dtype, x.device)
+            ws = workspace(lib.rtsds_conv2d_dgrad_workspace(ctypes.byref(d)), x.device)
+            lib.rtsds_conv2d_dgrad(ctypes.byref(d), _P(g), _P(wq), _P(dx), 0, _P(ws), ws.numel(),
+                                   stream())
+        if ctx.needs_input_grad[1] or ctx.needs_input_grad[2]:
+            dw = torch.empty((d.k, d.c, d.kh, d.kw), dtype=torch.float32, device=x.device,
+                             memory_format=CL)
+            db = torch.empty(d.k, dtype=torch.float32, device=x.device) if ctx.has_bias else None
+            ws = workspace(lib.rtsds_conv2d_wgrad_workspace(ctypes.byref(d)), x.device)
+            lib.rtsds_conv2d_wgrad(ctypes.byref(d), _P(x), _P(g), _P(dw), _P(db), _P(ws),
+                                   ws.numel(), stream())
+            if not ctx.needs_input_grad[1]:
+                dw = None
+        return dx, dw, db, None, None, None, None, None
+
+
+def conv2d(x, weight, bias, wq, stride=(1, 1), padding=(0, 0), dilation=(1, 1), act=0):
+    return ConvFn.apply(x, weight, bias, wq, tuple(stride), tuple(padding), tuple(dilation), act)
+
+
+class ConvSumFn(torch.autograd.Function):
+    """sum_i conv_i(x) + bias_i over convs sharing x and output shape (ASPP,
+    deeplabv2.py:62-66): one output buffer accumulated in the GEMM epilogue; the backward
+    accumulates all dgrads into one dx."""
+
+    @staticmethod
+    def forward(ctx, x, geoms, *wb):
+        require_hip(x)
+        x = nhwc(x)
+        m = len(geoms)
+        weights, biases, wqs = wb[:m], wb[m:2 * m], wb[2 * m:]
+        descs = []
+        y = None
+        for i, (stride, padding, dilation) in enumerate(geoms):
+            k, _, kh, kw = weights[i].shape
+            d = _conv_desc(x, k, kh, kw, stride, padding, dilation)
+            if y is None:
+                y = empty_nhwc(d.n, k, d.ho, d.wo, x.dtype, x.device)
+            lib.rtsds_conv2d_fwd(ctypes.byref(d), _P(x), _P(wqs[i]), _P(biases[i]), _P(y),
+                                 0x100 if i else 0, stream())
+            descs.append(d)
+        ctx.descs = descs
+        ctx.has_bias = [b is not None for b in biases]
+        ctx.save_for_backward(x, *wqs)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, *wqs = ctx.saved_tensors
+        dy = nhwc(dy)
+        m = len(wqs)
+        dx = None
+        dws, dbs = [None] * m, [None] * m
+        for i, d in enumerate(ctx.descs):
+            if ctx.needs_input_grad[0]:
+                if dx is None:
+                    dx = empty_nhwc(d.n, d.c, d.h, d.w, x.dtype, x.device)
+                ws = workspace(lib.rtsds_conv2d_dgrad_workspace(ctypes.byref(d)), x.device)
+                lib.rtsds_conv2d_dgrad(ctypes.byref(d), _P(dy), _P(wqs[i]), _P(dx), 1 if i else 0,
+                                       _P(ws), ws.numel(), stream())
+            if ctx.needs_input_grad[2 + i] or ctx.needs_input_grad[2 + m + i]:
+                dw = torch.empty((d.k, d.c, d.kh, d.kw), dtype=torch.float32, device=x.device,
+                                 memory_format=CL)
+                db = torch.empty(d.k, dtype=torch.float32, device=x.device) if ctx.has_bias[i] else None
+                ws = workspace(lib.rtsds_conv2d_wgrad_workspace(ctypes.byref(d)), x.device)
+                lib.rtsds_conv2d_wgrad(ctypes.byref(d), _P(x), _P(dy), _P(dw), _P(db), _P(ws),
+                                       ws.numel(), stream())
+                dws[i] = dw if ctx.needs_input_grad[2 + i] else None
+                dbs[i] = db
+        return (dx, None, *dws, *dbs, *([None] * m))
+
+
+# ----------------------------------------------------------------------------- batch norm
+class BatchNormFn(torch.autograd.Function):
+    """BatchNorm2d (+ residual add) (+ ReLU/LeakyReLU) fused, train or eval statistics."""
+
+    @staticmethod
+    def forward(ctx, x, gamma, beta, res, running_mean, running_var, training, momentum, eps, act):
+        require_hip(x)
+        x = nhwc(x)
+        if res is not None:
+            res = nhwc(res)
+        n, c, h, w = x.shape
+        rows = n * h * w
+        y = torch.empty_like(x, memory_format=CL)
+        sm = torch.empty(c, dtype=torch.float32, device=x.device)
+        si = torch.empty(c, dtype=torch.float32, device=x.device)
+        ws = workspace(lib.rtsds_bn_workspace(rows, c), x.device)
+        lib.rtsds_bn_fwd(_P(x), _P(res), _P(y), rows, c, _P(gamma), _P(beta), _P(running_mean),
+                         _P(running_var), _P(sm), _P(si), float(momentum), float(eps), int(training),
+                         act, dcode(x), _P(ws), ws.numel(), stream())
+        ctx.meta = (rows, c, int(training), act, res is not None)
+        ctx.save_for_backward(x, y, gamma, sm, si)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, y, gamma, sm, si = ctx.saved_tensors
+        rows, c, training, act, has_res = ctx.meta
+        dy = nhwc(dy)
+        need_dx, need_g, need_b, need_r = (ctx.needs_input_grad[0], ctx.needs_input_grad[1],
+                                           ctx.needs_input_grad[2], ctx.needs_input_grad[3])
+        dx = torch.empty_like(x, memory_format=CL) if need_dx else None
+        dres = torch.empty_like(x, memory_format=CL) if (has_res and need_r) else None
+        dg = torch.empty(c, dtype=torch.float32, device=x.device) if need_g else None
+        db = torch.empty(c, dtype=torch.float32, device=x.device) if need_b else None
+        ws = workspace(lib.rtsds_bn_workspace(rows, c), x.device)
+        lib.rtsds_bn_bwd(_P(dy), _P(x), _P(y), _P(dx), _P(dres), _P(dg), _P(db), rows, c,
+                         _P(gamma), _P(sm), _P(si), training, act, dcode(x), _P(ws), ws.numel(),
+                         stream())
+        return dx, dg, db, dres, None, None, None, None, None, None
+
+
+def batch_norm(x, gamma, beta, running_mean, running_var, training, momentum, eps, act=0,
+               residual=None):
+    return BatchNormFn.apply(x, gamma, beta, residual, running_mean, running_var, training,
+                             momentum, eps, act)
+
+
+# ----------------------------------------------------------------------------- layout / dtype
+def pack_input(x, dtype):
+    """NCHW fp32 image batch (reference loaders) -> NHWC compute dtype.  No gradient."""
+    require_hip(x)
+    if x.dtype == dtype and x.dim() == 4 and x.is_contiguous(memory_format=CL) and x.shape[1] > 1:
+        return x
+    xf = x if x.dtype == torch.float32 else cast(x, torch.float32)
+    xf = xf.contiguous()
+    n, c, h, w = xf.shape
+    y = empty_nhwc(n, c, h, w, dtype, x.device)
+    lib.rtsds_nchw_to_nhwc(_P(xf), _P(y), n, c, h, w, 0 if dtype == torch.float32 else 1, stream())
+    return y
+
+
+def cast(t, dtype):
+    """dtype conversion on device, preserving the memory layout."""
+    if t.dtype == dtype:
+        return t
+    out = torch.empty_like(t, dtype=dtype)
+    if not (t.is_contiguous() or t.is_contiguous(memory_format=CL)):
+        raise RuntimeError("rtsds_amd.cast: dense tensor required")
+    if out.stride() != t.stride():
+        raise RuntimeError("rtsds_amd.cast: layout mismatch")
+    lib.rtsds_cast(_P(t), dcode(t), _P(out), dcode(out), t.numel(), stream())
+    return out
+
+
+class CatFn(torch.autograd.Function):
+    """torch.cat(dim=1) of NHWC tensors (build_bisenet.py:72,153)."""
+
+    @staticmethod
+    def forward(ctx, *xs):
+        xs = [nhwc(x) for x in xs]
+        n, _, h, w = xs[0].shape
+        ct = sum(x.shape[1] for x in xs)
+        y = empty_nhwc(n, ct, h, w, xs[0].dtype, xs[0].device)
+        off = 0
+        for x in xs:
+            c = x.shape[1]
+            lib.rtsds_copy_channels(_P(x), c, 0, _P(y), ct, off, n * h * w, c, dcode(x), stream())
+            off += c
+        ctx.split = [x.shape[1] for x in xs]
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        dy = nhwc(dy)
+        n, ct, h, w = dy.shape
+        outs, off = [], 0
+        for i, c in enumerate(ctx.split):
+            if ctx.needs_input_grad[i]:
+                g = empty_nhwc(n, c, h, w, dy.dtype, dy.device)
+                lib.rtsds_copy_channels(_P(dy), ct, off, _P(g), c, 0, n * h * w, c, dcode(dy), stream())
+                outs.append(g)
+            else:
+                outs.append(None)
+            off += c
+        return tuple(outs)
+
+
+def cat(xs):
+    return CatFn.apply(*xs)
+
+
+# ----------------------------------------------------------------------------- pointwise
+class ActFn(torch.autograd.Function):
+    """ReLU (1) / LeakyReLU(0.2) (2) / sigmoid (3)."""
+
+    @staticmethod
+    def forward(ctx, x, act):
+        require_hip(x)
+        x = x.contiguous(memory_format=CL) if x.dim() == 4 else x.contiguous()
+        y = torch.empty_like(x)
+        lib.rtsds_act_fwd(_P(x), _P(y), x.numel(), act, dcode(x), stream())
+        ctx.act = act
+        ctx.save_for_backward(y)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (y,) = ctx.saved_tensors
+        dy = dy.contiguous(memory_format=CL) if dy.dim() == 4 else dy.contiguous()
+        dx = torch.empty_like(y)
+        lib.rtsds_act_bwd(_P(dy), _P(y), _P(dx), y.numel(), ctx.act, 1.0, dcode(y), stream())
+        return dx, None
+
+
+def relu(x):
+    return ActFn.apply(x, 1)
+
+
+def leaky_relu(x):
+    return ActFn.apply(x, 2)
+
+
+def sigmoid(x):
+    return ActFn.apply(x, 3)
+
+
+class GradReverseFn(torch.autograd.Function):
+    """GradientReversalFunction (model.py:9-17): identity forward, -alpha * grad backward."""
+
+    @staticmethod
+    def forward(ctx, x, alpha):
+        ctx.alpha = float(alpha)
+        return x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, dy):
+        dy = dy.contiguous(memory_format=CL) if dy.dim() == 4 else dy.contiguous()
+        dx = torch.empty_like(dy)
+        lib.rtsds_act_bwd(_P(dy), None, _P(dx), dy.numel(), 0, -ctx.alpha, dcode(dy), stream())
+        return dx, None
+
+
+# ----------------------------------------------------------------------------- pooling
+def pool_out(size, k, s, p, ceil_mode):
+    """ATen pooling_output_shape (dilation 1)."""
+    num = size + 2 * p - (k - 1) - 1 + ((s - 1) if ceil_mode else 0)
+    o = num // s + 1
+    if ceil_mode and (o - 1) * s >= size + p:
+        o -= 1
+    return o
+
+
+class MaxPoolFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, k, s, p, ceil_mode):
+        require_hip(x)
+        x = nhwc(x)
+        n, c, h, w = x.shape
+        ho, wo = pool_out(h, k, s, p, ceil_mode), pool_out(w, k, s, p, ceil_mode)
+        y = empty_nhwc(n, c, ho, wo, x.dtype, x.device)
+        idx = torch.empty((n, ho, wo, c), dtype=torch.uint8, device=x.device)
+        lib.rtsds_maxpool_fwd(_P(x), _P(y), _P(idx), n, h, w, c, ho, wo, k, s, p, dcode(x), stream())
+        ctx.geo = (n, h, w, c, ho, wo, k, s, p)
+        ctx.dtype = x.dtype
+        ctx.save_for_backward(idx)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (idx,) = ctx.saved_tensors
+        n, h, w, c, ho, wo, k, s, p = ctx.geo
+        dy = nhwc(dy)
+        dx = empty_nhwc(n, c, h, w, dy.dtype, dy.device)
+        lib.rtsds_maxpool_bwd(_P(dy), _P(idx), _P(dx), n, h, w, c, ho, wo, k, s, p, dcode(dy), stream())
+        return dx, None, None, None, None
+
+
+def max_pool2d(x, k, s, p, ceil_mode=False):
+    return MaxPoolFn.apply(x, k, s, p, ceil_mode)
+
+
+class GapFn(torch.autograd.Function):
+    """Mean over H, W keeping dims -> [N, C, 1, 1]."""
+
+    @staticmethod
+    def forward(ctx, x):
+        require_hip(x)
+        x = nhwc(x)
+        n, c, h, w = x.shape
+        y = empty_nhwc(n, c, 1, 1, x.dtype, x.device)
+        lib.rtsds_gap_fwd(_P(x), _P(y), n, h * w, c, dcode(x), stream())
+        ctx.shape = (n, c, h, w)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        n, c, h, w = ctx.shape
+        dy = dy.contiguous()
+        dx = empty_nhwc(n, c, h, w, dy.dtype, dy.device)
+        lib.rtsds_gap_bwd(_P(dy), _P(dx), n, h * w, c, dcode(dy), stream())
+        return dx
+
+
+def global_avg_pool(x):
+    return GapFn.apply(x)
+
+
+class ChScaleFn(torch.autograd.Function):
+    """x * a[N,C,1,1] (mode 0) or x * a + x (mode 1)."""
+
+    @staticmethod
+    def forward(ctx, x, a, mode):
+        require_hip(x, a)
+        x = nhwc(x)
+        a = a.contiguous()
+        n, c, h, w = x.shape
+        if a.dtype != x.dtype:
+            a = cast(a, x.dtype)
+        y = torch.empty_like(x, memory_format=CL)
+        lib.rtsds_chscale_fwd(_P(x), _P(a), _P(y), n, h * w, c, mode, dcode(x), stream())
+        ctx.mode = mode
+        ctx.save_for_backward(x, a)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, a = ctx.saved_tensors
+        n, c, h, w = x.shape
+        dy = nhwc(dy)
+        dx = torch.empty_like(x, memory_format=CL) if ctx.needs_input_grad[0] else None
+        da = torch.empty_like(a) if ctx.needs_input_grad[1] else None
+        lib.rtsds_chscale_bwd(_P(dy), _P(x), _P(a), _P(dx), _P(da), n, h * w, c, ctx.mode,
+                              dcode(x), stream())
+        return dx, da, None
+
+
+def channel_scale(x, a, residual=False):
+    return ChScaleFn.apply(x, a, 1 if residual else 0)
+
+
+# ----------------------------------------------------------------------------- bilinear
+def _src_scale(in_size, out_size, scale_factor):
+    """ATen area_pixel_compute_scale (align_corners=False), fp32."""
+    if scale_factor is not None and scale_factor > 0:
+        return float(np.float32(1.0 / scale_factor))
+    return float(np.float32(in_size) / np.float32(out_size))
+
+
+class BilinearFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, ho, wo, sh, sw):
+        require_hip(x)
+        x = nhwc(x)
+        n, c, hi, wi = x.shape
+        y = empty_nhwc(n, c, ho, wo, x.dtype, x.device)
+        lib.rtsds_bilinear_fwd(_P(x), _P(y), n, hi, wi, c, ho, wo, sh, sw, c, 0, dcode(x), stream())
+        ctx.geo = (n, hi, wi, c, ho, wo, sh, sw)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        n, hi, wi, c, ho, wo, sh, sw = ctx.geo
+        dy = nhwc(dy)
+        dx = empty_nhwc(n, c, hi, wi, dy.dtype, dy.device)
+        lib.rtsds_bilinear_bwd(_P(dy), _P(dx), n, hi, wi, c, ho, wo, sh, sw, c, 0, dcode(dy), stream())
+        return dx, None, None, None, None
+
+
+def interpolate_bilinear(x, size=None, scale_factor=None):
+    """F.interpolate(x, size | scale_factor, mode='bilinear', align_corners=False)."""
+    hi, wi = x.shape[-2:]
+    if size is not None:
+        ho, wo = int(size[0]), int(size[1])
+        sh, sw = _src_scale(hi, ho, None), _src_scale(wi, wo, None)
+    else:
+        ho, wo = int(np.floor(hi * scale_factor)), int(np.floor(wi * scale_factor))
+        sh = sw = _src_scale(hi, ho, scale_factor)
+    return BilinearFn.apply(x, ho, wo, sh, sw)
+
+
+# ----------------------------------------------------------------------------- softmax / losses
+def _pix_strides(x):
+    """(sn, sc, shw) element strides of a [N, C, H, W] tensor whose H, W flatten."""
+    sn, sc, s_h, s_w = x.stride()
+    if x.shape[2] > 1 and s_h != x.shape[3] * s_w:
+        raise RuntimeError("rtsds_amd: logits must have flattenable H, W")
+    return sn, sc, s_w
+
+
+class SoftmaxFn(torch.autograd.Function):
+    """F.softmax(x, dim=1) (train.py:225,245,256); output NHWC."""
+
+    @staticmethod
+    def forward(ctx, x):
+        require_hip(x)
+        n, c, h, w = x.shape
+        sn, sc, shw = _pix_strides(x)
+        y = empty_nhwc(n, c, h, w, x.dtype, x.device)
+        lib.rtsds_softmax_fwd(_P(x), sn, sc, shw, _P(y), c, n, h * w, c, dcode(x), stream())
+        ctx.save_for_backward(y)
+        ctx.xlayout = (x.stride(), x.dtype)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (y,) = ctx.saved_tensors
+        n, c, h, w = y.shape
+        dy = nhwc(dy)
+        if dy.dtype != y.dtype:
+            dy = cast(dy, y.dtype)
+        dx = empty_nhwc(n, c, h, w, y.dtype, y.device)
+        sn, sc, shw = _pix_strides(dx)
+        lib.rtsds_softmax_bwd(_P(dy), _P(y), c, _P(dx), sn, sc, shw, n, h * w, c, dcode(y), stream())
+        return dx
+
+
+def softmax(x, dim=1):
+    if dim != 1:
+        raise NotImplementedError("rtsds_amd.softmax: only dim=1 (channels) is on the hot path")
+    return SoftmaxFn.apply(x)
+
+
+class CrossEntropyFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, target, ignore_index):
+        require_hip(x, target)
+        if target.dim() == 4:
+            target = target.squeeze(1)
+        target = target.contiguous()
+        if target.dtype != torch.int64:
+            target = target.long()
+        n, c, h, w = x.shape
+        if tuple(target.shape) != (n, h, w):
+            raise RuntimeError(f"rtsds_amd: target shape {tuple(target.shape)} != {(n, h, w)}")
+        sn, sc, shw = _pix_strides(x)
+        loss = torch.empty((), dtype=torch.float32, device=x.device)
+        ws = workspace(lib.rtsds_ce_workspace(), x.device)
+        lib.rtsds_ce_fwd(_P(x), sn, sc, shw, _P(target), _P(loss), n, h * w, c, ignore_index,
+                         dcode(x), _P(ws), ws.numel(), stream())
+        ctx.ignore = ignore_index
+        ctx.save_for_backward(x, target, ws)
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        x, target, ws = ctx.saved_tensors
+        n, c, h, w = x.shape
+        sn, sc, shw = _pix_strides(x)
+        dx = torch.empty_strided(x.shape, x.stride(), dtype=x.dtype, device=x.device)
+        g = g.contiguous().float()
+        count = ws.view(torch.float32)[2048:2049]
+        lib.rtsds_ce_bwd(_P(x), sn, sc, shw, _P(target), _P(g), _P(count), _P(dx), n, h * w, c,
+                         ctx.ignore, dcode(x), stream())
+        return dx, None, None
+
+
+def cross_entropy(x, target, ignore_index=-100):
+    return CrossEntropyFn.apply(x, target, ignore_index)
+
+
+class BCEWithLogitsFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, target):
+        require_hip(x, target)
+        xf = cast(x.contiguous(), torch.float32)
+        tf = cast(target.contiguous(), torch.float32) if target.dtype != torch.float32 else target.contiguous()
+        loss = torch.empty((), dtype=torch.float32, device=x.device)
+        lib.rtsds_bce_fwd(_P(xf), _P(tf), _P(loss), xf.numel(), stream())
+        ctx.xdtype = x.dtype
+        ctx.save_for_backward(xf, tf)
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        xf, tf = ctx.saved_tensors
+        dx = torch.empty_like(xf)
+        lib.rtsds_bce_bwd(_P(xf), _P(tf), _P(g.contiguous().float()), _P(dx), xf.numel(), stream())
+        return cast(dx, ctx.xdtype), None
+
+
+def bce_with_logits(x, target):
+    return BCEWithLogitsFn.apply(x, target)
+
+
+# ----------------------------------------------------------------------------- metrics
+def argmax_channels(x, target=None, correct=None, want_map=True):
+    """argmax over dim 1 (first max wins) -> int64 [N, H, W]; optionally adds the number of
+    pixels equal to ``target`` into the device counter ``correct`` (uint64 view)."""
+    require_hip(x)
+    n, c, h, w = x.shape
+    sn, sc, shw = _pix_strides(x)
+    out = torch.empty((n, h, w), dtype=torch.int64, device=x.device) if want_map else None
+    t = None
+    if target is not None:
+        t = target.squeeze(1) if target.dim() == 4 else target
+        t = t.contiguous().long()
+    lib.rtsds_argmax(_P(x), sn, sc, shw, _P(out), _P(t), _P(correct), n, h * w, c, dcode(x), stream())
+    return out
+
+
+def confusion(label, pred, hist, nc):
+    lib.rtsds_confusion(_P(label.contiguous()), _P(pred.contiguous()), _P(hist), label.numel(), nc,
+                        stream())

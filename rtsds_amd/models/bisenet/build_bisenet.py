@@ -1,0 +1,143 @@
+"""BiSeNet on the MI355X kernels -- drop-in for the reference's models/bisenet/build_bisenet.py.
+
+Same classes, constructor arguments, attribute names (including the reference's
+``saptial_path`` spelling), ``state_dict`` keys and train/eval output contract
+(build_bisenet.py:141-172: training -> (result, cx1_sup, cx2_sup), eval -> result).
+The forward runs NHWC in the runtime compute dtype with these fusions:
+conv epilogues carry bias + ReLU/sigmoid, BatchNorm carries ReLU / sigmoid (ARM) and the
+cat / channel-attention scaling are single kernels.  Input: NCHW fp32 images on a HIP
+device; outputs: [N, num_classes, H, W] tensors in channels_last memory.
+"""
+import torch
+from torch import nn
+
+from rtsds_amd import functional as F
+from rtsds_amd.nn import AdaptiveAvgPool2d, BatchNorm2d, Conv2d, ReLU, Sigmoid, to_input
+from .build_contextpath import build_contextpath
+
+
+class ConvBlock(torch.nn.Module):
+    """conv(no bias) -> BN -> ReLU (build_bisenet.py:8-18); BN+ReLU fused."""
+
+    def __init__(self, in_channels, out_channels, kernel_size=3, stride=2, padding=1):
+        super().__init__()
+        self.conv1 = Conv2d(in_channels, out_channels, kernel_size=kernel_size, stride=stride,
+                            padding=padding, bias=False)
+        self.bn = BatchNorm2d(out_channels)
+        self.relu = ReLU()
+
+    def forward(self, input):
+        return self.bn(self.conv1(input), act="relu")
+
+
+class Spatial_path(torch.nn.Module):
+    """build_bisenet.py:21-32."""
+
+    def __init__(self):
+        super().__init__()
+        self.convblock1 = ConvBlock(in_channels=3, out_channels=64)
+        self.convblock2 = ConvBlock(in_channels=64, out_channels=128)
+        self.convblock3 = ConvBlock(in_channels=128, out_channels=256)
+
+    def forward(self, input):
+        return self.convblock3(self.convblock2(self.convblock1(input)))
+
+
+class AttentionRefinementModule(torch.nn.Module):
+    """GAP -> 1x1 conv(bias) -> BN -> sigmoid -> x*a (build_bisenet.py:35-53).
+    BN+sigmoid fused; BN statistics are over the N pooled vectors, as in the reference."""
+
+    def __init__(self, in_channels, out_channels):
+        super().__init__()
+        self.conv = Conv2d(in_channels, out_channels, kernel_size=1)
+        self.bn = BatchNorm2d(out_channels)
+        self.sigmoid = Sigmoid()
+        self.in_channels = in_channels
+        self.avgpool = AdaptiveAvgPool2d(output_size=(1, 1))
+
+    def forward(self, input):
+        pooled = self.avgpool(input)
+        assert self.in_channels == pooled.size(1), \
+            "in_channels and out_channels should all be {}".format(pooled.size(1))
+        att = self.bn(self.conv(pooled), act="sigmoid")
+        return F.channel_scale(input, att)
+
+
+class FeatureFusionModule(torch.nn.Module):
+    """build_bisenet.py:56-81: cat -> ConvBlock(s1) -> GAP -> 1x1+ReLU -> 1x1+sigmoid -> f*a + f."""
+
+    def __init__(self, num_classes, in_channels):
+        super().__init__()
+        self.in_channels = in_channels
+        self.convblock = ConvBlock(in_channels=self.in_channels, out_channels=num_classes, stride=1)
+        self.conv1 = Conv2d(num_classes, num_classes, kernel_size=1)
+        self.relu = ReLU()
+        self.conv2 = Conv2d(num_classes, num_classes, kernel_size=1)
+        self.sigmoid = Sigmoid()
+        self.avgpool = AdaptiveAvgPool2d(output_size=(1, 1))
+
+    def forward(self, input_1, input_2):
+        x = F.cat([input_1, input_2])
+        assert self.in_channels == x.size(1), \
+            "in_channels of ConvBlock should be {}".format(x.size(1))
+        feature = self.convblock(x)
+        att = self.conv2(self.conv1(self.avgpool(feature), act="relu"), act="sigmoid")
+        return F.channel_scale(feature, att, residual=True)
+
+
+_HEADS = {"resnet18": (256, 512), "resnet101": (1024, 2048)}
+
+
+class BiSeNet(torch.nn.Module):
+    """build_bisenet.py:84-172."""
+
+    def __init__(self, num_classes, context_path, with_interpolation=True):
+        super().__init__()
+        self.with_interpolation = with_interpolation
+        self.saptial_path = Spatial_path()
+        self.context_path = build_contextpath(name=context_path)
+        if context_path not in _HEADS:
+            print("Error: unspport context_path network \n")
+        c3, c4 = _HEADS.get(context_path, (256, 512))
+        self.attention_refinement_module1 = AttentionRefinementModule(c3, c3)
+        self.attention_refinement_module2 = AttentionRefinementModule(c4, c4)
+        self.supervision1 = Conv2d(in_channels=c3, out_channels=num_classes, kernel_size=1)
+        self.supervision2 = Conv2d(in_channels=c4, out_channels=num_classes, kernel_size=1)
+        self.feature_fusion_module = FeatureFusionModule(num_classes, 256 + c3 + c4)
+        self.conv = Conv2d(in_channels=num_classes, out_channels=num_classes, kernel_size=1)
+        self.init_weight()
+        self.mul_lr = [self.saptial_path, self.attention_refinement_module1,
+                       self.attention_refinement_module2, self.supervision1, self.supervision2,
+                       self.feature_fusion_module, self.conv]
+
+    def init_weight(self):
+        """kaiming fan_in on every conv outside the context path; BN 1/0 (build_bisenet.py:130-139)."""
+        for name, m in self.named_modules():
+            if "context_path" in name:
+                continue
+            if isinstance(m, nn.Conv2d):
+                nn.init.kaiming_normal_(m.weight, mode="fan_in", nonlinearity="relu")
+            elif isinstance(m, nn.BatchNorm2d):
+                m.eps, m.momentum = 1e-5, 0.1
+                nn.init.constant_(m.weight, 1)
+                nn.init.constant_(m.bias, 0)
+
+    def forward(self, input):
+        x = to_input(input)
+        sx = self.saptial_path(x)
+        f3, f4, tail = self.context_path(x)
+        cx1 = self.attention_refinement_module1(f3)
+        cx2 = F.channel_scale(self.attention_refinement_module2(f4), tail)
+        hw = sx.shape[-2:]
+        cx1 = F.interpolate_bilinear(cx1, size=hw)
+        cx2 = F.interpolate_bilinear(cx2, size=hw)
+        if self.training:
+            full = input.shape[-2:]
+            cx1_sup = F.interpolate_bilinear(self.supervision1(cx1), size=full)
+            cx2_sup = F.interpolate_bilinear(self.supervision2(cx2), size=full)
+        result = self.feature_fusion_module(sx, F.cat([cx1, cx2]))
+        if self.with_interpolation:
+            result = self.conv(F.interpolate_bilinear(result, scale_factor=8))
+        if self.training:
+            return result, cx1_sup, cx2_sup
+        return result

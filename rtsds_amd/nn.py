@@ -1,0 +1,121 @@
+"""torch.nn-compatible layers whose forward/backward run on librtsds_hip.so.
+
+``Conv2d`` / ``BatchNorm2d`` subclass the torch classes so parameters, buffers,
+``state_dict`` keys and ``isinstance`` checks (e.g. build_bisenet.py:130-139) are exactly the
+reference's; only ``forward`` differs.  Conv weights are stored channels_last, i.e. in the
+kernel's [Cout][KH][KW][Cin] layout, with the logical shape [Cout, Cin, KH, KW] unchanged.
+Extra keyword ``act`` fuses a following ReLU / LeakyReLU / sigmoid into the epilogue.
+"""
+import torch
+from torch import nn
+
+from . import functional as F
+from ._lib import lib
+from .runtime import CL, compute_dtype
+
+ACT = {None: 0, "relu": 1, "leaky": 2, "sigmoid": 3}
+
+
+def _shadow(w, dtype):
+    """Weight in compute dtype and kernel layout.  bf16 shadows are cached on the parameter
+    and refreshed when its storage or version changes (or written directly by rtsds Adam)."""
+    if dtype == torch.float32:
+        return w.detach() if w.is_contiguous(memory_format=CL) else w.detach().contiguous(memory_format=CL)
+    sh = getattr(w, "_rt_shadow", None)
+    key = (w.data_ptr(), w._version)
+    if sh is not None and getattr(w, "_rt_shadow_key", None) == key and sh.device == w.device:
+        return sh
+    if sh is None or sh.shape != w.shape or sh.device != w.device:
+        sh = torch.empty(w.shape, dtype=torch.bfloat16, device=w.device, memory_format=CL)
+    src = w.detach()
+    if not src.is_contiguous(memory_format=CL):
+        src = src.contiguous(memory_format=CL)
+    lib.rtsds_cast(src.data_ptr(), 0, sh.data_ptr(), 1, src.numel(), torch.cuda.current_stream().cuda_stream)
+    w._rt_shadow, w._rt_shadow_key = sh, key
+    return sh
+
+
+class Conv2d(nn.Conv2d):
+    def __init__(self, *args, **kwargs):
+        super().__init__(*args, **kwargs)
+        if self.groups != 1 or self.padding_mode != "zeros":
+            raise NotImplementedError("rtsds_amd.Conv2d: groups=1, zero padding only")
+        self.weight.data = self.weight.data.contiguous(memory_format=CL)
+
+    def _apply(self, fn, *a, **k):
+        out = super()._apply(fn, *a, **k)
+        if not self.weight.is_contiguous(memory_format=CL):
+            self.weight.data = self.weight.data.contiguous(memory_format=CL)
+        return out
+
+    def forward(self, x, act=None):
+        wq = _shadow(self.weight, x.dtype)
+        return F.conv2d(x, self.weight, self.bias, wq, self.stride, self.padding, self.dilation,
+                        ACT[act])
+
+
+class BatchNorm2d(nn.BatchNorm2d):
+    def forward(self, x, act=None, residual=None):
+        training = self.training or not self.track_running_stats
+        if training and x.shape[0] * x.shape[2] * x.shape[3] == 1:
+            raise ValueError(f"Expected more than 1 value per channel when training, got input size {tuple(x.shape)}")
+        if self.momentum is None:
+            raise NotImplementedError("rtsds_amd.BatchNorm2d: cumulative moving average (momentum=None)")
+        if self.training and self.track_running_stats:
+            self.num_batches_tracked.add_(1)
+        rm = self.running_mean if self.track_running_stats else None
+        rv = self.running_var if self.track_running_stats else None
+        return F.batch_norm(x, self.weight, self.bias, rm, rv, training, self.momentum, self.eps,
+                            ACT[act], residual)
+
+
+class ReLU(nn.Module):
+    def __init__(self, inplace=False):
+        super().__init__()
+        self.inplace = inplace
+
+    def forward(self, x):
+        return F.relu(x)
+
+
+class LeakyReLU(nn.Module):
+    def __init__(self, negative_slope=0.2):
+        super().__init__()
+        if negative_slope != 0.2:
+            raise NotImplementedError("rtsds_amd.LeakyReLU: slope 0.2 (model.py:62,73)")
+        self.negative_slope = negative_slope
+
+    def forward(self, x):
+        return F.leaky_relu(x)
+
+
+class Sigmoid(nn.Module):
+    def forward(self, x):
+        return F.sigmoid(x)
+
+
+class AdaptiveAvgPool2d(nn.Module):
+    def __init__(self, output_size=(1, 1)):
+        super().__init__()
+        osz = (output_size, output_size) if isinstance(output_size, int) else tuple(output_size)
+        if osz != (1, 1):
+            raise NotImplementedError("rtsds_amd.AdaptiveAvgPool2d: output (1, 1) only")
+        self.output_size = output_size
+
+    def forward(self, x):
+        return F.global_avg_pool(x)
+
+
+class MaxPool2d(nn.Module):
+    def __init__(self, kernel_size, stride=None, padding=0, ceil_mode=False):
+        super().__init__()
+        self.kernel_size, self.stride = kernel_size, stride or kernel_size
+        self.padding, self.ceil_mode = padding, ceil_mode
+
+    def forward(self, x):
+        return F.max_pool2d(x, self.kernel_size, self.stride, self.padding, self.ceil_mode)
+
+
+def to_input(x):
+    """Reference-layout NCHW fp32 batch -> NHWC in the runtime compute dtype."""
+    return F.pack_input(x, compute_dtype())

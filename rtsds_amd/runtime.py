@@ -1,0 +1,73 @@
+"""Process-wide runtime settings and helpers for the HIP path.
+
+* compute dtype: ``float32`` (default; exact-f32 MFMA, the parity mode) or ``bfloat16``
+  (bf16 activations / weight shadows, fp32 accumulation, statistics and master weights).
+* tensor helpers: NHWC ("channels_last") allocation, stream handle, HIP-only guard.
+"""
+import contextlib
+
+import torch
+
+_state = {"dtype": torch.float32}
+
+
+def set_compute_dtype(dtype):
+    if dtype not in (torch.float32, torch.bfloat16):
+        raise ValueError("compute dtype must be torch.float32 or torch.bfloat16")
+    _state["dtype"] = dtype
+
+
+def compute_dtype():
+    return _state["dtype"]
+
+
+@contextlib.contextmanager
+def precision(dtype):
+    old = _state["dtype"]
+    set_compute_dtype(dtype)
+    try:
+        yield
+    finally:
+        _state["dtype"] = old
+
+
+def dcode(t):
+    """torch dtype -> RTSDS_F32 / RTSDS_BF16."""
+    if t.dtype == torch.float32:
+        return 0
+    if t.dtype == torch.bfloat16:
+        return 1
+    raise RuntimeError(f"rtsds_amd: unsupported dtype {t.dtype}")
+
+
+def stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def require_hip(*tensors):
+    for t in tensors:
+        if t is not None and not t.is_cuda:
+            raise RuntimeError("rtsds_amd: ops run only on HIP (MI355X) tensors; "
+                               "there is no CPU fallback (move the model / data to 'cuda')")
+
+
+CL = torch.channels_last
+
+
+def empty_nhwc(n, c, h, w, dtype, device):
+    return torch.empty((n, c, h, w), dtype=dtype, device=device, memory_format=CL)
+
+
+def is_nhwc(t):
+    return t.dim() == 4 and t.is_contiguous(memory_format=CL)
+
+
+def nhwc(t):
+    """Return ``t`` with NHWC memory (no copy when it already is)."""
+    if is_nhwc(t):
+        return t
+    return t.contiguous(memory_format=CL)
+
+
+def workspace(nbytes, device):
+    return torch.empty(max(int(nbytes), 16), dtype=torch.uint8, device=device)

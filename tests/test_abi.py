@@ -1,0 +1,50 @@
+"""C-ABI boundary checks (CPU): the library builds/loads without a GPU, exports every
+function include/rtsds_hip.h declares, and the ctypes signatures agree with the header."""
+import os
+import re
+
+import pytest
+
+from rtsds_amd import _lib
+
+HDR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "rtsds_hip.h")
+
+
+def _declarations():
+    text = open(HDR).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    decls = {}
+    for m in re.finditer(r"\b(int|size_t)\s+(rtsds_\w+)\s*\(([^)]*)\)\s*;", text):
+        args = m.group(3).strip()
+        n = 0 if args in ("", "void") else len(args.split(","))
+        decls[m.group(2)] = (m.group(1), n)
+    return decls
+
+
+def test_header_parses():
+    d = _declarations()
+    assert "rtsds_conv2d_fwd" in d and len(d) >= 30
+
+
+def test_library_exports_every_declared_symbol():
+    lib = _lib.load()
+    for name in _declarations():
+        assert hasattr(lib, name), name
+
+
+@pytest.mark.parametrize("name", sorted(_declarations()))
+def test_ctypes_signature_matches_header(name):
+    ret, nargs = _declarations()[name]
+    assert name in _lib.SIGNATURES, f"{name} not bound in rtsds_amd/_lib.py"
+    res, args = _lib.SIGNATURES[name]
+    assert len(args) == nargs, (name, len(args), nargs)
+    assert (res is _lib.c_size_t) == (ret == "size_t"), name
+
+
+def test_errors_raise_without_fallback():
+    # the product path refuses CPU tensors instead of silently computing elsewhere
+    import torch
+    from rtsds_amd import functional as F
+    x = torch.zeros(1, 3, 8, 8)
+    with pytest.raises(RuntimeError, match="HIP"):
+        F.pack_input(x, torch.float32)

@@ -1,0 +1,309 @@
+"""Per-op parity of the HIP kernels against the ATen CPU ops the reference calls
+(torch.nn.functional on CPU, float64) -- forward and backward.  GPU only.
+
+Tolerances: fp32 mode (exact-f32 MFMA) max|err| <= 1e-4 * max|ref| (+ tiny abs floor);
+bf16 mode 3e-2 * max|ref| (bf16 operands, fp32 accumulation).
+"""
+import pytest
+import torch
+import torch.nn.functional as TF
+
+pytestmark = pytest.mark.gpu
+
+if not torch.cuda.is_available():  # pragma: no cover
+    pytest.skip("no HIP device", allow_module_level=True)
+
+from rtsds_amd import functional as F  # noqa: E402
+from rtsds_amd.nn import _shadow  # noqa: E402
+
+DEV = "cuda"
+CL = torch.channels_last
+TOL = {torch.float32: 2e-4, torch.bfloat16: 3e-2}
+
+
+def _close(got, ref, dt, what, tol=None):
+    got = got.detach().double().cpu()
+    ref = ref.detach().double().cpu()
+    assert got.shape == ref.shape, (what, got.shape, ref.shape)
+    scale = ref.abs().max().item() + 1e-12
+    err = (got - ref).abs().max().item()
+    t = tol if tol is not None else TOL[dt]
+    assert err <= t * scale + 1e-6, f"{what}: max err {err:.3e} vs scale {scale:.3e} (tol {t})"
+
+
+def _dev(t, dt):
+    return t.to(DEV, dt).contiguous(memory_format=CL)
+
+
+CONV_CASES = [
+    # n, c, h, w, k, kh, stride, pad, dil, bias
+    (2, 3, 32, 48, 64, 7, 2, 3, 1, False),     # ResNet stem (Cin=3, scalar gather)
+    (2, 3, 32, 32, 64, 3, 2, 1, 1, False),     # spatial path conv1
+    (2, 64, 16, 24, 64, 3, 1, 1, 1, False),    # BasicBlock 3x3
+    (2, 64, 16, 16, 128, 3, 2, 1, 1, False),   # stride-2 3x3
+    (2, 64, 16, 16, 128, 1, 2, 0, 1, False),   # downsample 1x1 s2
+    (2, 19, 32, 64, 64, 4, 2, 1, 1, True),     # TinyD conv1 (Cin=19)
+    (2, 64, 16, 32, 1, 4, 2, 1, 1, True),      # D classifier (Cout=1)
+    (1, 64, 13, 17, 64, 3, 1, 2, 2, False),    # atrous d=2, odd sizes
+    (1, 128, 9, 11, 19, 3, 1, 6, 6, True),     # ASPP-like, Cout=19
+    (2, 19, 16, 16, 19, 1, 1, 0, 1, True),     # final 1x1 19->19
+    (8, 256, 1, 1, 256, 1, 1, 0, 1, True),     # ARM 1x1 on pooled vectors
+    (2, 1024, 8, 16, 19, 3, 1, 1, 1, False),   # FFM conv (K=9216, N=19)
+    (2, 256, 8, 8, 512, 3, 2, 1, 1, False),    # layer4 conv1
+]
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv_fwd_bwd(case, dt):
+    n, c, h, w, k, kh, s, p, d, bias = case
+    g = torch.Generator().manual_seed(hash(case) & 0xFFFF)
+    x = torch.randn(n, c, h, w, generator=g, dtype=torch.float64)
+    wt = torch.randn(k, c, kh, kh, generator=g, dtype=torch.float64) / (c * kh * kh) ** 0.5
+    b = torch.randn(k, generator=g, dtype=torch.float64) if bias else None
+    if dt == torch.bfloat16:  # compare against the bf16-rounded operands
+        x, wt = x.bfloat16().double(), wt.bfloat16().double()
+    xr, wr = x.clone().requires_grad_(), wt.clone().requires_grad_()
+    br = b.clone().requires_grad_() if bias else None
+    yr = TF.conv2d(xr, wr, br, s, p, d)
+    gy = torch.randn(yr.shape, generator=g, dtype=torch.float64)
+    if dt == torch.bfloat16:
+        gy = gy.bfloat16().double()
+    yr.backward(gy)
+
+    xd = _dev(x, dt).requires_grad_()
+    wp = torch.nn.Parameter(wt.float().to(DEV).contiguous(memory_format=CL))
+    bp = torch.nn.Parameter(b.float().to(DEV)) if bias else None
+    y = F.conv2d(xd, wp, bp, _shadow(wp, dt), (s, s), (p, p), (d, d), 0)
+    y.backward(_dev(gy, dt))
+    torch.cuda.synchronize()
+    _close(y, yr, dt, "y")
+    _close(xd.grad, xr.grad, dt, "dx")
+    _close(wp.grad, wr.grad, dt, "dw")
+    if bias:
+        _close(bp.grad, br.grad, dt, "db")
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("act", [0, 1, 2])
+def test_conv_fused_act(dt, act):
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(2, 64, 12, 12, generator=g, dtype=torch.float64)
+    wt = torch.randn(32, 64, 3, 3, generator=g, dtype=torch.float64) / 24
+    b = torch.randn(32, generator=g, dtype=torch.float64)
+    if dt == torch.bfloat16:
+        x, wt = x.bfloat16().double(), wt.bfloat16().double()
+    xr, wr, br = x.clone().requires_grad_(), wt.clone().requires_grad_(), b.clone().requires_grad_()
+    yr = TF.conv2d(xr, wr, br, 1, 1)
+    yr = [yr, TF.relu(yr), TF.leaky_relu(yr, 0.2)][act]
+    yr.sum().backward()
+    xd = _dev(x, dt).requires_grad_()
+    wp = torch.nn.Parameter(wt.float().to(DEV).contiguous(memory_format=CL))
+    bp = torch.nn.Parameter(b.float().to(DEV))
+    y = F.conv2d(xd, wp, bp, _shadow(wp, dt), (1, 1), (1, 1), (1, 1), act)
+    y.backward(torch.ones_like(y))
+    _close(y, yr, dt, "y")
+    _close(xd.grad, xr.grad, dt, "dx")
+    _close(wp.grad, wr.grad, dt, "dw")
+    _close(bp.grad, br.grad, dt, "db")
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("shape,act,res", [((4, 64, 8, 12), 1, False), ((2, 128, 5, 7), 1, True),
+                                           ((8, 512, 1, 1), 3, False), ((2, 19, 9, 9), 1, False),
+                                           ((3, 2048, 3, 3), 0, True)])
+def test_batchnorm_train(shape, act, res, dt):
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn(shape, generator=g, dtype=torch.float64) * 3 + 50  # large mean
+    r = torch.randn(shape, generator=g, dtype=torch.float64)
+    c = shape[1]
+    gam = 1 + 0.1 * torch.randn(c, generator=g, dtype=torch.float64)
+    bet = 0.1 * torch.randn(c, generator=g, dtype=torch.float64)
+    if dt == torch.bfloat16:
+        x, r = x.bfloat16().double(), r.bfloat16().double()
+    rm0 = 0.1 * torch.randn(c, generator=g, dtype=torch.float64)
+    rv0 = 1 + torch.rand(c, generator=g, dtype=torch.float64)
+    xr, gr, br = x.clone().requires_grad_(), gam.clone().requires_grad_(), bet.clone().requires_grad_()
+    rr = r.clone().requires_grad_()
+    rm, rv = rm0.clone(), rv0.clone()
+    yr = TF.batch_norm(xr, rm, rv, gr, br, True, 0.1, 1e-5)
+    if res:
+        yr = yr + rr
+    yr = [yr, TF.relu(yr), None, torch.sigmoid(yr)][act]
+    gy = torch.randn(shape, generator=g, dtype=torch.float64)
+    yr.backward(gy)
+
+    xd = _dev(x, dt).requires_grad_()
+    rd = _dev(r, dt).requires_grad_() if res else None
+    gp = gam.float().to(DEV).requires_grad_()
+    bp = bet.float().to(DEV).requires_grad_()
+    rmd, rvd = rm0.float().to(DEV), rv0.float().to(DEV)
+    y = F.batch_norm(xd, gp, bp, rmd, rvd, True, 0.1, 1e-5, act, rd)
+    y.backward(_dev(gy, dt))
+    tol = 5e-4 if dt == torch.float32 else None
+    _close(y, yr, dt, "y", tol)
+    _close(xd.grad, xr.grad, dt, "dx", 2e-3 if dt == torch.float32 else 6e-2)
+    _close(gp.grad, gr.grad, dt, "dgamma", 2e-3 if dt == torch.float32 else 6e-2)
+    _close(bp.grad, br.grad, dt, "dbeta", tol)
+    if res:
+        _close(rd.grad, rr.grad, dt, "dres", tol)
+    _close(rmd, rm, torch.float32, "running_mean", 1e-4)
+    _close(rvd, rv, torch.float32, "running_var", 1e-3)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_batchnorm_eval(dt):
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(2, 64, 6, 6, generator=g, dtype=torch.float64)
+    rm, rv = torch.randn(64, generator=g, dtype=torch.float64), 1 + torch.rand(64, generator=g, dtype=torch.float64)
+    gam, bet = torch.randn(64, generator=g, dtype=torch.float64), torch.randn(64, generator=g, dtype=torch.float64)
+    if dt == torch.bfloat16:
+        x = x.bfloat16().double()
+    yr = TF.relu(TF.batch_norm(x, rm, rv, gam, bet, False, 0.1, 1e-5))
+    y = F.batch_norm(_dev(x, dt), gam.float().to(DEV), bet.float().to(DEV), rm.float().to(DEV),
+                     rv.float().to(DEV), False, 0.1, 1e-5, 1, None)
+    _close(y, yr, dt, "y", 1e-4 if dt == torch.float32 else None)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("geo", [(3, 2, 1, False, 17, 23), (3, 2, 1, True, 17, 23), (3, 2, 1, True, 16, 16)])
+def test_maxpool(geo, dt):
+    k, s, p, ceil, h, w = geo
+    g = torch.Generator().manual_seed(1)
+    x = torch.randn(2, 8, h, w, generator=g, dtype=torch.float64)
+    if dt == torch.bfloat16:
+        x = x.bfloat16().double()
+    xr = x.clone().requires_grad_()
+    yr = TF.max_pool2d(xr, k, s, p, ceil_mode=ceil)
+    gy = torch.randn(yr.shape, generator=g, dtype=torch.float64)
+    yr.backward(gy)
+    xd = _dev(x, dt).requires_grad_()
+    y = F.max_pool2d(xd, k, s, p, ceil)
+    y.backward(_dev(gy, dt))
+    _close(y, yr, dt, "y", 0.0)
+    _close(xd.grad, xr.grad, dt, "dx", 1e-6 if dt == torch.float32 else 1e-2)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("geo", [((4, 8), (16, 32), None), ((16, 32), None, 8), ((65, 129), (512, 1024), None),
+                                 ((5, 7), (9, 13), None), ((8, 8), (8, 8), None)])
+def test_bilinear(geo, dt):
+    (hi, wi), size, sf = geo
+    g = torch.Generator().manual_seed(2)
+    x = torch.randn(2, 5, hi, wi, generator=g, dtype=torch.float64)
+    if dt == torch.bfloat16:
+        x = x.bfloat16().double()
+    xr = x.clone().requires_grad_()
+    yr = TF.interpolate(xr, size=size, scale_factor=sf, mode="bilinear")
+    gy = torch.randn(yr.shape, generator=g, dtype=torch.float64)
+    yr.backward(gy)
+    xd = _dev(x, dt).requires_grad_()
+    y = F.interpolate_bilinear(xd, size=size, scale_factor=sf)
+    y.backward(_dev(gy, dt))
+    _close(y, yr, dt, "y", 1e-5 if dt == torch.float32 else 1e-2)
+    _close(xd.grad, xr.grad, dt, "dx", 1e-5 if dt == torch.float32 else 2e-2)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_gap_chscale_cat_act(dt):
+    g = torch.Generator().manual_seed(4)
+    x = torch.randn(3, 24, 7, 9, generator=g, dtype=torch.float64)
+    x2 = torch.randn(3, 16, 7, 9, generator=g, dtype=torch.float64)
+    if dt == torch.bfloat16:
+        x, x2 = x.bfloat16().double(), x2.bfloat16().double()
+    xr, x2r = x.clone().requires_grad_(), x2.clone().requires_grad_()
+    a_r = torch.sigmoid(xr.mean((2, 3), keepdim=True))
+    yr = torch.cat((xr * a_r + xr, x2r), 1)
+    yr = TF.relu(yr)
+    gy = torch.randn(yr.shape, generator=g, dtype=torch.float64)
+    yr.backward(gy)
+    xd, x2d = _dev(x, dt).requires_grad_(), _dev(x2, dt).requires_grad_()
+    a = F.sigmoid(F.global_avg_pool(xd))
+    y = F.relu(F.cat([F.channel_scale(xd, a, residual=True), x2d]))
+    y.backward(_dev(gy, dt))
+    _close(y, yr, dt, "y", 1e-5 if dt == torch.float32 else 2e-2)
+    _close(xd.grad, xr.grad, dt, "dx", 1e-4 if dt == torch.float32 else 5e-2)
+    _close(x2d.grad, x2r.grad, dt, "dx2", 1e-6 if dt == torch.float32 else 1e-2)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_softmax_ce_argmax(dt):
+    g = torch.Generator().manual_seed(9)
+    x = torch.randn(2, 19, 12, 20, generator=g, dtype=torch.float64) * 3
+    t = torch.randint(0, 20, (2, 12, 20), generator=g)
+    if dt == torch.bfloat16:
+        x = x.bfloat16().double()
+    xr = x.clone().requires_grad_()
+    lr = TF.cross_entropy(xr, t, ignore_index=19)
+    sr = torch.softmax(xr, 1)
+    gs = torch.randn(sr.shape, generator=g, dtype=torch.float64)
+    (lr * 2.0 + (sr * gs).sum()).backward()
+
+    xd = _dev(x, dt).requires_grad_()
+    td = t.to(DEV)
+    loss = F.cross_entropy(xd, td, ignore_index=19)
+    s = F.softmax(xd, 1)
+    loss.backward(torch.tensor(2.0, device=DEV), retain_graph=True)
+    s.backward(_dev(gs, dt))
+    _close(loss, lr, torch.float32, "ce", 1e-5 if dt == torch.float32 else 1e-2)
+    _close(s, sr, dt, "softmax", 1e-5 if dt == torch.float32 else 1e-2)
+    _close(xd.grad, xr.grad, dt, "dx", 1e-5 if dt == torch.float32 else 3e-2)
+
+    # NCHW-strided logits work too
+    xn = x.float().to(DEV).requires_grad_()
+    ln = F.cross_entropy(xn, td, ignore_index=19)
+    ln.backward()
+    _close(ln, TF.cross_entropy(x, t, ignore_index=19), torch.float32, "ce_nchw", 1e-5)
+
+    correct = torch.zeros(1, dtype=torch.int64, device=DEV)
+    am = F.argmax_channels(_dev(x, torch.float32), td, correct)
+    ref = x.argmax(1)
+    assert torch.equal(am.cpu(), ref)
+    assert int(correct.item()) == int((ref == t).sum())
+
+
+def test_bce():
+    g = torch.Generator().manual_seed(6)
+    x = torch.randn(8, 1, 1, 1, generator=g, dtype=torch.float64) * 4
+    for tv in (0.0, 1.0):
+        t = torch.full_like(x, tv)
+        xr = x.clone().requires_grad_()
+        lr = TF.binary_cross_entropy_with_logits(xr, t)
+        lr.backward()
+        xd = x.float().to(DEV).requires_grad_()
+        l = F.bce_with_logits(xd, t.float().to(DEV))
+        l.backward()
+        _close(l, lr, torch.float32, "bce", 1e-6)
+        _close(xd.grad, xr.grad, torch.float32, "dx", 1e-6)
+
+
+def test_adam_matches_torch():
+    from rtsds_amd._lib import lib
+    from rtsds_amd.runtime import stream
+    g = torch.Generator().manual_seed(8)
+    p0 = torch.randn(10007, generator=g)
+    grads = [torch.randn(10007, generator=g) for _ in range(3)]
+    pr = p0.clone().requires_grad_()
+    opt = torch.optim.Adam([pr], lr=1e-3, weight_decay=1e-4)
+    pd = p0.to(DEV)
+    m, v = torch.zeros_like(pd), torch.zeros_like(pd)
+    sh = torch.empty(10007, dtype=torch.bfloat16, device=DEV)
+    for i, gr in enumerate(grads, 1):
+        pr.grad = gr.clone()
+        opt.step()
+        gd = gr.to(DEV)
+        lib.rtsds_adam_step(pd.data_ptr(), gd.data_ptr(), m.data_ptr(), v.data_ptr(), sh.data_ptr(),
+                            10007, 1e-3, 0.9, 0.999, 1e-8, 1e-4, i, 1.0, stream())
+    _close(pd, pr, torch.float32, "param", 1e-6)
+    _close(sh.float(), pr.detach().bfloat16().float(), torch.float32, "shadow", 1e-2)
+
+
+def test_confusion():
+    g = torch.Generator().manual_seed(12)
+    lab = torch.randint(0, 20, (3, 40, 50), generator=g)
+    pred = torch.randint(0, 19, (3, 40, 50), generator=g)
+    hist = torch.zeros(19 * 19, dtype=torch.int64, device=DEV)
+    F.confusion(lab.to(DEV), pred.to(DEV), hist, 19)
+    k = (lab >= 0) & (lab < 19)
+    ref = torch.bincount(19 * lab[k] + pred[k], minlength=361)
+    assert torch.equal(hist.cpu(), ref)
