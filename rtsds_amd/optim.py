@@ -1,0 +1,145 @@
+"""Fused Adam over a flat parameter arena (drop-in for torch.optim.Adam, main.py:116-117).
+
+On first use the optimizer moves every parameter of each group into one fp32 arena
+(``p.data`` becomes a view, same shape and strides, so modules and ``state_dict`` are
+unchanged), points ``p.grad`` at views of a flat gradient buffer, and keeps exp_avg /
+exp_avg_sq flat too.  One ``rtsds_adam_step`` launch then updates a whole group and, in the
+same pass, refreshes the bf16 weight shadows the bf16 convs read.  With
+``torch.distributed`` initialised (world > 1) the flat gradients are all-reduced over RCCL
+(one collective per arena) before the update and scaled by 1/world inside the kernel --
+this replaces the reference's nn.DataParallel grad reduce (utils.py:104-105).
+
+Semantics match torch.optim.Adam(amsgrad=False, maximize=False): L2 weight decay added to the
+gradient, per-parameter step counts, parameters whose gradient was not produced in a step
+are skipped (tracked with post-accumulate-grad hooks instead of ``grad is None``).
+``zero_grad`` zeroes the arena rather than dropping ``.grad`` tensors.
+"""
+import warnings
+
+import torch
+import torch.distributed as dist
+
+from ._lib import lib
+from .runtime import stream
+
+
+class _Arena:
+    def __init__(self, params):
+        dev = params[0].device
+        self.params = params
+        self.offsets = []
+        total = 0
+        for p in params:
+            if p.dtype != torch.float32 or not p.is_cuda:
+                raise RuntimeError("rtsds_amd.optim.Adam: fp32 HIP parameters required")
+            if not (p.is_contiguous() or p.is_contiguous(memory_format=torch.channels_last)):
+                p.data = p.data.contiguous()
+            self.offsets.append(total)
+            total += (p.numel() + 63) // 64 * 64  # 256-B aligned segments
+        self.total = total
+        self.flat = torch.zeros(total, dtype=torch.float32, device=dev)
+        self.gflat = torch.zeros(total, dtype=torch.float32, device=dev)
+        self.m = torch.zeros(total, dtype=torch.float32, device=dev)
+        self.v = torch.zeros(total, dtype=torch.float32, device=dev)
+        self.shadow = torch.empty(total, dtype=torch.bfloat16, device=dev)
+        self.steps = [0] * len(params)
+        self.touched = [False] * len(params)
+        with torch.no_grad():
+            for i, p in enumerate(params):
+                off, n = self.offsets[i], p.numel()
+                view = self.flat[off:off + n].as_strided(p.shape, p.stride())
+                view.copy_(p.data)
+                p.data = view
+                p.grad = self.gflat[off:off + n].as_strided(p.shape, p.stride())
+        lib.rtsds_cast(self.flat.data_ptr(), 0, self.shadow.data_ptr(), 1, total, stream())
+        for i, p in enumerate(params):
+            off, n = self.offsets[i], p.numel()
+            if p.dim() == 4:
+                p._rt_shadow = self.shadow[off:off + n].as_strided(p.shape, p.stride())
+                p._rt_shadow_key = (p.data_ptr(), p._version)
+            if p.requires_grad:
+                p.register_post_accumulate_grad_hook(self._hook(i))
+
+    def _hook(self, i):
+        def mark(_p):
+            self.touched[i] = True
+        return mark
+
+    def grad_ptr_ok(self, i):
+        p = self.params[i]
+        return p.grad is not None and p.grad.data_ptr() == self.gflat.data_ptr() + 4 * self.offsets[i]
+
+    def rebind_grad(self, i):
+        """AccumulateGrad replaced .grad out of place: fold it back into the arena."""
+        p = self.params[i]
+        off, n = self.offsets[i], p.numel()
+        view = self.gflat[off:off + n].as_strided(p.shape, p.stride())
+        if p.grad is not None:
+            view.copy_(p.grad)
+        p.grad = view
+
+
+class Adam(torch.optim.Optimizer):
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0, amsgrad=False):
+        if amsgrad:
+            raise NotImplementedError("rtsds_amd.optim.Adam: amsgrad")
+        super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
+        self._arenas = None
+        self._warned = False
+
+    # ------------------------------------------------------------------ arena
+    def _ensure(self):
+        if self._arenas is None:
+            self._arenas = [_Arena(list(g["params"])) for g in self.param_groups]
+        return self._arenas
+
+    def arenas(self):
+        return self._ensure()
+
+    def zero_grad(self, set_to_none=True):
+        for a in self._ensure():
+            a.gflat.zero_()
+            for i in range(len(a.params)):
+                a.touched[i] = False
+                if not a.grad_ptr_ok(i):
+                    a.rebind_grad(i)
+                    a.gflat[a.offsets[i]:a.offsets[i] + a.params[i].numel()].zero_()
+
+    # ------------------------------------------------------------------ step
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = closure() if closure is not None else None
+        arenas = self._ensure()
+        world = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+        for a in arenas:
+            for i in range(len(a.params)):
+                if a.touched[i] and not a.grad_ptr_ok(i):
+                    if not self._warned:
+                        warnings.warn("rtsds_amd.Adam: gradient left the arena; copying back")
+                        self._warned = True
+                    a.rebind_grad(i)
+            if world > 1:
+                dist.all_reduce(a.gflat)
+        for g, a in zip(self.param_groups, arenas):
+            b1, b2 = g["betas"]
+            # contiguous runs of touched parameters with equal step counts -> one launch each
+            i, n = 0, len(a.params)
+            while i < n:
+                if not a.touched[i]:
+                    i += 1
+                    continue
+                j = i
+                step = a.steps[i] + 1
+                while j + 1 < n and a.touched[j + 1] and a.steps[j + 1] + 1 == step:
+                    j += 1
+                lo = a.offsets[i]
+                hi = a.offsets[j] + a.params[j].numel()
+                lib.rtsds_adam_step(a.flat.data_ptr() + 4 * lo, a.gflat.data_ptr() + 4 * lo,
+                                    a.m.data_ptr() + 4 * lo, a.v.data_ptr() + 4 * lo,
+                                    a.shadow.data_ptr() + 2 * lo, hi - lo, float(g["lr"]), float(b1),
+                                    float(b2), float(g["eps"]), float(g["weight_decay"]), step,
+                                    1.0 / world, stream())
+                for k in range(i, j + 1):
+                    a.steps[k] = step
+                i = j + 1
+        return loss
