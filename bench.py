@@ -1,0 +1,185 @@
+"""RTSDS MI355X benchmark -- BASELINE.json metric on configs[1]:
+BiSeNet ResNet-18, 19 classes, 1024x512, batch 8 per GPU, bf16, seg-only train.py step.
+
+One "step" = one train.train iteration body (train.py:65-113): zero_grad, poly LR,
+forward (3 heads), 3x cross-entropy(ignore 19), backward, Adam step, pixel-accuracy count --
+``rtsds_amd.train.seg_step`` on synthetic, HBM-resident inputs.  N GPUs = one process per GPU
+(torchrun), each with its own batch of 8 (weak scaling); gradients all-reduced over RCCL
+inside the optimizer step.  Prints ONE JSON line on rank 0.
+
+Extra fields: inference FPS (eval forward, bs 8 and bs 1), the live conv roofline
+(HIP events around every implicit-GEMM launch over one extra step after the timed
+region), and the CPU baseline (the oracle's restatement of the reference step on the host
+cores, bounded sample, rank 0 at N=1 only).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+MFMA_BF16_PEAK_TFLOPS = 2500.0   # MI355X dense bf16 (MI355X_MICROARCH.md)
+GFLOP_PER_IMG_TRAIN = 151.6      # conv GFLOP fwd+bwd per image, 1024x512
+H, W, NC = 512, 1024, 19
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=8)
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-infer", action="store_true")
+    return ap.parse_args()
+
+
+def synthetic_batch(n, seed, device):
+    """ImageNet-normalised 0-255 images + labels in [0, 19] (19 = ignore), SURVEY 8(d)."""
+    g = torch.Generator().manual_seed(seed)
+    x = torch.randint(0, 256, (n, 3, H, W), generator=g).float()
+    mean = torch.tensor([0.485, 0.456, 0.406]).view(1, 3, 1, 1)
+    std = torch.tensor([0.229, 0.224, 0.225]).view(1, 3, 1, 1)
+    x = (x - mean) / std
+    y = torch.randint(0, NC + 1, (n, H, W), generator=g)
+    return x.to(device), y.to(device)
+
+
+def cpu_baseline(seconds=15.0):
+    """Oracle (plain-PyTorch CPU restatement of the reference, pinned to the reference's
+    golden captures) timed on the host: train step at 1024x512, batch 2."""
+    from oracle import models as om
+    from oracle import steps as osteps
+    from oracle.weights import apply_recipe, synthetic_images, synthetic_labels
+    threads = max(1, min(16, os.cpu_count() or 1))
+    torch.set_num_threads(threads)
+    net = apply_recipe(om.BiSeNet(NC, "resnet18"), seed=1).train()
+    opt = torch.optim.Adam(net.parameters(), lr=1e-4)
+    ce = torch.nn.CrossEntropyLoss(ignore_index=NC)
+    x = synthetic_images(2, H, W, seed=42)
+    y = synthetic_labels(2, H, W, seed=43)
+    osteps.seg_step(net, opt, ce, x, y)  # warm-up
+    n, t0 = 0, time.perf_counter()
+    while True:
+        osteps.seg_step(net, opt, ce, x, y)
+        n += 1
+        if time.perf_counter() - t0 > seconds or n >= 20:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": round(2 * n / dt, 4), "unit": "images/s", "cores": threads, "kind": "port",
+            "sample": f"oracle BiSeNet-R18 train step (fwd+3xCE+bwd+Adam), fp32, 2x3x512x1024, "
+                      f"{n} timed steps after 1 warm-up ({dt:.1f} s)"}
+
+
+def main():
+    args = parse()
+    from rtsds_amd import functional as F
+    from rtsds_amd import losses, optim, set_compute_dtype
+    from rtsds_amd.models.bisenet.build_bisenet import BiSeNet
+    from rtsds_amd.train import seg_step
+    from rtsds_amd.utils import init_distributed, poly_lr_scheduler
+
+    rank, local, world = init_distributed()
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
+    set_compute_dtype(dtype)
+    torch.manual_seed(42)
+
+    net = BiSeNet(NC, "resnet18").to(dev).train()
+    opt = optim.Adam(net.parameters(), lr=1e-4)
+    crit = losses.CrossEntropyLoss(ignore_index=NC)
+    x, y = synthetic_batch(args.batch, 42 + 2 * rank, dev)
+    max_iter = 1000
+
+    def step(i):
+        poly_lr_scheduler(opt, 1e-4, i, 1, max_iter, 0.9)
+        return seg_step(net, crit, opt, x, y)
+
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        loss, corr = step(args.warmup + i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ms = 1000.0 * elapsed / args.steps
+    imgs = args.batch * world * args.steps / elapsed
+    final_loss = float(loss.item())
+
+    # ---- live conv roofline: one more step with HIP events around each implicit-GEMM launch
+    F.CONV_PROFILE = []
+    step(args.warmup + args.steps)
+    torch.cuda.synchronize()
+    recs, F.CONV_PROFILE = F.CONV_PROFILE, None
+    conv_ms = sum(a.elapsed_time(b) for a, b, _ in recs)
+    conv_flop = sum(f for _, _, f in recs)
+    achieved = conv_flop / (conv_ms * 1e-3) / 1e12
+
+    # ---- inference FPS (eval forward, no grad)
+    infer = {}
+    if not args.no_infer:
+        net.eval()
+        with torch.no_grad():
+            for bs in (args.batch, 1):
+                xb = x[:bs].contiguous()
+                for _ in range(3):
+                    net(xb)
+                torch.cuda.synchronize()
+                k = 20 if bs > 1 else 50
+                t1 = time.perf_counter()
+                for _ in range(k):
+                    net(xb)
+                torch.cuda.synchronize()
+                infer[f"inference_fps_bs{bs}"] = round(bs * k * world / (time.perf_counter() - t1), 2)
+        net.train()
+
+    out = {
+        "metric": "images/sec/node (train step) + inference FPS@1024x512, BiSeNet 19-cls",
+        "value": round(imgs, 3), "unit": "images/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
+        "data": "synthetic (ImageNet-normalised 0-255 images, labels 0..19, 19=ignore; random-init weights)",
+        "config": {"workload": "BiSeNet-R18 seg-only train step (train.py:65-113)", "model": "BiSeNet-ResNet18",
+                   "global_batch": args.batch * world, "per_gpu_batch": args.batch,
+                   "image": "3x512x1024", "num_classes": NC, "parallelism": f"dp{world}"},
+        **infer,
+        "roofline": {"bound": "mfma", "kernel": "conv_gemm_kernel (implicit-GEMM conv fwd/dgrad/wgrad, "
+                                                "incl. dgrad repack + wgrad split-reduce launches)",
+                     "achieved": round(achieved, 2), "peak": MFMA_BF16_PEAK_TFLOPS if dtype == torch.bfloat16 else 157.3,
+                     "unit": "TFLOP/s", "frac": round(achieved / (MFMA_BF16_PEAK_TFLOPS if dtype == torch.bfloat16 else 157.3), 4),
+                     "traffic": None, "launches_per_step": len(recs),
+                     "conv_ms_per_step": round(conv_ms, 3),
+                     "conv_gflop_per_step": round(conv_flop / 1e9, 1)},
+        "whole_step_conv_flop_rate_tflops": round(GFLOP_PER_IMG_TRAIN * args.batch / ms, 2),
+        "final_loss": round(final_loss, 4),
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline()
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -130,8 +130,12 @@ int rtsds_chscale_bwd(const void* dy, const void* x, const void* a, void* dx, vo
  * of a wider NHWC tensor: pixel pitch *_ld (0 = c), channel offset *_off.               */
 int rtsds_bilinear_fwd(const void* x, void* y, int n, int hi, int wi, int c, int ho, int wo,
                        float scale_h, float scale_w, int y_ld, int y_off, int dtype, void* stream);
+/* Backward = separable two-pass gather (W then H) through an fp32 workspace of
+ * rtsds_bilinear_bwd_workspace() bytes; deterministic (no atomics).                      */
+size_t rtsds_bilinear_bwd_workspace(int n, int hi, int wi, int c, int ho, int wo);
 int rtsds_bilinear_bwd(const void* dy, void* dx, int n, int hi, int wi, int c, int ho, int wo,
-                       float scale_h, float scale_w, int dy_ld, int dy_off, int dtype, void* stream);
+                       float scale_h, float scale_w, int dy_ld, int dy_off, int dtype, void* ws,
+                       size_t ws_bytes, void* stream);
 
 /* ---------------------------------------------------------------- softmax / losses
  * Logits addressed by element strides (sn, sc, shw) per (image, channel, pixel): NHWC and

@@ -114,17 +114,26 @@ __global__ void __launch_bounds__(256) bn_stats_kernel(const T* __restrict__ x, 
   }
 }
 
-// Pass 2 (forward): merge row blocks per channel, update running stats, emit scale/shift.
-__global__ void bn_finalize_kernel(const float* __restrict__ part, int nrb, int c, long rows, const float* gamma,
+// Pass 2 (forward): one wave per channel merges the row-block partials (Chan, lane-strided,
+// then a shuffle tree), updates running stats and emits scale/shift.
+RT_DEV void chan_merge_shfl(float& n, float& m, float& M) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float nb = __shfl_xor(n, o, 64), mb = __shfl_xor(m, o, 64), Mb = __shfl_xor(M, o, 64);
+    chan_merge(n, m, M, nb, mb, Mb);
+  }
+}
+__global__ void __launch_bounds__(64) bn_finalize_kernel(const float* __restrict__ part, int nrb, int c, long rows, const float* gamma,
                                    const float* beta, float* rmean, float* rvar, float* smean, float* sinv,
                                    float* scale, float* shift, float momentum, float eps) {
-  const int ch = blockIdx.x * blockDim.x + threadIdx.x;
-  if (ch >= c) return;
+  const int ch = blockIdx.x, lane = threadIdx.x;
   float n = 0.f, m = 0.f, M = 0.f;
-  for (int b = 0; b < nrb; ++b) {
+  for (int b = lane; b < nrb; b += 64) {
     const float* p = part + ((long)b * c + ch) * 3;
     chan_merge(n, m, M, p[0], p[1], p[2]);
   }
+  chan_merge_shfl(n, m, M);
+  if (lane != 0) return;
   const float var = M / (float)rows;
   const float inv = 1.0f / sqrtf(var + eps);
   smean[ch] = m;
@@ -237,31 +246,27 @@ __global__ void __launch_bounds__(256) bn_bwd_stats_kernel(const T* __restrict__
   }
 }
 
-// Backward pass 2: coefficients  dx = A*g + B*(x-mean) + C  per channel.
-__global__ void bn_bwd_finalize_kernel(const float* __restrict__ part, int nrb, int c, long rows, const float* gamma,
+// Backward pass 2: coefficients  dx = A*g + B*(x-mean) + C  per channel (one wave each).
+__global__ void __launch_bounds__(64) bn_bwd_finalize_kernel(const float* __restrict__ part, int nrb, int c, long rows, const float* gamma,
                                        const float* smean, const float* sinv, float* dgamma, float* dbeta,
                                        float* coefA, float* coefB, float* coefC, int training) {
-  const int ch = blockIdx.x * blockDim.x + threadIdx.x;
-  if (ch >= c) return;
+  const int ch = blockIdx.x, lane = threadIdx.x;
   float sg = 0.f, sgx = 0.f;
-  for (int b = 0; b < nrb; ++b) {
+  for (int b = lane; b < nrb; b += 64) {
     sg += part[((long)b * c + ch) * 2];
     sgx += part[((long)b * c + ch) * 2 + 1];
   }
+  sg = wave_sum(sg);
+  sgx = wave_sum(sgx);
+  if (lane != 0) return;
   const float inv = sinv[ch], g = gamma ? gamma[ch] : 1.f;
   if (dgamma) dgamma[ch] = sgx * inv;
   if (dbeta) dbeta[ch] = sg;
   const float a = g * inv;
-  if (training) {
-    const float invn = 1.f / (float)rows;
-    coefA[ch] = a;
-    coefB[ch] = -a * inv * inv * sgx * invn;
-    coefC[ch] = -a * sg * invn;
-  } else {
-    coefA[ch] = a;
-    coefB[ch] = 0.f;
-    coefC[ch] = 0.f;
-  }
+  const float invn = 1.f / (float)rows;
+  coefA[ch] = a;
+  coefB[ch] = training ? -a * inv * inv * sgx * invn : 0.f;
+  coefC[ch] = training ? -a * sg * invn : 0.f;
   (void)smean;
 }
 
@@ -318,7 +323,7 @@ static void bn_fwd_launch(const void* x, const void* res, void* y, long rows, in
   if (training) {
     const int rb = bn_rb(rows, c, VEC);
     hipLaunchKernelGGL((bn_stats_kernel<T, VEC>), dim3(rb, rt_cdiv(c, 256 * VEC)), dim3(256), 0, st, (const T*)x, part, rows, c);
-    hipLaunchKernelGGL(bn_finalize_kernel, dim3(rt_cdiv(c, 256)), dim3(256), 0, st, part, rb, c, rows, gamma, beta, rm, rv,
+    hipLaunchKernelGGL(bn_finalize_kernel, dim3(c), dim3(64), 0, st, part, rb, c, rows, gamma, beta, rm, rv,
                        sm, si, scale, shift, mom, eps);
   } else {
     hipLaunchKernelGGL(bn_eval_coef_kernel, dim3(rt_cdiv(c, 256)), dim3(256), 0, st, c, gamma, beta, rm, rv, scale, shift, sm, si, eps);
@@ -358,7 +363,7 @@ static void bn_bwd_launch(const void* dy, const void* x, const void* y, void* dx
   const int rb = bn_rb(rows, c, VEC);
   hipLaunchKernelGGL((bn_bwd_stats_kernel<T, VEC>), dim3(rb, rt_cdiv(c, 256 * VEC)), dim3(256), 0, st, (const T*)dy, (const T*)x, (const T*)y, smean,
                      part, rows, c, act);
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(rt_cdiv(c, 256)), dim3(256), 0, st, part, rb, c, rows, gamma, smean, sinv,
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(c), dim3(64), 0, st, part, rb, c, rows, gamma, smean, sinv,
                      dgamma, dbeta, A, B, C, training);
   if (dx || dres) {
     const long total = rows * ((c + VEC - 1) / VEC);

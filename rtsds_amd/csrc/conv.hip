@@ -455,29 +455,50 @@ __global__ void split_reduce_kernel(const float* __restrict__ part, float* __res
   }
 }
 
-// dbias: two-stage deterministic column sum of dy[rows][c].
-// Stage 1: grid (ceil(c/64), RB); block sums rows blockIdx.y*4+rw (+= 4*RB) -> part[RB][c].
-template <typename T>
-__global__ void colsum_part_kernel(const T* __restrict__ dy, float* __restrict__ part, long rows, int c) {
-  __shared__ float red[4][64];
-  const int cc = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int rw = threadIdx.x >> 6;
-  float s = 0.f;
-  if (cc < c)
-    for (long r = (long)blockIdx.y * 4 + rw; r < rows; r += 4L * gridDim.y) s += to_f(dy[r * c + cc]);
-  red[rw][threadIdx.x & 63] = s;
+// dbias: two-stage deterministic column sum of dy[rows][c].  Stage 1: grid (RB, channel
+// chunks); 256 threads laid out [row group][channel vector] (coalesced whole-row reads);
+// block b sums rows b*rpi + rg (+= RB*rpi) -> part[b][c].  Stage 2 sums the RB partials.
+template <typename T, int VEC>
+__global__ void __launch_bounds__(256) colsum_part_kernel(const T* __restrict__ dy, float* __restrict__ part, long rows, int c) {
+  __shared__ float red[256 * VEC];
+  const int cbase = blockIdx.y * 256 * VEC;
+  const int cl = min(c - cbase, 256 * VEC);
+  const int tpr = (cl + VEC - 1) / VEC, rpi = 256 / tpr;
+  const int tid = threadIdx.x, cv = tid % tpr, rg = tid / tpr;
+  const int ch0 = cbase + cv * VEC;
+  float acc[VEC];
+#pragma unroll
+  for (int j = 0; j < VEC; ++j) acc[j] = 0.f;
+  if (rg < rpi)
+    for (long r = (long)blockIdx.x * rpi + rg; r < rows; r += (long)gridDim.x * rpi) {
+      if (VEC > 1) {
+        typename VecT<T>::v16 v = *(const typename VecT<T>::v16*)(dy + r * c + ch0);
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) acc[j] += to_f(v[j]);
+      } else {
+        acc[0] += to_f(dy[r * c + ch0]);
+      }
+    }
+#pragma unroll
+  for (int j = 0; j < VEC; ++j) red[tid * VEC + j] = acc[j];
   __syncthreads();
-  if (rw == 0 && cc < c)
-    part[(long)blockIdx.y * c + cc] = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+  if (rg == 0) {
+    for (int g = 1; g < rpi; ++g)
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) acc[j] += red[(g * tpr + cv) * VEC + j];
+#pragma unroll
+    for (int j = 0; j < VEC; ++j)
+      if (ch0 + j < c) part[(long)blockIdx.x * c + ch0 + j] = acc[j];
+  }
 }
 __global__ void colsum_final_kernel(const float* __restrict__ part, float* __restrict__ out, int rb, int c) {
-  const int cc = blockIdx.x * blockDim.x + threadIdx.x;
-  if (cc >= c) return;
+  const int cc = blockIdx.x, lane = threadIdx.x;
   float s = 0.f;
-  for (int i = 0; i < rb; ++i) s += part[(long)i * c + cc];
-  out[cc] = s;
+  for (int i = lane; i < rb; i += 64) s += part[(long)i * c + cc];
+  s = wave_sum(s);
+  if (lane == 0) out[cc] = s;
 }
-static const int kColsumRB = 256;
+static const int kColsumRB = 1024;
 
 // ---- host side ---------------------------------------------------------------------------
 static ConvArgs make_args(const rtsds_conv_desc* d) {
@@ -668,10 +689,16 @@ extern "C" int rtsds_conv2d_wgrad(const rtsds_conv_desc* d, const void* x, const
     const long rows = (long)d->n * d->ho * d->wo;
     const size_t slab = splits <= 1 ? 0 : ((size_t)splits * p.split_stride * 4 + 255) & ~(size_t)255;
     float* part = (float*)((char*)ws + slab);
-    dim3 g1(rt_cdiv(d->k, 64), kColsumRB);
-    if (b16) hipLaunchKernelGGL(colsum_part_kernel<bf16>, g1, dim3(256), 0, st, (const bf16*)dy, part, rows, d->k);
-    else hipLaunchKernelGGL(colsum_part_kernel<float>, g1, dim3(256), 0, st, (const float*)dy, part, rows, d->k);
-    hipLaunchKernelGGL(colsum_final_kernel, dim3(rt_cdiv(d->k, 256)), dim3(256), 0, st, (const float*)part, dbias, kColsumRB, d->k);
+    const int rb = (int)std::max<long>(1, std::min<long>(kColsumRB, rows / 64));
+    if (b16 && d->k % 8 == 0)
+      hipLaunchKernelGGL((colsum_part_kernel<bf16, 8>), dim3(rb, rt_cdiv(d->k, 2048)), dim3(256), 0, st, (const bf16*)dy, part, rows, d->k);
+    else if (b16)
+      hipLaunchKernelGGL((colsum_part_kernel<bf16, 1>), dim3(rb, rt_cdiv(d->k, 256)), dim3(256), 0, st, (const bf16*)dy, part, rows, d->k);
+    else if (d->k % 4 == 0)
+      hipLaunchKernelGGL((colsum_part_kernel<float, 4>), dim3(rb, rt_cdiv(d->k, 1024)), dim3(256), 0, st, (const float*)dy, part, rows, d->k);
+    else
+      hipLaunchKernelGGL((colsum_part_kernel<float, 1>), dim3(rb, rt_cdiv(d->k, 256)), dim3(256), 0, st, (const float*)dy, part, rows, d->k);
+    hipLaunchKernelGGL(colsum_final_kernel, dim3(d->k), dim3(64), 0, st, (const float*)part, dbias, rb, d->k);
   }
   return hipGetLastError() == hipSuccess ? RTSDS_OK : RTSDS_ERR_LAUNCH;
 }

@@ -201,17 +201,59 @@ extern "C" int rtsds_maxpool_bwd(const void* dy, const uint8_t* idx, void* dx, i
 // ------------------------------------------------------------------ global average pool
 // y[img][c] = mean_hw x[img][hw][c]   (AdaptiveAvgPool2d(1) / torch.mean over H,W:
 // build_bisenet.py:46,75, build_contextpath.py:27-28, model.py:63,82).
-// grid (img, ceil(c/64)); 256 threads = 4 row groups x 64 channels.
-template <typename T>
-__global__ void gap_fwd_kernel(const T* __restrict__ x, T* __restrict__ y, long hw, int c) {
-  __shared__ float red[4][64];
-  const int img = blockIdx.x, ch = blockIdx.y * 64 + (threadIdx.x & 63), rg = threadIdx.x >> 6;
-  float s = 0.f;
-  if (ch < c)
-    for (long r = rg; r < hw; r += 4) s += to_f(x[((long)img * hw + r) * c + ch]);
-  red[rg][threadIdx.x & 63] = s;
+//
+// Shared per-image channel reduction: out[img][c] = scale * sum_hw a (* b if DOT).  A 1024-thread
+// block is laid out [row group][16-B channel vector] (VEC = 8 bf16 / 4 f32 when c allows, else
+// 1), so each iteration reads rpi whole rows coalesced; grid = (img, channel chunk).
+template <typename T, int VEC, bool DOT>
+__global__ void __launch_bounds__(1024) chan_reduce_kernel(const T* __restrict__ a, const T* __restrict__ b, T* __restrict__ out,
+                                                           long hw, int c, float scale) {
+  __shared__ float red[1024 * VEC];
+  const int img = blockIdx.x;
+  const int cbase = blockIdx.y * 1024 * VEC;
+  const int cl = min(c - cbase, 1024 * VEC);
+  const int tpr = (cl + VEC - 1) / VEC, rpi = 1024 / tpr;
+  const int tid = threadIdx.x, cv = tid % tpr, rg = tid / tpr;
+  const int ch0 = cbase + cv * VEC;
+  float acc[VEC];
+#pragma unroll
+  for (int j = 0; j < VEC; ++j) acc[j] = 0.f;
+  if (rg < rpi) {
+    const long base = (long)img * hw * c + ch0;
+    for (long r = rg; r < hw; r += rpi) {
+      const long o = base + r * c;
+      if (VEC > 1) {
+        typename VecT<T>::v16 va = *(const typename VecT<T>::v16*)(a + o);
+        if (DOT) {
+          typename VecT<T>::v16 vb = *(const typename VecT<T>::v16*)(b + o);
+#pragma unroll
+          for (int j = 0; j < VEC; ++j) acc[j] = fmaf(to_f(va[j]), to_f(vb[j]), acc[j]);
+        } else {
+#pragma unroll
+          for (int j = 0; j < VEC; ++j) acc[j] += to_f(va[j]);
+        }
+      } else {
+        acc[0] = DOT ? fmaf(to_f(a[o]), to_f(b[o]), acc[0]) : acc[0] + to_f(a[o]);
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < VEC; ++j) red[tid * VEC + j] = acc[j];
   __syncthreads();
-  if (rg == 0 && ch < c) y[(long)img * c + ch] = from_f<T>((red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x]) / (float)hw);
+  if (rg == 0) {
+    for (int g = 1; g < rpi; ++g)
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) acc[j] += red[(g * tpr + cv) * VEC + j];
+#pragma unroll
+    for (int j = 0; j < VEC; ++j)
+      if (ch0 + j < c) out[(long)img * c + ch0 + j] = from_f<T>(acc[j] * scale);
+  }
+}
+template <typename T, bool DOT>
+static void chan_reduce(const T* a, const T* b, T* out, int n, long hw, int c, float scale, hipStream_t st) {
+  constexpr int V = VecT<T>::N;
+  if (c % V == 0) hipLaunchKernelGGL((chan_reduce_kernel<T, V, DOT>), dim3(n, rt_cdiv(c, 1024 * V)), dim3(1024), 0, st, a, b, out, hw, c, scale);
+  else hipLaunchKernelGGL((chan_reduce_kernel<T, 1, DOT>), dim3(n, rt_cdiv(c, 1024)), dim3(1024), 0, st, a, b, out, hw, c, scale);
 }
 template <typename T>
 __global__ void gap_bwd_kernel(const T* __restrict__ dy, T* __restrict__ dx, int n, long hw, int c) {
@@ -225,7 +267,7 @@ __global__ void gap_bwd_kernel(const T* __restrict__ dy, T* __restrict__ dx, int
 }
 extern "C" int rtsds_gap_fwd(const void* x, void* y, int n, long hw, int c, int dtype, void* stream) {
   if (n <= 0 || hw <= 0 || c <= 0) return RTSDS_ERR_SHAPE;
-  DISPATCH_T(dtype, hipLaunchKernelGGL(gap_fwd_kernel<T>, dim3(n, rt_cdiv(c, 64)), dim3(256), 0, (hipStream_t)stream, (const T*)x, (T*)y, hw, c));
+  DISPATCH_T(dtype, (chan_reduce<T, false>((const T*)x, nullptr, (T*)y, n, hw, c, 1.f / (float)hw, (hipStream_t)stream)));
   RET_LAUNCH();
 }
 extern "C" int rtsds_gap_bwd(const void* dy, void* dx, int n, long hw, int c, int dtype, void* stream) {
@@ -257,21 +299,6 @@ __global__ void chscale_bwd_dx_kernel(const T* __restrict__ dy, const T* __restr
     dx[i] = from_f<T>(to_f(dy[i]) * av);
   }
 }
-// da[img][c] = sum_hw dy * x   (grid (img, ceil(c/64)))
-template <typename T>
-__global__ void chscale_bwd_da_kernel(const T* __restrict__ dy, const T* __restrict__ x, T* __restrict__ da, long hw, int c) {
-  __shared__ float red[4][64];
-  const int img = blockIdx.x, ch = blockIdx.y * 64 + (threadIdx.x & 63), rg = threadIdx.x >> 6;
-  float s = 0.f;
-  if (ch < c)
-    for (long r = rg; r < hw; r += 4) {
-      const long o = ((long)img * hw + r) * c + ch;
-      s = fmaf(to_f(dy[o]), to_f(x[o]), s);
-    }
-  red[rg][threadIdx.x & 63] = s;
-  __syncthreads();
-  if (rg == 0 && ch < c) da[(long)img * c + ch] = from_f<T>(red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x]);
-}
 extern "C" int rtsds_chscale_fwd(const void* x, const void* a, void* y, int n, long hw, int c, int mode, int dtype, void* stream) {
   const long total = (long)n * hw * c;
   if (total <= 0) return RTSDS_ERR_SHAPE;
@@ -285,7 +312,7 @@ extern "C" int rtsds_chscale_bwd(const void* dy, const void* x, const void* a, v
   hipStream_t st = (hipStream_t)stream;
   DISPATCH_T(dtype, {
     if (dx) hipLaunchKernelGGL(chscale_bwd_dx_kernel<T>, dim3(ew_blocks(total)), dim3(256), 0, st, (const T*)dy, (const T*)a, (T*)dx, n, hw, c, mode);
-    if (da) hipLaunchKernelGGL(chscale_bwd_da_kernel<T>, dim3(n, rt_cdiv(c, 64)), dim3(256), 0, st, (const T*)dy, (const T*)x, (T*)da, hw, c);
+    if (da) chan_reduce<T, true>((const T*)dy, (const T*)x, (T*)da, n, hw, c, 1.f, st);
   });
   RET_LAUNCH();
 }
@@ -303,13 +330,18 @@ RT_DEV void bil_src(int o, float scale, int in, int& i0, int& i1, float& l0, flo
   l1 = src - (float)i0;
   l0 = 1.f - l1;
 }
-template <typename T>
+// Forward: one thread per (output pixel, channel chunk of CH); the 4 taps and weights are
+// computed once per chunk.  CH = 16-B vector when the channel layout allows it, else the whole
+// pixel (c <= 64, e.g. the 19-class heads) or single channels.
+template <typename T, int MODE>  // MODE 0: 16-B vectors, 1: whole pixel loop, 2: per channel
 __global__ void bilinear_fwd_kernel(const T* __restrict__ x, T* __restrict__ y, int n, int hi, int wi, int c, int ho, int wo,
                                     float sh, float sw, int yld, int yoff) {
-  const long total = (long)n * ho * wo * c;
+  constexpr int V = VecT<T>::N;
+  const int cpp = MODE == 0 ? c / V : (MODE == 1 ? 1 : c);  // chunks per pixel
+  const long total = (long)n * ho * wo * cpp;
   GRID_STRIDE(i, total) {
-    const int ch = (int)(i % c);
-    long q = i / c;
+    const int chunk = (int)(i % cpp);
+    long q = i / cpp;
     const int ow = (int)(q % wo); q /= wo;
     const int oh = (int)(q % ho);
     const int img = (int)(q / ho);
@@ -317,44 +349,82 @@ __global__ void bilinear_fwd_kernel(const T* __restrict__ x, T* __restrict__ y, 
     float lh0, lh1, lw0, lw1;
     bil_src(oh, sh, hi, h0, h1, lh0, lh1);
     bil_src(ow, sw, wi, w0, w1, lw0, lw1);
-    const T* b = x + (long)img * hi * wi * c + ch;
-    const float v00 = to_f(b[((long)h0 * wi + w0) * c]), v01 = to_f(b[((long)h0 * wi + w1) * c]);
-    const float v10 = to_f(b[((long)h1 * wi + w0) * c]), v11 = to_f(b[((long)h1 * wi + w1) * c]);
-    const float v = lh0 * (lw0 * v00 + lw1 * v01) + lh1 * (lw0 * v10 + lw1 * v11);
-    y[((((long)img * ho + oh) * wo) + ow) * yld + yoff + ch] = from_f<T>(v);
+    const T* b = x + (long)img * hi * wi * c;
+    const T* p00 = b + ((long)h0 * wi + w0) * c;
+    const T* p01 = b + ((long)h0 * wi + w1) * c;
+    const T* p10 = b + ((long)h1 * wi + w0) * c;
+    const T* p11 = b + ((long)h1 * wi + w1) * c;
+    T* o = y + ((((long)img * ho + oh) * wo) + ow) * yld + yoff;
+    if (MODE == 0) {
+      typedef typename VecT<T>::v16 V16;
+      const int c0 = chunk * V;
+      const V16 a = *(const V16*)(p00 + c0), bb = *(const V16*)(p01 + c0);
+      const V16 cc = *(const V16*)(p10 + c0), dd = *(const V16*)(p11 + c0);
+      V16 r;
+#pragma unroll
+      for (int j = 0; j < V; ++j)
+        r[j] = from_f<T>(lh0 * (lw0 * to_f(a[j]) + lw1 * to_f(bb[j])) + lh1 * (lw0 * to_f(cc[j]) + lw1 * to_f(dd[j])));
+      *(V16*)(o + c0) = r;
+    } else {
+      const int cs = MODE == 1 ? 0 : chunk, ce = MODE == 1 ? c : chunk + 1;
+      for (int ch = cs; ch < ce; ++ch)
+        o[ch] = from_f<T>(lh0 * (lw0 * to_f(p00[ch]) + lw1 * to_f(p01[ch])) + lh1 * (lw0 * to_f(p10[ch]) + lw1 * to_f(p11[ch])));
+    }
   }
 }
-// Backward as a gather (deterministic): input pixel (ih, iw) collects every output pixel whose
-// (i0 | i1) equals it.  Candidate outputs span [(i-1.5)/scale, (i+1.5)/scale].
+
+// Backward, separable gather (deterministic, no atomics): input index i along one axis
+// receives from outputs o with i0(o) == i (weight l0) or i1(o) == i (weight l1); those o lie
+// in [(i-0.5)/s - 0.5, (i+1.5)/s - 0.5], widened by one and tested exactly with bil_src.
+RT_DEV float bil_wsum_range(int i, float s, int in, int out, int& lo, int& hi) {
+  lo = max(0, (int)floorf(((float)i - 0.5f) / s - 0.5f) - 1);
+  hi = min(out - 1, (int)ceilf(((float)i + 1.5f) / s - 0.5f) + 1);
+  return 0.f;
+}
+RT_DEV float bil_weight(int o, int i, float s, int in) {
+  int a0, a1;
+  float l0, l1;
+  bil_src(o, s, in, a0, a1, l0, l1);
+  return (a0 == i ? l0 : 0.f) + (a1 == i ? l1 : 0.f);
+}
+// pass 1 (W): tmp[img][oh][iw][c] = sum_ow w(ow->iw) dy[img][oh][ow][c]   (fp32)
 template <typename T>
-__global__ void bilinear_bwd_kernel(const T* __restrict__ dy, T* __restrict__ dx, int n, int hi, int wi, int c, int ho, int wo,
-                                    float sh, float sw, int dyld, int dyoff) {
-  const long total = (long)n * hi * wi * c;
+__global__ void bilinear_bwd_w_kernel(const T* __restrict__ dy, float* __restrict__ tmp, int n, int wi, int c, int ho, int wo, float sw,
+                                      int dyld, int dyoff) {
+  const long total = (long)n * ho * wi * c;
   GRID_STRIDE(i, total) {
     const int ch = (int)(i % c);
     long q = i / c;
-    const int iw = (int)(q % wi); q /= wi;
+    const int iw = (int)(q % wi);
+    const long row = q / wi;  // img * ho + oh
+    int lo, hi;
+    bil_wsum_range(iw, sw, wi, wo, lo, hi);
+    const T* src = dy + row * wo * dyld + dyoff + ch;
+    float acc = 0.f;
+    for (int ow = lo; ow <= hi; ++ow) {
+      const float wt = bil_weight(ow, iw, sw, wi);
+      if (wt != 0.f) acc = fmaf(wt, to_f(src[(long)ow * dyld]), acc);
+    }
+    tmp[i] = acc;
+  }
+}
+// pass 2 (H): dx[img][ih][iw][c] = sum_oh w(oh->ih) tmp[img][oh][iw][c]
+template <typename T>
+__global__ void bilinear_bwd_h_kernel(const float* __restrict__ tmp, T* __restrict__ dx, int n, int hi, int wi, int c, int ho, float sh) {
+  const long total = (long)n * hi * wi * c;
+  const long plane = (long)wi * c;
+  GRID_STRIDE(i, total) {
+    const long inner = i % plane;  // iw * c + ch
+    long q = i / plane;
     const int ih = (int)(q % hi);
     const int img = (int)(q / hi);
-    const int oh_lo = max(0, (int)floorf(((float)ih - 1.5f) / sh) - 1), oh_hi = min(ho - 1, (int)ceilf(((float)ih + 1.5f) / sh) + 1);
-    const int ow_lo = max(0, (int)floorf(((float)iw - 1.5f) / sw) - 1), ow_hi = min(wo - 1, (int)ceilf(((float)iw + 1.5f) / sw) + 1);
+    int lo, hh;
+    bil_wsum_range(ih, sh, hi, ho, lo, hh);
+    const float* src = tmp + (long)img * ho * plane + inner;
     float acc = 0.f;
-    for (int oh = oh_lo; oh <= oh_hi; ++oh) {
-      int h0, h1;
-      float lh0, lh1;
-      bil_src(oh, sh, hi, h0, h1, lh0, lh1);
-      const float wh = (h0 == ih ? lh0 : 0.f) + (h1 == ih ? lh1 : 0.f);
-      if (wh == 0.f) continue;
-      float racc = 0.f;
-      for (int ow = ow_lo; ow <= ow_hi; ++ow) {
-        int w0, w1;
-        float lw0, lw1;
-        bil_src(ow, sw, wi, w0, w1, lw0, lw1);
-        const float ww = (w0 == iw ? lw0 : 0.f) + (w1 == iw ? lw1 : 0.f);
-        if (ww == 0.f) continue;
-        racc = fmaf(ww, to_f(dy[((((long)img * ho + oh) * wo) + ow) * dyld + dyoff + ch]), racc);
-      }
-      acc = fmaf(wh, racc, acc);
+    for (int oh = lo; oh <= hh; ++oh) {
+      const float wt = bil_weight(oh, ih, sh, hi);
+      if (wt != 0.f) acc = fmaf(wt, src[(long)oh * plane], acc);
     }
     dx[i] = from_f<T>(acc);
   }
@@ -364,15 +434,35 @@ extern "C" int rtsds_bilinear_fwd(const void* x, void* y, int n, int hi, int wi,
   const long total = (long)n * ho * wo * c;
   if (total <= 0 || hi <= 0 || wi <= 0) return RTSDS_ERR_SHAPE;
   if (y_ld <= 0) y_ld = c;
-  DISPATCH_T(dtype, hipLaunchKernelGGL(bilinear_fwd_kernel<T>, dim3(ew_blocks(total)), dim3(256), 0, (hipStream_t)stream, (const T*)x, (T*)y, n, hi, wi, c, ho, wo, scale_h, scale_w, y_ld, y_off));
+  hipStream_t st = (hipStream_t)stream;
+  DISPATCH_T(dtype, {
+    constexpr int V = VecT<T>::N;
+    const long pix = (long)n * ho * wo;
+    if (c % V == 0 && y_ld % V == 0 && y_off % V == 0)
+      hipLaunchKernelGGL((bilinear_fwd_kernel<T, 0>), dim3(ew_blocks(pix * (c / V))), dim3(256), 0, st, (const T*)x, (T*)y, n, hi, wi, c, ho, wo, scale_h, scale_w, y_ld, y_off);
+    else if (c <= 64)
+      hipLaunchKernelGGL((bilinear_fwd_kernel<T, 1>), dim3(ew_blocks(pix)), dim3(256), 0, st, (const T*)x, (T*)y, n, hi, wi, c, ho, wo, scale_h, scale_w, y_ld, y_off);
+    else
+      hipLaunchKernelGGL((bilinear_fwd_kernel<T, 2>), dim3(ew_blocks(pix * c)), dim3(256), 0, st, (const T*)x, (T*)y, n, hi, wi, c, ho, wo, scale_h, scale_w, y_ld, y_off);
+  });
   RET_LAUNCH();
 }
+extern "C" size_t rtsds_bilinear_bwd_workspace(int n, int hi, int wi, int c, int ho, int wo) {
+  (void)hi; (void)wo;
+  return (size_t)n * ho * wi * c * sizeof(float) + 256;
+}
 extern "C" int rtsds_bilinear_bwd(const void* dy, void* dx, int n, int hi, int wi, int c, int ho, int wo, float scale_h, float scale_w,
-                                  int dy_ld, int dy_off, int dtype, void* stream) {
+                                  int dy_ld, int dy_off, int dtype, void* ws, size_t ws_bytes, void* stream) {
   const long total = (long)n * hi * wi * c;
   if (total <= 0 || ho <= 0 || wo <= 0) return RTSDS_ERR_SHAPE;
+  if (ws_bytes < rtsds_bilinear_bwd_workspace(n, hi, wi, c, ho, wo)) return RTSDS_ERR_WORKSPACE;
   if (dy_ld <= 0) dy_ld = c;
-  DISPATCH_T(dtype, hipLaunchKernelGGL(bilinear_bwd_kernel<T>, dim3(ew_blocks(total)), dim3(256), 0, (hipStream_t)stream, (const T*)dy, (T*)dx, n, hi, wi, c, ho, wo, scale_h, scale_w, dy_ld, dy_off));
+  hipStream_t st = (hipStream_t)stream;
+  float* tmp = (float*)ws;
+  DISPATCH_T(dtype, {
+    hipLaunchKernelGGL(bilinear_bwd_w_kernel<T>, dim3(ew_blocks((long)n * ho * wi * c)), dim3(256), 0, st, (const T*)dy, tmp, n, wi, c, ho, wo, scale_w, dy_ld, dy_off);
+    hipLaunchKernelGGL(bilinear_bwd_h_kernel<T>, dim3(ew_blocks(total)), dim3(256), 0, st, (const float*)tmp, (T*)dx, n, hi, wi, c, ho, scale_h);
+  });
   RET_LAUNCH();
 }
 

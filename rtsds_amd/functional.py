@@ -15,6 +15,32 @@ from .runtime import CL, dcode, empty_nhwc, nhwc, require_hip, stream, workspace
 
 _P = lambda t: None if t is None else t.data_ptr()  # noqa: E731
 
+# Optional conv-kernel timing (bench.py's live roofline): when ``CONV_PROFILE`` is a list,
+# every implicit-GEMM launch is bracketed by HIP events on the launch stream and
+# (start, end, algorithmic_flops) is appended.
+CONV_PROFILE = None
+
+
+def _conv_flops(d):
+    return 2.0 * d.n * d.ho * d.wo * d.k * d.c * d.kh * d.kw
+
+
+class _Timed:
+    def __init__(self, d):
+        self.d = d
+
+    def __enter__(self):
+        if CONV_PROFILE is not None:
+            self.e0 = torch.cuda.Event(enable_timing=True)
+            self.e1 = torch.cuda.Event(enable_timing=True)
+            self.e0.record()
+        return self
+
+    def __exit__(self, *exc):
+        if CONV_PROFILE is not None:
+            self.e1.record()
+            CONV_PROFILE.append((self.e0, self.e1, _conv_flops(self.d)))
+
 
 # ----------------------------------------------------------------------------- conv
 def _conv_desc(x, k, kh, kw, stride, padding, dilation):
@@ -39,7 +65,8 @@ class ConvFn(torch.autograd.Function):
         k, _, kh, kw = weight.shape
         d = _conv_desc(x, k, kh, kw, stride, padding, dilation)
         y = empty_nhwc(d.n, k, d.ho, d.wo, x.dtype, x.device)
-        lib.rtsds_conv2d_fwd(ctypes.byref(d), _P(x), _P(wq), _P(bias), _P(y), act, stream())
+        with _Timed(d):
+            lib.rtsds_conv2d_fwd(ctypes.byref(d), _P(x), _P(wq), _P(bias), _P(y), act, stream())
         ctx.d, ctx.act, ctx.has_bias = d, act, bias is not None
         ctx.save_for_backward(x, wq, y if act else None)
         return y
@@ -60,15 +87,17 @@ class ConvFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = empty_nhwc(d.n, d.c, d.h, d.w, x.dtype, x.device)
             ws = workspace(lib.rtsds_conv2d_dgrad_workspace(ctypes.byref(d)), x.device)
-            lib.rtsds_conv2d_dgrad(ctypes.byref(d), _P(g), _P(wq), _P(dx), 0, _P(ws), ws.numel(),
-                                   stream())
+            with _Timed(d):
+                lib.rtsds_conv2d_dgrad(ctypes.byref(d), _P(g), _P(wq), _P(dx), 0, _P(ws), ws.numel(),
+                                       stream())
         if ctx.needs_input_grad[1] or ctx.needs_input_grad[2]:
             dw = torch.empty((d.k, d.c, d.kh, d.kw), dtype=torch.float32, device=x.device,
                              memory_format=CL)
             db = torch.empty(d.k, dtype=torch.float32, device=x.device) if ctx.has_bias else None
             ws = workspace(lib.rtsds_conv2d_wgrad_workspace(ctypes.byref(d)), x.device)
-            lib.rtsds_conv2d_wgrad(ctypes.byref(d), _P(x), _P(g), _P(dw), _P(db), _P(ws),
-                                   ws.numel(), stream())
+            with _Timed(d):
+                lib.rtsds_conv2d_wgrad(ctypes.byref(d), _P(x), _P(g), _P(dw), _P(db), _P(ws),
+                                       ws.numel(), stream())
             if not ctx.needs_input_grad[1]:
                 dw = None
         return dx, dw, db, None, None, None, None, None
@@ -96,8 +125,9 @@ class ConvSumFn(torch.autograd.Function):
             d = _conv_desc(x, k, kh, kw, stride, padding, dilation)
             if y is None:
                 y = empty_nhwc(d.n, k, d.ho, d.wo, x.dtype, x.device)
-            lib.rtsds_conv2d_fwd(ctypes.byref(d), _P(x), _P(wqs[i]), _P(biases[i]), _P(y),
-                                 0x100 if i else 0, stream())
+            with _Timed(d):
+                lib.rtsds_conv2d_fwd(ctypes.byref(d), _P(x), _P(wqs[i]), _P(biases[i]), _P(y),
+                                     0x100 if i else 0, stream())
             descs.append(d)
         ctx.descs = descs
         ctx.has_bias = [b is not None for b in biases]
@@ -116,15 +146,17 @@ class ConvSumFn(torch.autograd.Function):
                 if dx is None:
                     dx = empty_nhwc(d.n, d.c, d.h, d.w, x.dtype, x.device)
                 ws = workspace(lib.rtsds_conv2d_dgrad_workspace(ctypes.byref(d)), x.device)
-                lib.rtsds_conv2d_dgrad(ctypes.byref(d), _P(dy), _P(wqs[i]), _P(dx), 1 if i else 0,
-                                       _P(ws), ws.numel(), stream())
+                with _Timed(d):
+                    lib.rtsds_conv2d_dgrad(ctypes.byref(d), _P(dy), _P(wqs[i]), _P(dx), 1 if i else 0,
+                                           _P(ws), ws.numel(), stream())
             if ctx.needs_input_grad[2 + i] or ctx.needs_input_grad[2 + m + i]:
                 dw = torch.empty((d.k, d.c, d.kh, d.kw), dtype=torch.float32, device=x.device,
                                  memory_format=CL)
                 db = torch.empty(d.k, dtype=torch.float32, device=x.device) if ctx.has_bias[i] else None
                 ws = workspace(lib.rtsds_conv2d_wgrad_workspace(ctypes.byref(d)), x.device)
-                lib.rtsds_conv2d_wgrad(ctypes.byref(d), _P(x), _P(dy), _P(dw), _P(db), _P(ws),
-                                       ws.numel(), stream())
+                with _Timed(d):
+                    lib.rtsds_conv2d_wgrad(ctypes.byref(d), _P(x), _P(dy), _P(dw), _P(db), _P(ws),
+                                           ws.numel(), stream())
                 dws[i] = dw if ctx.needs_input_grad[2 + i] else None
                 dbs[i] = db
         return (dx, None, *dws, *dbs, *([None] * m))
@@ -414,7 +446,9 @@ class BilinearFn(torch.autograd.Function):
         n, hi, wi, c, ho, wo, sh, sw = ctx.geo
         dy = nhwc(dy)
         dx = empty_nhwc(n, c, hi, wi, dy.dtype, dy.device)
-        lib.rtsds_bilinear_bwd(_P(dy), _P(dx), n, hi, wi, c, ho, wo, sh, sw, c, 0, dcode(dy), stream())
+        ws = workspace(lib.rtsds_bilinear_bwd_workspace(n, hi, wi, c, ho, wo), dy.device)
+        lib.rtsds_bilinear_bwd(_P(dy), _P(dx), n, hi, wi, c, ho, wo, sh, sw, c, 0, dcode(dy), _P(ws),
+                               ws.numel(), stream())
         return dx, None, None, None, None
 
 

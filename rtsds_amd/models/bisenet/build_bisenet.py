@@ -137,7 +137,11 @@ class BiSeNet(torch.nn.Module):
             cx2_sup = F.interpolate_bilinear(self.supervision2(cx2), size=full)
         result = self.feature_fusion_module(sx, F.cat([cx1, cx2]))
         if self.with_interpolation:
-            result = self.conv(F.interpolate_bilinear(result, scale_factor=8))
+            # reference: conv(up8(result)) (build_bisenet.py:165-167).  A 1x1 conv mixes channels
+            # per pixel and bilinear resize mixes pixels per channel with weights summing to 1,
+            # so up8(conv(result)) is the same function (bias included) at 1/64 of the conv work
+            # and without the full-resolution intermediate.
+            result = F.interpolate_bilinear(self.conv(result), scale_factor=8)
         if self.training:
             return result, cx1_sup, cx2_sup
         return result

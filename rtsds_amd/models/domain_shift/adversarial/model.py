@@ -26,14 +26,15 @@ class GradientReversalFunction(Function):
 
 
 class UpSampler(nn.Module):
-    """model.py:19-28: x8 bilinear -> 1x1 conv."""
+    """model.py:19-28: x8 bilinear -> 1x1 conv, evaluated as 1x1 conv -> x8 bilinear (the two
+    commute exactly: see build_bisenet.BiSeNet.forward)."""
 
     def __init__(self, num_classes) -> None:
         super().__init__()
         self.conv = Conv2d(in_channels=num_classes, out_channels=num_classes, kernel_size=1)
 
     def forward(self, x):
-        return self.conv(F.interpolate_bilinear(_nhwc_input(x), scale_factor=8))
+        return F.interpolate_bilinear(self.conv(_nhwc_input(x)), scale_factor=8)
 
 
 def _nhwc_input(x):
