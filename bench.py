@@ -38,6 +38,7 @@ def parse():
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-infer", action="store_true")
+    ap.add_argument("--conv-report", action="store_true")
     return ap.parse_args()
 
 
@@ -130,8 +131,17 @@ def main():
     step(args.warmup + args.steps)
     torch.cuda.synchronize()
     recs, F.CONV_PROFILE = F.CONV_PROFILE, None
-    conv_ms = sum(a.elapsed_time(b) for a, b, _ in recs)
-    conv_flop = sum(f for _, _, f in recs)
+    conv_ms = sum(r[0].elapsed_time(r[1]) for r in recs)
+    conv_flop = sum(r[2] for r in recs)
+    if args.conv_report and rank == 0:
+        rows = []
+        for e0, e1, fl, tag, d in recs:
+            ms_ = e0.elapsed_time(e1)
+            rows.append((ms_, tag, f"n{d.n} {d.h}x{d.w}x{d.c} -> {d.ho}x{d.wo}x{d.k} k{d.kh} s{d.sh} d{d.dh}",
+                         fl / 1e9, fl / (ms_ * 1e-3) / 1e12))
+        rows.sort(reverse=True)
+        for r in rows:
+            print(f"{r[0]*1000:8.1f} us  {r[1]:5s} {r[2]:45s} {r[3]:7.2f} GF {r[4]:7.1f} TF/s", file=sys.stderr)
     achieved = conv_flop / (conv_ms * 1e-3) / 1e12
 
     # ---- inference FPS (eval forward, no grad)

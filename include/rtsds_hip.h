@@ -51,19 +51,22 @@ typedef struct {
  * build_contextpath.py:19-24; deeplabv2.py:13,19,24,56,73,99; model.py:54-58,69-70.
  * Implicit GEMM on MFMA (bf16: v_mfma_f32_16x16x32_bf16, f32: v_mfma_f32_16x16x4_f32).  */
 
-/* y = act(conv(x, w) + bias [+ y if act & RTSDS_ACCUMULATE]).  bias may be NULL (fp32 [k]). */
+/* y = act(conv(x, w) + bias [+ y if act & RTSDS_ACCUMULATE]).  bias may be NULL (fp32 [k]).
+ * ws >= rtsds_conv2d_fwd_workspace(d) (non-zero only when Cin needs channel padding).   */
+size_t rtsds_conv2d_fwd_workspace(const rtsds_conv_desc* d);
 int rtsds_conv2d_fwd(const rtsds_conv_desc* d, const void* x, const void* w, const float* bias,
-                     void* y, int act, void* stream);
+                     void* y, int act, void* ws, size_t ws_bytes, void* stream);
 /* dx (+)= conv_transpose(dy, w) (accumulate != 0: dx += ...).  Needs ws >=
  * rtsds_conv2d_dgrad_workspace(d).  Strides 1 and 2 only.                               */
 size_t rtsds_conv2d_dgrad_workspace(const rtsds_conv_desc* d);
 int rtsds_conv2d_dgrad(const rtsds_conv_desc* d, const void* dy, const void* w, void* dx,
                        int accumulate, void* ws, size_t ws_bytes, void* stream);
-/* dw (fp32 [k][kh][kw][c], overwritten) = sum_pixels dy (x) patch(x);
- * dbias (fp32 [k], overwritten, may be NULL) = sum_pixels dy.                            */
+/* dw (fp32 [k][kh][kw][c]) = sum_pixels dy (x) patch(x); dbias (fp32 [k], may be NULL) =
+ * sum_pixels dy.  accumulate != 0 adds into dw / dbias instead of overwriting (gradients go
+ * straight into the optimizer's flat gradient arena, replacing autograd's AccumulateGrad).  */
 size_t rtsds_conv2d_wgrad_workspace(const rtsds_conv_desc* d);
 int rtsds_conv2d_wgrad(const rtsds_conv_desc* d, const void* x, const void* dy, float* dw,
-                       float* dbias, void* ws, size_t ws_bytes, void* stream);
+                       float* dbias, int accumulate, void* ws, size_t ws_bytes, void* stream);
 
 /* ---------------------------------------------------------------- batch norm (train/eval)
  * Replaces nn.BatchNorm2d at build_bisenet.py:13,39; torchvision ResNet bn*; deeplabv2.py:14-27,
@@ -79,12 +82,12 @@ int rtsds_bn_fwd(const void* x, const void* res, void* y, long rows, int c, cons
                  float* save_invstd, float momentum, float eps, int training, int act, int dtype,
                  void* ws, size_t ws_bytes, void* stream);
 /* Backward of the fused BN(+res)(+act) above, given y (post-activation output) for the
- * activation mask.  dx, dres (may be NULL), dgamma/dbeta (fp32, overwritten, may be NULL).
- * training=0 gives the eval-mode backward (constant statistics).                         */
+ * activation mask.  dx, dres (may be NULL), dgamma/dbeta (fp32, may be NULL; overwritten, or
+ * added to when accumulate_params != 0).  training=0: eval-mode backward (constant stats). */
 int rtsds_bn_bwd(const void* dy, const void* x, const void* y, void* dx, void* dres,
                  float* dgamma, float* dbeta, long rows, int c, const float* gamma,
                  const float* save_mean, const float* save_invstd, int training, int act,
-                 int dtype, void* ws, size_t ws_bytes, void* stream);
+                 int accumulate_params, int dtype, void* ws, size_t ws_bytes, void* stream);
 
 /* ---------------------------------------------------------------- layout / dtype
  * Input images arrive NCHW fp32 from the reference's loaders (datasets/cityscapes.py:62,

@@ -249,7 +249,7 @@ __global__ void __launch_bounds__(256) bn_bwd_stats_kernel(const T* __restrict__
 // Backward pass 2: coefficients  dx = A*g + B*(x-mean) + C  per channel (one wave each).
 __global__ void __launch_bounds__(64) bn_bwd_finalize_kernel(const float* __restrict__ part, int nrb, int c, long rows, const float* gamma,
                                        const float* smean, const float* sinv, float* dgamma, float* dbeta,
-                                       float* coefA, float* coefB, float* coefC, int training) {
+                                       float* coefA, float* coefB, float* coefC, int training, int accumulate) {
   const int ch = blockIdx.x, lane = threadIdx.x;
   float sg = 0.f, sgx = 0.f;
   for (int b = lane; b < nrb; b += 64) {
@@ -260,8 +260,8 @@ __global__ void __launch_bounds__(64) bn_bwd_finalize_kernel(const float* __rest
   sgx = wave_sum(sgx);
   if (lane != 0) return;
   const float inv = sinv[ch], g = gamma ? gamma[ch] : 1.f;
-  if (dgamma) dgamma[ch] = sgx * inv;
-  if (dbeta) dbeta[ch] = sg;
+  if (dgamma) dgamma[ch] = accumulate ? dgamma[ch] + sgx * inv : sgx * inv;
+  if (dbeta) dbeta[ch] = accumulate ? dbeta[ch] + sg : sg;
   const float a = g * inv;
   const float invn = 1.f / (float)rows;
   coefA[ch] = a;
@@ -359,12 +359,12 @@ extern "C" int rtsds_bn_fwd(const void* x, const void* res, void* y, long rows, 
 template <typename T, int VEC>
 static void bn_bwd_launch(const void* dy, const void* x, const void* y, void* dx, void* dres, float* dgamma, float* dbeta,
                           long rows, int c, const float* gamma, const float* smean, const float* sinv, int training,
-                          int act, float* part, float* A, float* B, float* C, hipStream_t st) {
+                          int act, int accumulate, float* part, float* A, float* B, float* C, hipStream_t st) {
   const int rb = bn_rb(rows, c, VEC);
   hipLaunchKernelGGL((bn_bwd_stats_kernel<T, VEC>), dim3(rb, rt_cdiv(c, 256 * VEC)), dim3(256), 0, st, (const T*)dy, (const T*)x, (const T*)y, smean,
                      part, rows, c, act);
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(c), dim3(64), 0, st, part, rb, c, rows, gamma, smean, sinv,
-                     dgamma, dbeta, A, B, C, training);
+                     dgamma, dbeta, A, B, C, training, accumulate);
   if (dx || dres) {
     const long total = rows * ((c + VEC - 1) / VEC);
     const int blocks = (int)std::min<long>(8192, (total + 255) / 256);
@@ -375,7 +375,7 @@ static void bn_bwd_launch(const void* dy, const void* x, const void* y, void* dx
 
 extern "C" int rtsds_bn_bwd(const void* dy, const void* x, const void* y, void* dx, void* dres, float* dgamma, float* dbeta,
                             long rows, int c, const float* gamma, const float* save_mean, const float* save_invstd,
-                            int training, int act, int dtype, void* ws, size_t ws_bytes, void* stream) {
+                            int training, int act, int accumulate_params, int dtype, void* ws, size_t ws_bytes, void* stream) {
   if (rows <= 0 || c <= 0) return RTSDS_ERR_SHAPE;
   if (ws_bytes < rtsds_bn_workspace(rows, c)) return RTSDS_ERR_WORKSPACE;
   if (act && !y) return RTSDS_ERR_UNSUPPORTED;
@@ -385,11 +385,11 @@ extern "C" int rtsds_bn_bwd(const void* dy, const void* x, const void* y, void* 
   float* B = A + c;
   float* C = B + c;
   if (dtype == RTSDS_BF16) {
-    if (c % 8 == 0) bn_bwd_launch<bf16, 8>(dy, x, y, dx, dres, dgamma, dbeta, rows, c, gamma, save_mean, save_invstd, training, act, part, A, B, C, st);
-    else bn_bwd_launch<bf16, 1>(dy, x, y, dx, dres, dgamma, dbeta, rows, c, gamma, save_mean, save_invstd, training, act, part, A, B, C, st);
+    if (c % 8 == 0) bn_bwd_launch<bf16, 8>(dy, x, y, dx, dres, dgamma, dbeta, rows, c, gamma, save_mean, save_invstd, training, act, accumulate_params, part, A, B, C, st);
+    else bn_bwd_launch<bf16, 1>(dy, x, y, dx, dres, dgamma, dbeta, rows, c, gamma, save_mean, save_invstd, training, act, accumulate_params, part, A, B, C, st);
   } else if (dtype == RTSDS_F32) {
-    if (c % 4 == 0) bn_bwd_launch<float, 4>(dy, x, y, dx, dres, dgamma, dbeta, rows, c, gamma, save_mean, save_invstd, training, act, part, A, B, C, st);
-    else bn_bwd_launch<float, 1>(dy, x, y, dx, dres, dgamma, dbeta, rows, c, gamma, save_mean, save_invstd, training, act, part, A, B, C, st);
+    if (c % 4 == 0) bn_bwd_launch<float, 4>(dy, x, y, dx, dres, dgamma, dbeta, rows, c, gamma, save_mean, save_invstd, training, act, accumulate_params, part, A, B, C, st);
+    else bn_bwd_launch<float, 1>(dy, x, y, dx, dres, dgamma, dbeta, rows, c, gamma, save_mean, save_invstd, training, act, accumulate_params, part, A, B, C, st);
   } else return RTSDS_ERR_UNSUPPORTED;
   return hipGetLastError() == hipSuccess ? RTSDS_OK : RTSDS_ERR_LAUNCH;
 }

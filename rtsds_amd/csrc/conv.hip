@@ -433,25 +433,41 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(const ConvArgs P) {
 }
 
 // ---- small helper kernels -------------------------------------------------------------
-// W[co][r][s][ci] -> Wt[ci][r][s][co]   (DGRAD's B operand)
+// W[co][r][s][ci] -> Wt[ci][r][s][co_p] (DGRAD's B operand), zero for co >= co_n.
 template <typename T>
-__global__ void repack_wt_kernel(const T* __restrict__ w, T* __restrict__ wt, int co_n, int taps, int ci_n) {
-  const long total = (long)co_n * taps * ci_n;
+__global__ void repack_wt_kernel(const T* __restrict__ w, T* __restrict__ wt, int co_n, int co_p, int taps, int ci_n) {
+  const long total = (long)co_p * taps * ci_n;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    const int co = (int)(i % co_n);
-    const long rest = i / co_n;
+    const int co = (int)(i % co_p);
+    const long rest = i / co_p;
     const int tap = (int)(rest % taps);
     const int ci = (int)(rest / taps);
-    wt[i] = w[((long)co * taps + tap) * ci_n + ci];
+    wt[i] = co < co_n ? w[((long)co * taps + tap) * ci_n + ci] : (T)0.0f;
   }
 }
 
-// dw[i] = sum_s partial[s][i]
-__global__ void split_reduce_kernel(const float* __restrict__ part, float* __restrict__ out, long n, int splits) {
+// dst[r][j] = j < c ? src[r][j] : 0   (channel padding of an NHWC tensor or of [co][tap][ci] weights)
+template <typename T>
+__global__ void pad_channels_kernel(const T* __restrict__ src, T* __restrict__ dst, long rows, int c, int cp) {
+  const long total = rows * cp;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const long r = i / cp;
+    const int j = (int)(i - r * cp);
+    dst[i] = j < c ? src[r * c + j] : (T)0.0f;
+  }
+}
+
+// dw[co][tap][ci] = sum_s part[s][co][tap][ci_p]   (split-K reduce + channel unpad)
+__global__ void split_reduce_kernel(const float* __restrict__ part, float* __restrict__ out, int k, int taps, int c, int cp,
+                                    long slab, int splits, int accumulate) {
+  const long n = (long)k * taps * c;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const int ci = (int)(i % c);
+    const long rt = i / c;  // co * taps + tap
+    const long src = rt * cp + ci;
     float s = 0.f;
-    for (int k = 0; k < splits; ++k) s += part[(long)k * n + i];
-    out[i] = s;
+    for (int q = 0; q < splits; ++q) s += part[(long)q * slab + src];
+    out[i] = accumulate ? out[i] + s : s;
   }
 }
 
@@ -491,12 +507,12 @@ __global__ void __launch_bounds__(256) colsum_part_kernel(const T* __restrict__ 
       if (ch0 + j < c) part[(long)blockIdx.x * c + ch0 + j] = acc[j];
   }
 }
-__global__ void colsum_final_kernel(const float* __restrict__ part, float* __restrict__ out, int rb, int c) {
+__global__ void colsum_final_kernel(const float* __restrict__ part, float* __restrict__ out, int rb, int c, int accumulate) {
   const int cc = blockIdx.x, lane = threadIdx.x;
   float s = 0.f;
   for (int i = lane; i < rb; i += 64) s += part[(long)i * c + cc];
   s = wave_sum(s);
-  if (lane == 0) out[cc] = s;
+  if (lane == 0) out[cc] = accumulate ? out[cc] + s : s;
 }
 static const int kColsumRB = 1024;
 
@@ -525,9 +541,35 @@ static int check_desc(const rtsds_conv_desc* d) {
   const int wo = (d->w + 2 * d->pw - d->dw * (d->kw - 1) - 1) / d->sw + 1;
   if (ho != d->ho || wo != d->wo || ho <= 0 || wo <= 0) return RTSDS_ERR_SHAPE;
   if (d->dtype != RTSDS_F32 && d->dtype != RTSDS_BF16) return RTSDS_ERR_UNSUPPORTED;
-  if ((long)d->n * d->h * d->w * d->c >= (1L << 31) || (long)d->n * d->ho * d->wo * d->k >= (1L << 31))
+  if ((long)d->n * d->h * d->w * 32 * ((d->c + 31) / 32) >= (1L << 31) ||
+      (long)d->n * d->ho * d->wo * 32 * ((d->k + 31) / 32) >= (1L << 31))
     return RTSDS_ERR_UNSUPPORTED;
   return RTSDS_OK;
+}
+
+// Channel padding target so every gather runs on 16-B vectors: channel counts that are not a
+// multiple of the vector width (3-channel images, 19-class maps, the 1-channel D logit) are
+// zero-padded into workspace -- to a multiple of 32 (one filter tap per K-tile) when that
+// costs < 1.7x, else to the vector width.
+static int pad_c(int c, int dtype) {
+  const int V = dtype == RTSDS_BF16 ? 8 : 4;
+  if (c % V == 0) return c;
+  const int c32 = (c + 31) / 32 * 32;
+  if (c >= 8 && c32 * 10 < c * 17) return c32;
+  return (c + V - 1) / V * V;
+}
+static size_t al256(size_t b) { return (b + 255) & ~(size_t)255; }
+static size_t esize(int dtype) { return dtype == RTSDS_BF16 ? 2 : 4; }
+
+template <typename T>
+static void pad_launch(const void* src, void* dst, long rows, int c, int cp, hipStream_t st) {
+  const long total = rows * cp;
+  const int blocks = (int)std::max<long>(1, std::min<long>(8192, (total + 255) / 256));
+  hipLaunchKernelGGL(pad_channels_kernel<T>, dim3(blocks), dim3(256), 0, st, (const T*)src, (T*)dst, rows, c, cp);
+}
+static void pad_any(int dtype, const void* src, void* dst, long rows, int c, int cp, hipStream_t st) {
+  if (dtype == RTSDS_BF16) pad_launch<bf16>(src, dst, rows, c, cp, st);
+  else pad_launch<float>(src, dst, rows, c, cp, st);
 }
 
 template <typename T, int MODE, int BM, int BN, int BK, int WM, int WN, int ALA, int ALB>
@@ -536,169 +578,222 @@ static void launch(const ConvArgs& p, int splits, hipStream_t st) {
   hipLaunchKernelGGL((conv_gemm_kernel<T, MODE, BM, BN, BK, WM, WN, ALA, ALB>), grid, dim3(256), 0, st, p);
 }
 
-// Tile selection for FWD / DGRAD.  bf16: 128x128 (2x2 waves of 64x64) for wide outputs,
-// 128x64 for 64-channel outputs, 256x32 for the 19/1-channel heads; f32: 64x64 / 128x32.
-template <typename T, int MODE, int ALA, int ALB>
+// Tile selection for FWD / DGRAD (occupancy-aware): the widest tile that still puts >= 256
+// workgroups on the 256 CUs.  bf16: 128x128 / 128x64 / 256x32 (19- and 1-channel outputs),
+// falling back to 64x64 / 128x32 for small-M layers (ResNet layer4, pooled vectors).
+template <typename T, int MODE, int ALA>
 static void dispatch_mn(const ConvArgs& p, hipStream_t st) {
   constexpr int BK = sizeof(T) == 2 ? 32 : 16;
+  auto blocks = [&](int bm, int bn) { return (long)rt_cdiv(p.M, bm) * rt_cdiv(p.N, bn); };
   if (sizeof(T) == 2) {
-    if (p.N <= 32) launch<T, MODE, 256, 32, BK, 4, 1, ALA, ALB>(p, 1, st);
-    else if (p.N <= 64) launch<T, MODE, 128, 64, BK, 2, 2, ALA, ALB>(p, 1, st);
-    else launch<T, MODE, 128, 128, BK, 2, 2, ALA, ALB>(p, 1, st);
+    if (p.N <= 32) {
+      if (blocks(256, 32) >= 256) launch<T, MODE, 256, 32, BK, 4, 1, ALA, 1>(p, 1, st);
+      else launch<T, MODE, 128, 32, BK, 4, 1, ALA, 1>(p, 1, st);
+    } else if (p.N <= 64) {
+      if (blocks(128, 64) >= 256) launch<T, MODE, 128, 64, BK, 2, 2, ALA, 1>(p, 1, st);
+      else launch<T, MODE, 64, 64, BK, 2, 2, ALA, 1>(p, 1, st);
+    } else {
+      if (blocks(128, 128) >= 256) launch<T, MODE, 128, 128, BK, 2, 2, ALA, 1>(p, 1, st);
+      else launch<T, MODE, 64, 64, BK, 2, 2, ALA, 1>(p, 1, st);
+    }
   } else {
-    if (p.N <= 32) launch<T, MODE, 128, 32, BK, 4, 1, ALA, ALB>(p, 1, st);
-    else launch<T, MODE, 64, 64, BK, 2, 2, ALA, ALB>(p, 1, st);
+    if (p.N <= 32) launch<T, MODE, 128, 32, BK, 4, 1, ALA, 1>(p, 1, st);
+    else launch<T, MODE, 64, 64, BK, 2, 2, ALA, 1>(p, 1, st);
   }
 }
 
 template <typename T, int MODE>
 static void dispatch_align(const ConvArgs& p, int cr, hipStream_t st) {
-  constexpr int V = VecT<T>::N;
   constexpr int BK = sizeof(T) == 2 ? 32 : 16;
-  const int alb = (p.K % V == 0) ? 1 : 0;
-  if (cr % BK == 0) {
-    if (alb) dispatch_mn<T, MODE, 2, 1>(p, st); else dispatch_mn<T, MODE, 2, 0>(p, st);
-  } else if (cr % V == 0) {
-    if (alb) dispatch_mn<T, MODE, 1, 1>(p, st); else dispatch_mn<T, MODE, 1, 0>(p, st);
-  } else {
-    if (alb) dispatch_mn<T, MODE, 0, 1>(p, st); else dispatch_mn<T, MODE, 0, 0>(p, st);
-  }
+  if (cr % BK == 0) dispatch_mn<T, MODE, 2>(p, st);
+  else dispatch_mn<T, MODE, 1>(p, st);
 }
 
-extern "C" int rtsds_conv2d_fwd(const rtsds_conv_desc* d, const void* x, const void* w, const float* bias,
-                                void* y, int act, void* stream) {
-  int e = check_desc(d);
+// FWD workspace: channel-padded copies of x and w when Cin is not a vector multiple.
+extern "C" size_t rtsds_conv2d_fwd_workspace(const rtsds_conv_desc* d) {
+  const int cp = pad_c(d->c, d->dtype);
+  if (cp == d->c) return 0;
+  const size_t es = esize(d->dtype);
+  return al256((size_t)d->n * d->h * d->w * cp * es) + al256((size_t)d->k * d->kh * d->kw * cp * es);
+}
+
+extern "C" int rtsds_conv2d_fwd(const rtsds_conv_desc* d0, const void* x, const void* w, const float* bias,
+                                void* y, int act, void* ws, size_t ws_bytes, void* stream) {
+  int e = check_desc(d0);
   if (e) return e;
-  ConvArgs p = make_args(d);
+  if (ws_bytes < rtsds_conv2d_fwd_workspace(d0)) return RTSDS_ERR_WORKSPACE;
+  hipStream_t st = (hipStream_t)stream;
+  rtsds_conv_desc d = *d0;
+  const int cp = pad_c(d.c, d.dtype);
+  if (cp != d.c) {
+    const size_t es = esize(d.dtype);
+    void* xp = ws;
+    void* wp = (char*)ws + al256((size_t)d.n * d.h * d.w * cp * es);
+    pad_any(d.dtype, x, xp, (long)d.n * d.h * d.w, d.c, cp, st);
+    pad_any(d.dtype, w, wp, (long)d.k * d.kh * d.kw, d.c, cp, st);
+    x = xp;
+    w = wp;
+    d.c = cp;
+  }
+  ConvArgs p = make_args(&d);
   p.a = x; p.b = w; p.bias = bias; p.out = y;
   p.act = act & 0xff;
   p.accum = (act & RTSDS_ACCUMULATE) ? 1 : 0;
-  p.M = d->n * d->ho * d->wo;
-  p.N = d->k;
-  p.K = d->kh * d->kw * d->c;
-  hipStream_t st = (hipStream_t)stream;
-  if (d->dtype == RTSDS_BF16) dispatch_align<bf16, MODE_FWD>(p, d->c, st);
-  else dispatch_align<float, MODE_FWD>(p, d->c, st);
+  p.M = d.n * d.ho * d.wo;
+  p.N = d.k;
+  p.K = d.kh * d.kw * d.c;
+  if (d.dtype == RTSDS_BF16) dispatch_align<bf16, MODE_FWD>(p, d.c, st);
+  else dispatch_align<float, MODE_FWD>(p, d.c, st);
   return hipGetLastError() == hipSuccess ? RTSDS_OK : RTSDS_ERR_LAUNCH;
 }
 
+// DGRAD workspace: repacked (and Cout-padded) weights + a Cout-padded copy of dy if needed.
 extern "C" size_t rtsds_conv2d_dgrad_workspace(const rtsds_conv_desc* d) {
-  const size_t es = d->dtype == RTSDS_BF16 ? 2 : 4;
-  return ((size_t)d->k * d->kh * d->kw * d->c * es + 255) & ~(size_t)255;
+  const int kp = pad_c(d->k, d->dtype);
+  const size_t es = esize(d->dtype);
+  size_t b = al256((size_t)kp * d->kh * d->kw * d->c * es);
+  if (kp != d->k) b += al256((size_t)d->n * d->ho * d->wo * kp * es);
+  return b;
 }
 
-extern "C" int rtsds_conv2d_dgrad(const rtsds_conv_desc* d, const void* dy, const void* w, void* dx,
+extern "C" int rtsds_conv2d_dgrad(const rtsds_conv_desc* d0, const void* dy, const void* w, void* dx,
                                   int accumulate, void* ws, size_t ws_bytes, void* stream) {
-  int e = check_desc(d);
+  int e = check_desc(d0);
   if (e) return e;
-  if (d->sh > 2 || d->sw > 2) return RTSDS_ERR_UNSUPPORTED;
-  if (ws_bytes < rtsds_conv2d_dgrad_workspace(d)) return RTSDS_ERR_WORKSPACE;
+  if (d0->sh > 2 || d0->sw > 2) return RTSDS_ERR_UNSUPPORTED;
+  if (ws_bytes < rtsds_conv2d_dgrad_workspace(d0)) return RTSDS_ERR_WORKSPACE;
   hipStream_t st = (hipStream_t)stream;
-  const int taps = d->kh * d->kw;
-  const long wn = (long)d->k * taps * d->c;
+  rtsds_conv_desc d = *d0;
+  const int taps = d.kh * d.kw;
+  const int kp = pad_c(d.k, d.dtype);
+  const size_t es = esize(d.dtype);
+  void* wt = ws;
+  const long wn = (long)kp * taps * d.c;
   const int blocks = (int)std::min<long>(4096, (wn + 255) / 256);
-  if (d->dtype == RTSDS_BF16)
-    hipLaunchKernelGGL(repack_wt_kernel<bf16>, dim3(blocks), dim3(256), 0, st, (const bf16*)w, (bf16*)ws, d->k, taps, d->c);
+  if (d.dtype == RTSDS_BF16)
+    hipLaunchKernelGGL(repack_wt_kernel<bf16>, dim3(blocks), dim3(256), 0, st, (const bf16*)w, (bf16*)wt, d.k, kp, taps, d.c);
   else
-    hipLaunchKernelGGL(repack_wt_kernel<float>, dim3(blocks), dim3(256), 0, st, (const float*)w, (float*)ws, d->k, taps, d->c);
-  ConvArgs p = make_args(d);
-  p.a = dy; p.b = ws; p.bias = nullptr; p.out = dx; p.act = 0;
+    hipLaunchKernelGGL(repack_wt_kernel<float>, dim3(blocks), dim3(256), 0, st, (const float*)w, (float*)wt, d.k, kp, taps, d.c);
+  if (kp != d.k) {
+    void* dyp = (char*)ws + al256((size_t)kp * taps * d.c * es);
+    pad_any(d.dtype, dy, dyp, (long)d.n * d.ho * d.wo, d.k, kp, st);
+    dy = dyp;
+    d.k = kp;
+  }
+  ConvArgs p = make_args(&d);
+  p.a = dy; p.b = wt; p.bias = nullptr; p.out = dx; p.act = 0;
   p.accum = accumulate ? 1 : 0;
-  p.M = d->n * d->h * d->w;
-  p.N = d->c;
-  p.K = taps * d->k;
-  if (d->dtype == RTSDS_BF16) dispatch_align<bf16, MODE_DGRAD>(p, d->k, st);
-  else dispatch_align<float, MODE_DGRAD>(p, d->k, st);
+  p.M = d.n * d.h * d.w;
+  p.N = d.c;
+  p.K = taps * d.k;
+  if (d.dtype == RTSDS_BF16) dispatch_align<bf16, MODE_DGRAD>(p, d.k, st);
+  else dispatch_align<float, MODE_DGRAD>(p, d.k, st);
   return hipGetLastError() == hipSuccess ? RTSDS_OK : RTSDS_ERR_LAUNCH;
 }
 
 // WGRAD split-K: enough (M/BM)*(N/BN)*splits workgroups to fill 256 CUs ~2x, each split at
-// least 8 K-tiles; fp32 partial slabs summed by split_reduce_kernel (deterministic).
-static void wgrad_plan(const rtsds_conv_desc* d, int& bm, int& bn, int& splits, int& tps) {
+// least 8 K-tiles; fp32 partial slabs summed (and channel-unpadded) by split_reduce_kernel --
+// deterministic, no atomics.
+struct WgradPlan {
+  int kp, cp, bm, bn, splits, tps;
+  size_t slab_bytes, dyp_bytes, xp_bytes, colsum_bytes;
+};
+static WgradPlan wgrad_plan(const rtsds_conv_desc* d) {
+  WgradPlan w;
   const bool b16 = d->dtype == RTSDS_BF16;
-  const int M = d->k, N = d->kh * d->kw * d->c;
+  w.kp = pad_c(d->k, d->dtype);
+  w.cp = pad_c(d->c, d->dtype);
+  const int M = w.kp, N = d->kh * d->kw * w.cp;
   const long R = (long)d->n * d->ho * d->wo;
   const int BK = b16 ? 32 : 16;
-  bm = b16 ? (M <= 64 ? 64 : 128) : 64;
-  bn = b16 ? (N <= 64 ? 64 : 128) : 64;
-  const long tiles = (long)rt_cdiv(M, bm) * rt_cdiv(N, bn);
+  w.bm = b16 ? (M <= 64 ? 64 : 128) : 64;
+  w.bn = b16 ? (N <= 64 ? 64 : 128) : 64;
+  const long tiles = (long)rt_cdiv(M, w.bm) * rt_cdiv(N, w.bn);
   const long nk = (R + BK - 1) / BK;
   long want = std::max<long>(1, 512 / tiles);
   want = std::min<long>(want, std::max<long>(1, nk / 8));
   want = std::min<long>(want, 256);
-  tps = (int)((nk + want - 1) / want);
-  splits = (int)((nk + tps - 1) / tps);
+  w.tps = (int)((nk + want - 1) / want);
+  w.splits = (int)((nk + w.tps - 1) / w.tps);
+  const size_t es = esize(d->dtype);
+  w.slab_bytes = al256((size_t)w.splits * M * N * 4);
+  w.dyp_bytes = w.kp != d->k ? al256((size_t)R * w.kp * es) : 0;
+  w.xp_bytes = w.cp != d->c ? al256((size_t)d->n * d->h * d->w * w.cp * es) : 0;
+  w.colsum_bytes = al256((size_t)kColsumRB * d->k * 4);
+  return w;
 }
 
 extern "C" size_t rtsds_conv2d_wgrad_workspace(const rtsds_conv_desc* d) {
-  int bm, bn, splits, tps;
-  wgrad_plan(d, bm, bn, splits, tps);
-  size_t slab = splits <= 1 ? 0 : ((size_t)splits * d->k * d->kh * d->kw * d->c * 4 + 255) & ~(size_t)255;
-  return slab + (((size_t)kColsumRB * d->k * 4 + 255) & ~(size_t)255);
+  const WgradPlan w = wgrad_plan(d);
+  return w.slab_bytes + w.dyp_bytes + w.xp_bytes + w.colsum_bytes;
 }
 
-template <typename T, int ALA, int ALB>
+template <typename T>
 static void wgrad_launch(const ConvArgs& p, int bm, int bn, int splits, hipStream_t st) {
   constexpr int BK = sizeof(T) == 2 ? 32 : 16;
   if (sizeof(T) == 2) {
-    if (bm == 64 && bn == 64) launch<T, MODE_WGRAD, 64, 64, BK, 2, 2, ALA, ALB>(p, splits, st);
-    else if (bm == 64) launch<T, MODE_WGRAD, 64, 128, BK, 2, 2, ALA, ALB>(p, splits, st);
-    else if (bn == 64) launch<T, MODE_WGRAD, 128, 64, BK, 2, 2, ALA, ALB>(p, splits, st);
-    else launch<T, MODE_WGRAD, 128, 128, BK, 2, 2, ALA, ALB>(p, splits, st);
+    if (bm == 64 && bn == 64) launch<T, MODE_WGRAD, 64, 64, BK, 2, 2, 1, 1>(p, splits, st);
+    else if (bm == 64) launch<T, MODE_WGRAD, 64, 128, BK, 2, 2, 1, 1>(p, splits, st);
+    else if (bn == 64) launch<T, MODE_WGRAD, 128, 64, BK, 2, 2, 1, 1>(p, splits, st);
+    else launch<T, MODE_WGRAD, 128, 128, BK, 2, 2, 1, 1>(p, splits, st);
   } else {
-    launch<T, MODE_WGRAD, 64, 64, BK, 2, 2, ALA, ALB>(p, splits, st);
+    launch<T, MODE_WGRAD, 64, 64, BK, 2, 2, 1, 1>(p, splits, st);
   }
 }
 
-extern "C" int rtsds_conv2d_wgrad(const rtsds_conv_desc* d, const void* x, const void* dy, float* dw,
-                                  float* dbias, void* ws, size_t ws_bytes, void* stream) {
-  int e = check_desc(d);
+extern "C" int rtsds_conv2d_wgrad(const rtsds_conv_desc* d0, const void* x, const void* dy, float* dw,
+                                  float* dbias, int accumulate, void* ws, size_t ws_bytes, void* stream) {
+  int e = check_desc(d0);
   if (e) return e;
-  if (ws_bytes < rtsds_conv2d_wgrad_workspace(d)) return RTSDS_ERR_WORKSPACE;
+  if (ws_bytes < rtsds_conv2d_wgrad_workspace(d0)) return RTSDS_ERR_WORKSPACE;
   hipStream_t st = (hipStream_t)stream;
-  int bm, bn, splits, tps;
-  wgrad_plan(d, bm, bn, splits, tps);
-  ConvArgs p = make_args(d);
-  p.a = dy; p.b = x; p.bias = nullptr; p.act = 0;
-  p.M = d->k;
-  p.N = d->kh * d->kw * d->c;
-  p.K = d->n * d->ho * d->wo;
-  p.tiles_per_split = tps;
-  p.split_stride = (long)p.M * p.N;
-  p.out = splits > 1 ? ws : (void*)dw;
-  const bool b16 = d->dtype == RTSDS_BF16;
-  const int V = b16 ? 8 : 4;
-  const int ala = d->k % V == 0, alb = d->c % V == 0;
-  if (b16) {
-    if (ala && alb) wgrad_launch<bf16, 1, 1>(p, bm, bn, splits, st);
-    else if (ala) wgrad_launch<bf16, 1, 0>(p, bm, bn, splits, st);
-    else if (alb) wgrad_launch<bf16, 0, 1>(p, bm, bn, splits, st);
-    else wgrad_launch<bf16, 0, 0>(p, bm, bn, splits, st);
-  } else {
-    if (ala && alb) wgrad_launch<float, 1, 1>(p, bm, bn, splits, st);
-    else if (ala) wgrad_launch<float, 1, 0>(p, bm, bn, splits, st);
-    else if (alb) wgrad_launch<float, 0, 1>(p, bm, bn, splits, st);
-    else wgrad_launch<float, 0, 0>(p, bm, bn, splits, st);
+  const WgradPlan pl = wgrad_plan(d0);
+  char* slab = (char*)ws;
+  char* dyp = slab + pl.slab_bytes;
+  char* xp = dyp + pl.dyp_bytes;
+  float* part = (float*)(xp + pl.xp_bytes);
+  const long R = (long)d0->n * d0->ho * d0->wo;
+  rtsds_conv_desc d = *d0;
+  const void* dyk = dy;
+  if (pl.kp != d.k) {
+    pad_any(d.dtype, dy, dyp, R, d.k, pl.kp, st);
+    dyk = dyp;
+    d.k = pl.kp;
   }
-  if (splits > 1) {
-    const long n = p.split_stride;
+  if (pl.cp != d.c) {
+    pad_any(d.dtype, x, xp, (long)d.n * d.h * d.w, d.c, pl.cp, st);
+    x = xp;
+    d.c = pl.cp;
+  }
+  ConvArgs p = make_args(&d);
+  p.a = dyk; p.b = x; p.bias = nullptr; p.act = 0;
+  p.M = d.k;
+  p.N = d.kh * d.kw * d.c;
+  p.K = (int)R;
+  p.tiles_per_split = pl.tps;
+  p.split_stride = (long)p.M * p.N;
+  p.out = slab;
+  if (d.dtype == RTSDS_BF16) wgrad_launch<bf16>(p, pl.bm, pl.bn, pl.splits, st);
+  else wgrad_launch<float>(p, pl.bm, pl.bn, pl.splits, st);
+  {
+    const long n = (long)d0->k * d0->kh * d0->kw * d0->c;
     const int blocks = (int)std::min<long>(2048, (n + 255) / 256);
-    hipLaunchKernelGGL(split_reduce_kernel, dim3(blocks), dim3(256), 0, st, (const float*)ws, dw, n, splits);
+    hipLaunchKernelGGL(split_reduce_kernel, dim3(blocks), dim3(256), 0, st, (const float*)slab, dw, d0->k, d0->kh * d0->kw,
+                       d0->c, pl.cp, p.split_stride, pl.splits, accumulate);
   }
   if (dbias) {
-    const long rows = (long)d->n * d->ho * d->wo;
-    const size_t slab = splits <= 1 ? 0 : ((size_t)splits * p.split_stride * 4 + 255) & ~(size_t)255;
-    float* part = (float*)((char*)ws + slab);
-    const int rb = (int)std::max<long>(1, std::min<long>(kColsumRB, rows / 64));
-    if (b16 && d->k % 8 == 0)
-      hipLaunchKernelGGL((colsum_part_kernel<bf16, 8>), dim3(rb, rt_cdiv(d->k, 2048)), dim3(256), 0, st, (const bf16*)dy, part, rows, d->k);
+    const int k = d0->k;
+    const int rb = (int)std::max<long>(1, std::min<long>(kColsumRB, R / 64));
+    const bool b16 = d0->dtype == RTSDS_BF16;
+    if (b16 && k % 8 == 0)
+      hipLaunchKernelGGL((colsum_part_kernel<bf16, 8>), dim3(rb, rt_cdiv(k, 2048)), dim3(256), 0, st, (const bf16*)dy, part, R, k);
     else if (b16)
-      hipLaunchKernelGGL((colsum_part_kernel<bf16, 1>), dim3(rb, rt_cdiv(d->k, 256)), dim3(256), 0, st, (const bf16*)dy, part, rows, d->k);
-    else if (d->k % 4 == 0)
-      hipLaunchKernelGGL((colsum_part_kernel<float, 4>), dim3(rb, rt_cdiv(d->k, 1024)), dim3(256), 0, st, (const float*)dy, part, rows, d->k);
+      hipLaunchKernelGGL((colsum_part_kernel<bf16, 1>), dim3(rb, rt_cdiv(k, 256)), dim3(256), 0, st, (const bf16*)dy, part, R, k);
+    else if (k % 4 == 0)
+      hipLaunchKernelGGL((colsum_part_kernel<float, 4>), dim3(rb, rt_cdiv(k, 1024)), dim3(256), 0, st, (const float*)dy, part, R, k);
     else
-      hipLaunchKernelGGL((colsum_part_kernel<float, 1>), dim3(rb, rt_cdiv(d->k, 256)), dim3(256), 0, st, (const float*)dy, part, rows, d->k);
-    hipLaunchKernelGGL(colsum_final_kernel, dim3(d->k), dim3(64), 0, st, (const float*)part, dbias, rb, d->k);
+      hipLaunchKernelGGL((colsum_part_kernel<float, 1>), dim3(rb, rt_cdiv(k, 256)), dim3(256), 0, st, (const float*)dy, part, R, k);
+    hipLaunchKernelGGL(colsum_final_kernel, dim3(k), dim3(64), 0, st, (const float*)part, dbias, rb, k, accumulate);
   }
   return hipGetLastError() == hipSuccess ? RTSDS_OK : RTSDS_ERR_LAUNCH;
 }

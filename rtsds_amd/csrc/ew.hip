@@ -183,18 +183,108 @@ __global__ void maxpool_bwd_kernel(const T* __restrict__ dy, const uint8_t* __re
     dx[i] = from_f<T>(acc);
   }
 }
+
+// Vector variants (c % V == 0): one thread per (pixel, 16-B channel vector).
+template <typename T>
+__global__ void maxpool_fwd_vec(const T* __restrict__ x, T* __restrict__ y, uint8_t* __restrict__ idx, int n, int h, int w,
+                                int c, int ho, int wo, int k, int s, int p) {
+  typedef typename VecT<T>::v16 V16;
+  constexpr int V = VecT<T>::N;
+  const int cv = c / V;
+  const long total = (long)n * ho * wo * cv;
+  GRID_STRIDE(i, total) {
+    const int ch = (int)(i % cv) * V;
+    long q = i / cv;
+    const int ow = (int)(q % wo); q /= wo;
+    const int oh = (int)(q % ho);
+    const int img = (int)(q / ho);
+    const int h0 = oh * s - p, w0 = ow * s - p;
+    float best[V];
+    int bi[V];
+#pragma unroll
+    for (int j = 0; j < V; ++j) { best[j] = -INFINITY; bi[j] = -1; }
+    for (int a = 0; a < k; ++a) {
+      const int hh = h0 + a;
+      if (hh < 0 || hh >= h) continue;
+      for (int b = 0; b < k; ++b) {
+        const int ww = w0 + b;
+        if (ww < 0 || ww >= w) continue;
+        const V16 v = *(const V16*)(x + (((long)img * h + hh) * w + ww) * c + ch);
+#pragma unroll
+        for (int j = 0; j < V; ++j) {
+          const float f = to_f(v[j]);
+          if (bi[j] < 0 || f > best[j] || (f != f && best[j] == best[j])) { best[j] = f; bi[j] = a * k + b; }
+        }
+      }
+    }
+    V16 o;
+    const long oi = (((long)img * ho + oh) * wo + ow) * c + ch;
+#pragma unroll
+    for (int j = 0; j < V; ++j) { o[j] = from_f<T>(best[j]); idx[oi + j] = (uint8_t)(bi[j] < 0 ? 0 : bi[j]); }
+    *(V16*)(y + oi) = o;
+  }
+}
+template <typename T>
+__global__ void maxpool_bwd_vec(const T* __restrict__ dy, const uint8_t* __restrict__ idx, T* __restrict__ dx, int n, int h, int w,
+                                int c, int ho, int wo, int k, int s, int p) {
+  typedef typename VecT<T>::v16 V16;
+  constexpr int V = VecT<T>::N;
+  const int cv = c / V;
+  const long total = (long)n * h * w * cv;
+  GRID_STRIDE(i, total) {
+    const int ch = (int)(i % cv) * V;
+    long q = i / cv;
+    const int iw = (int)(q % w); q /= w;
+    const int ih = (int)(q % h);
+    const int img = (int)(q / h);
+    const int oh_lo = max(0, (ih + p - k + s) / s), oh_hi = min(ho - 1, (ih + p) / s);
+    const int ow_lo = max(0, (iw + p - k + s) / s), ow_hi = min(wo - 1, (iw + p) / s);
+    float acc[V];
+#pragma unroll
+    for (int j = 0; j < V; ++j) acc[j] = 0.f;
+    for (int oh = oh_lo; oh <= oh_hi; ++oh) {
+      const int a = ih - (oh * s - p);
+      if (a < 0 || a >= k) continue;
+      for (int ow = ow_lo; ow <= ow_hi; ++ow) {
+        const int b = iw - (ow * s - p);
+        if (b < 0 || b >= k) continue;
+        const long o = (((long)img * ho + oh) * wo + ow) * c + ch;
+        const V16 g = *(const V16*)(dy + o);
+        const int want = a * k + b;
+#pragma unroll
+        for (int j = 0; j < V; ++j)
+          if (idx[o + j] == want) acc[j] += to_f(g[j]);
+      }
+    }
+    V16 r;
+#pragma unroll
+    for (int j = 0; j < V; ++j) r[j] = from_f<T>(acc[j]);
+    *(V16*)(dx + (((long)img * h + ih) * w + iw) * c + ch) = r;
+  }
+}
+
 extern "C" int rtsds_maxpool_fwd(const void* x, void* y, uint8_t* idx, int n, int h, int w, int c, int ho, int wo, int k, int s,
                                  int p, int dtype, void* stream) {
   if (k * k > 255 || n <= 0 || ho <= 0 || wo <= 0) return RTSDS_ERR_SHAPE;
   const long total = (long)n * ho * wo * c;
-  DISPATCH_T(dtype, hipLaunchKernelGGL(maxpool_fwd_kernel<T>, dim3(ew_blocks(total)), dim3(256), 0, (hipStream_t)stream, (const T*)x, (T*)y, idx, n, h, w, c, ho, wo, k, s, p));
+  DISPATCH_T(dtype, {
+    if (c % VecT<T>::N == 0)
+      hipLaunchKernelGGL(maxpool_fwd_vec<T>, dim3(ew_blocks(total / VecT<T>::N)), dim3(256), 0, (hipStream_t)stream, (const T*)x, (T*)y, idx, n, h, w, c, ho, wo, k, s, p);
+    else
+      hipLaunchKernelGGL(maxpool_fwd_kernel<T>, dim3(ew_blocks(total)), dim3(256), 0, (hipStream_t)stream, (const T*)x, (T*)y, idx, n, h, w, c, ho, wo, k, s, p);
+  });
   RET_LAUNCH();
 }
 extern "C" int rtsds_maxpool_bwd(const void* dy, const uint8_t* idx, void* dx, int n, int h, int w, int c, int ho, int wo, int k,
                                  int s, int p, int dtype, void* stream) {
   const long total = (long)n * h * w * c;
   if (total <= 0) return RTSDS_ERR_SHAPE;
-  DISPATCH_T(dtype, hipLaunchKernelGGL(maxpool_bwd_kernel<T>, dim3(ew_blocks(total)), dim3(256), 0, (hipStream_t)stream, (const T*)dy, idx, (T*)dx, n, h, w, c, ho, wo, k, s, p));
+  DISPATCH_T(dtype, {
+    if (c % VecT<T>::N == 0)
+      hipLaunchKernelGGL(maxpool_bwd_vec<T>, dim3(ew_blocks(total / VecT<T>::N)), dim3(256), 0, (hipStream_t)stream, (const T*)dy, idx, (T*)dx, n, h, w, c, ho, wo, k, s, p);
+    else
+      hipLaunchKernelGGL(maxpool_bwd_kernel<T>, dim3(ew_blocks(total)), dim3(256), 0, (hipStream_t)stream, (const T*)dy, idx, (T*)dx, n, h, w, c, ho, wo, k, s, p);
+  });
   RET_LAUNCH();
 }
 
@@ -466,6 +556,90 @@ extern "C" int rtsds_bilinear_bwd(const void* dy, void* dx, int n, int hi, int w
   RET_LAUNCH();
 }
 
+
+// ------------------------------------------------------------------ LDS-staged per-pixel kernels
+// The per-pixel channel loops (C = 19 classes) read/write rows of C*sizeof(T) bytes (38 B for
+// bf16) that are not 16-B aligned per pixel.  These variants move a block's 256 pixels
+// (256*C elements, contiguous in NHWC) between HBM and LDS with 16-B vector accesses and
+// run the per-pixel math out of LDS, so global traffic is fully coalesced.
+static const int kStagePix = 256;
+template <typename T>
+RT_DEV void stage_in(const T* __restrict__ g, T* s, int nel) {
+  const int nb = nel * (int)sizeof(T);
+  const char* gb = (const char*)g;
+  char* sb = (char*)s;
+  if ((((uintptr_t)gb) & 15) == 0) {
+    const int nv = nb >> 4;
+    for (int i = threadIdx.x; i < nv; i += blockDim.x) ((uint4*)sb)[i] = ((const uint4*)gb)[i];
+    for (int i = (nv << 4) / (int)sizeof(T) + threadIdx.x; i < nel; i += blockDim.x) s[i] = g[i];
+  } else {
+    for (int i = threadIdx.x; i < nel; i += blockDim.x) s[i] = g[i];
+  }
+}
+template <typename T>
+RT_DEV void stage_out(T* __restrict__ g, const T* s, int nel) {
+  const int nb = nel * (int)sizeof(T);
+  char* gb = (char*)g;
+  const char* sb = (const char*)s;
+  if ((((uintptr_t)gb) & 15) == 0) {
+    const int nv = nb >> 4;
+    for (int i = threadIdx.x; i < nv; i += blockDim.x) ((uint4*)gb)[i] = ((const uint4*)sb)[i];
+    for (int i = (nv << 4) / (int)sizeof(T) + threadIdx.x; i < nel; i += blockDim.x) g[i] = s[i];
+  } else {
+    for (int i = threadIdx.x; i < nel; i += blockDim.x) g[i] = s[i];
+  }
+}
+// Staged variants need NHWC-contiguous logits with c <= kStageMaxC.
+static const int kStageMaxC = 64;
+static inline bool stage_ok(long sn, long sc, long shw, long hw, int c) {
+  return sc == 1 && shw == c && sn == hw * c && c <= kStageMaxC;
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) softmax_fwd_staged(const T* __restrict__ x, T* __restrict__ y, long total, int c) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  T* buf = (T*)smem_raw;
+  for (long p0 = (long)blockIdx.x * kStagePix; p0 < total; p0 += (long)gridDim.x * kStagePix) {
+    const int np = (int)min<long>(kStagePix, total - p0);
+    __syncthreads();
+    stage_in(x + p0 * c, buf, np * c);
+    __syncthreads();
+    if ((int)threadIdx.x < np) {
+      T* r = buf + threadIdx.x * c;
+      float m = -INFINITY;
+      for (int k = 0; k < c; ++k) m = fmaxf(m, to_f(r[k]));
+      float z = 0.f;
+      for (int k = 0; k < c; ++k) z += expf(to_f(r[k]) - m);
+      const float iz = 1.f / z;
+      for (int k = 0; k < c; ++k) r[k] = from_f<T>(expf(to_f(r[k]) - m) * iz);
+    }
+    __syncthreads();
+    stage_out(y + p0 * c, buf, np * c);
+  }
+}
+template <typename T>
+__global__ void __launch_bounds__(256) softmax_bwd_staged(const T* __restrict__ dy, const T* __restrict__ y, T* __restrict__ dx, long total, int c) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  T* bg = (T*)smem_raw;
+  T* by = bg + kStagePix * c;
+  for (long p0 = (long)blockIdx.x * kStagePix; p0 < total; p0 += (long)gridDim.x * kStagePix) {
+    const int np = (int)min<long>(kStagePix, total - p0);
+    __syncthreads();
+    stage_in(dy + p0 * c, bg, np * c);
+    stage_in(y + p0 * c, by, np * c);
+    __syncthreads();
+    if ((int)threadIdx.x < np) {
+      T* g = bg + threadIdx.x * c;
+      const T* yy = by + threadIdx.x * c;
+      float dot = 0.f;
+      for (int k = 0; k < c; ++k) dot = fmaf(to_f(g[k]), to_f(yy[k]), dot);
+      for (int k = 0; k < c; ++k) g[k] = from_f<T>(to_f(yy[k]) * (to_f(g[k]) - dot));
+    }
+    __syncthreads();
+    stage_out(dx + p0 * c, bg, np * c);
+  }
+}
+
 // ------------------------------------------------------------------ channel softmax (dim=1)
 // train.py:225,245,256.  One thread per pixel; logits addressed by (sn, sc, shw) strides so
 // NHWC and NCHW tensors both work.  Output NHWC contiguous with row pitch yld (zero-padded
@@ -504,13 +678,25 @@ __global__ void softmax_bwd_kernel(const O* __restrict__ dy, const O* __restrict
 extern "C" int rtsds_softmax_fwd(const void* x, long sn, long sc, long shw, void* y, int y_ld, int n, long hw, int c, int dtype,
                                  void* stream) {
   if (n <= 0 || hw <= 0 || c <= 0 || y_ld < c) return RTSDS_ERR_SHAPE;
-  DISPATCH_T(dtype, hipLaunchKernelGGL((softmax_fwd_kernel<T, T>), dim3(ew_blocks((long)n * hw)), dim3(256), 0, (hipStream_t)stream, (const T*)x, (T*)y, n, hw, c, sn, sc, shw, y_ld));
+  DISPATCH_T(dtype, {
+    if (y_ld == c && stage_ok(sn, sc, shw, hw, c))
+      hipLaunchKernelGGL(softmax_fwd_staged<T>, dim3(ew_blocks((long)n * hw, kStagePix, 4096)), dim3(256), kStagePix * c * sizeof(T),
+                         (hipStream_t)stream, (const T*)x, (T*)y, (long)n * hw, c);
+    else
+      hipLaunchKernelGGL((softmax_fwd_kernel<T, T>), dim3(ew_blocks((long)n * hw)), dim3(256), 0, (hipStream_t)stream, (const T*)x, (T*)y, n, hw, c, sn, sc, shw, y_ld);
+  });
   RET_LAUNCH();
 }
 extern "C" int rtsds_softmax_bwd(const void* dy, const void* y, int ld, void* dx, long sn, long sc, long shw, int n, long hw, int c,
                                  int dtype, void* stream) {
   if (n <= 0 || hw <= 0 || c <= 0 || ld < c) return RTSDS_ERR_SHAPE;
-  DISPATCH_T(dtype, hipLaunchKernelGGL((softmax_bwd_kernel<T, T>), dim3(ew_blocks((long)n * hw)), dim3(256), 0, (hipStream_t)stream, (const T*)dy, (const T*)y, (T*)dx, n, hw, c, ld, sn, sc, shw));
+  DISPATCH_T(dtype, {
+    if (ld == c && stage_ok(sn, sc, shw, hw, c))
+      hipLaunchKernelGGL(softmax_bwd_staged<T>, dim3(ew_blocks((long)n * hw, kStagePix, 4096)), dim3(256), 2 * kStagePix * c * sizeof(T),
+                         (hipStream_t)stream, (const T*)dy, (const T*)y, (T*)dx, (long)n * hw, c);
+    else
+      hipLaunchKernelGGL((softmax_bwd_kernel<T, T>), dim3(ew_blocks((long)n * hw)), dim3(256), 0, (hipStream_t)stream, (const T*)dy, (const T*)y, (T*)dx, n, hw, c, ld, sn, sc, shw);
+  });
   RET_LAUNCH();
 }
 
@@ -588,14 +774,86 @@ __global__ void ce_bwd_kernel(const T* __restrict__ x, const int64_t* __restrict
     }
   }
 }
+
+template <typename T>
+__global__ void __launch_bounds__(256) ce_fwd_part_staged(const T* __restrict__ x, const int64_t* __restrict__ tgt, float* __restrict__ part,
+                                                          long total, int c, int ignore) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  T* buf = (T*)smem_raw;
+  __shared__ float rs[4], rc[4];
+  float ls = 0.f, lc = 0.f;
+  for (long p0 = (long)blockIdx.x * kStagePix; p0 < total; p0 += (long)gridDim.x * kStagePix) {
+    const int np = (int)min<long>(kStagePix, total - p0);
+    __syncthreads();
+    stage_in(x + p0 * c, buf, np * c);
+    __syncthreads();
+    if ((int)threadIdx.x < np) {
+      const long t = tgt[p0 + threadIdx.x];
+      if (t != ignore) {
+        const T* r = buf + threadIdx.x * c;
+        float m = -INFINITY;
+        for (int k = 0; k < c; ++k) m = fmaxf(m, to_f(r[k]));
+        float z = 0.f;
+        for (int k = 0; k < c; ++k) z += expf(to_f(r[k]) - m);
+        const float xt = (t >= 0 && t < c) ? to_f(r[t]) : NAN;
+        ls += logf(z) + m - xt;
+        lc += 1.f;
+      }
+    }
+  }
+  ls = wave_sum(ls);
+  lc = wave_sum(lc);
+  if ((threadIdx.x & 63) == 0) { rs[threadIdx.x >> 6] = ls; rc[threadIdx.x >> 6] = lc; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    part[blockIdx.x] = rs[0] + rs[1] + rs[2] + rs[3];
+    part[kCeRB + blockIdx.x] = rc[0] + rc[1] + rc[2] + rc[3];
+  }
+}
+template <typename T>
+__global__ void __launch_bounds__(256) ce_bwd_staged(const T* __restrict__ x, const int64_t* __restrict__ tgt, const float* __restrict__ gout,
+                                                     const float* __restrict__ count, T* __restrict__ dx, long total, int c, int ignore) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  T* buf = (T*)smem_raw;
+  const float g = gout[0] / count[0];
+  for (long p0 = (long)blockIdx.x * kStagePix; p0 < total; p0 += (long)gridDim.x * kStagePix) {
+    const int np = (int)min<long>(kStagePix, total - p0);
+    __syncthreads();
+    stage_in(x + p0 * c, buf, np * c);
+    __syncthreads();
+    if ((int)threadIdx.x < np) {
+      const long t = tgt[p0 + threadIdx.x];
+      T* r = buf + threadIdx.x * c;
+      if (t == ignore) {
+        for (int k = 0; k < c; ++k) r[k] = from_f<T>(0.f);
+      } else {
+        float m = -INFINITY;
+        for (int k = 0; k < c; ++k) m = fmaxf(m, to_f(r[k]));
+        float z = 0.f;
+        for (int k = 0; k < c; ++k) z += expf(to_f(r[k]) - m);
+        const float gz = g / z;
+        for (int k = 0; k < c; ++k) r[k] = from_f<T>(gz * expf(to_f(r[k]) - m) - (k == t ? g : 0.f));
+      }
+    }
+    __syncthreads();
+    stage_out(dx + p0 * c, buf, np * c);
+  }
+}
+
 extern "C" size_t rtsds_ce_workspace(void) { return (2 * kCeRB + 64) * sizeof(float); }
 extern "C" int rtsds_ce_fwd(const void* x, long sn, long sc, long shw, const int64_t* tgt, float* loss, int n, long hw, int c,
                             int ignore_index, int dtype, void* ws, size_t ws_bytes, void* stream) {
   if (n <= 0 || hw <= 0 || c <= 0) return RTSDS_ERR_SHAPE;
   if (ws_bytes < rtsds_ce_workspace()) return RTSDS_ERR_WORKSPACE;
   hipStream_t st = (hipStream_t)stream;
-  const int nb = std::min<int>(kCeRB, ew_blocks((long)n * hw, 256, kCeRB));
-  DISPATCH_T(dtype, hipLaunchKernelGGL(ce_fwd_part_kernel<T>, dim3(nb), dim3(256), 0, st, (const T*)x, tgt, (float*)ws, n, hw, c, sn, sc, shw, ignore_index));
+  const int nb = std::min<int>(kCeRB, ew_blocks((long)n * hw, kStagePix, kCeRB));
+  DISPATCH_T(dtype, {
+    if (stage_ok(sn, sc, shw, hw, c))
+      hipLaunchKernelGGL(ce_fwd_part_staged<T>, dim3(nb), dim3(256), kStagePix * c * sizeof(T), st, (const T*)x, tgt, (float*)ws,
+                         (long)n * hw, c, ignore_index);
+    else
+      hipLaunchKernelGGL(ce_fwd_part_kernel<T>, dim3(nb), dim3(256), 0, st, (const T*)x, tgt, (float*)ws, n, hw, c, sn, sc, shw, ignore_index);
+  });
   hipLaunchKernelGGL(ce_fwd_final_kernel, dim3(1), dim3(256), 0, st, (float*)ws, nb, loss);
   RET_LAUNCH();
 }
@@ -603,7 +861,13 @@ extern "C" int rtsds_ce_fwd(const void* x, long sn, long sc, long shw, const int
 extern "C" int rtsds_ce_bwd(const void* x, long sn, long sc, long shw, const int64_t* tgt, const float* grad_loss, const float* count,
                             void* dx, int n, long hw, int c, int ignore_index, int dtype, void* stream) {
   if (n <= 0 || hw <= 0 || c <= 0) return RTSDS_ERR_SHAPE;
-  DISPATCH_T(dtype, hipLaunchKernelGGL(ce_bwd_kernel<T>, dim3(ew_blocks((long)n * hw)), dim3(256), 0, (hipStream_t)stream, (const T*)x, tgt, grad_loss, count, (T*)dx, n, hw, c, sn, sc, shw, ignore_index));
+  DISPATCH_T(dtype, {
+    if (stage_ok(sn, sc, shw, hw, c))
+      hipLaunchKernelGGL(ce_bwd_staged<T>, dim3(ew_blocks((long)n * hw, kStagePix, 4096)), dim3(256), kStagePix * c * sizeof(T),
+                         (hipStream_t)stream, (const T*)x, tgt, grad_loss, count, (T*)dx, (long)n * hw, c, ignore_index);
+    else
+      hipLaunchKernelGGL(ce_bwd_kernel<T>, dim3(ew_blocks((long)n * hw)), dim3(256), 0, (hipStream_t)stream, (const T*)x, tgt, grad_loss, count, (T*)dx, n, hw, c, sn, sc, shw, ignore_index);
+  });
   RET_LAUNCH();
 }
 
@@ -698,10 +962,47 @@ __global__ void argmax_kernel(const T* __restrict__ x, int64_t* __restrict__ out
     if ((threadIdx.x & 63) == 0 && cnt) atomicAdd(correct, cnt);
   }
 }
+
+template <typename T>
+__global__ void __launch_bounds__(256) argmax_staged(const T* __restrict__ x, int64_t* __restrict__ out, const int64_t* __restrict__ tgt,
+                                                     unsigned long long* __restrict__ correct, long total, int c) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  T* buf = (T*)smem_raw;
+  unsigned long long cnt = 0;
+  for (long p0 = (long)blockIdx.x * kStagePix; p0 < total; p0 += (long)gridDim.x * kStagePix) {
+    const int np = (int)min<long>(kStagePix, total - p0);
+    __syncthreads();
+    stage_in(x + p0 * c, buf, np * c);
+    __syncthreads();
+    if ((int)threadIdx.x < np) {
+      const T* r = buf + threadIdx.x * c;
+      float best = to_f(r[0]);
+      int bi = 0;
+      for (int k = 1; k < c; ++k) {
+        const float v = to_f(r[k]);
+        if (v > best || (v != v && best == best)) { best = v; bi = k; }
+      }
+      const long p = p0 + threadIdx.x;
+      if (out) out[p] = bi;
+      if (tgt && tgt[p] == bi) ++cnt;
+    }
+  }
+  if (correct) {
+    for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
+    if ((threadIdx.x & 63) == 0 && cnt) atomicAdd(correct, cnt);
+  }
+}
+
 extern "C" int rtsds_argmax(const void* x, long sn, long sc, long shw, int64_t* out, const int64_t* target, unsigned long long* correct,
                             int n, long hw, int c, int dtype, void* stream) {
   if (n <= 0 || hw <= 0 || c <= 0) return RTSDS_ERR_SHAPE;
-  DISPATCH_T(dtype, hipLaunchKernelGGL(argmax_kernel<T>, dim3(ew_blocks((long)n * hw, 256, 4096)), dim3(256), 0, (hipStream_t)stream, (const T*)x, out, target, correct, n, hw, c, sn, sc, shw));
+  DISPATCH_T(dtype, {
+    if (stage_ok(sn, sc, shw, hw, c))
+      hipLaunchKernelGGL(argmax_staged<T>, dim3(ew_blocks((long)n * hw, kStagePix, 4096)), dim3(256), kStagePix * c * sizeof(T),
+                         (hipStream_t)stream, (const T*)x, out, target, correct, (long)n * hw, c);
+    else
+      hipLaunchKernelGGL(argmax_kernel<T>, dim3(ew_blocks((long)n * hw, 256, 4096)), dim3(256), 0, (hipStream_t)stream, (const T*)x, out, target, correct, n, hw, c, sn, sc, shw);
+  });
   RET_LAUNCH();
 }
 

@@ -26,8 +26,8 @@ def _conv_flops(d):
 
 
 class _Timed:
-    def __init__(self, d):
-        self.d = d
+    def __init__(self, d, tag="fwd"):
+        self.d, self.tag = d, tag
 
     def __enter__(self):
         if CONV_PROFILE is not None:
@@ -39,7 +39,33 @@ class _Timed:
     def __exit__(self, *exc):
         if CONV_PROFILE is not None:
             self.e1.record()
-            CONV_PROFILE.append((self.e0, self.e1, _conv_flops(self.d)))
+            CONV_PROFILE.append((self.e0, self.e1, _conv_flops(self.d), self.tag, self.d))
+
+
+# ----------------------------------------------------------------------------- grad sinks
+def _sink(p):
+    """The flat-arena gradient view of parameter ``p`` if an rtsds optimizer owns it.
+    Backward kernels then accumulate straight into it (accumulate flag) and the Function
+    returns None for ``p``, so autograd's per-parameter AccumulateGrad add never runs."""
+    ref = getattr(p, "_rt_arena", None) if p is not None else None
+    if ref is None:
+        return None
+    arena, i = ref
+    return arena.sink(i)
+
+
+def _sinks(*params):
+    """All-or-nothing: the sinks of every given (non-None) parameter, or None."""
+    out = []
+    for p in params:
+        if p is None:
+            out.append(None)
+            continue
+        s = _sink(p)
+        if s is None:
+            return None
+        out.append(s)
+    return out
 
 
 # ----------------------------------------------------------------------------- conv
@@ -65,9 +91,12 @@ class ConvFn(torch.autograd.Function):
         k, _, kh, kw = weight.shape
         d = _conv_desc(x, k, kh, kw, stride, padding, dilation)
         y = empty_nhwc(d.n, k, d.ho, d.wo, x.dtype, x.device)
-        with _Timed(d):
-            lib.rtsds_conv2d_fwd(ctypes.byref(d), _P(x), _P(wq), _P(bias), _P(y), act, stream())
+        ws = workspace(lib.rtsds_conv2d_fwd_workspace(ctypes.byref(d)), x.device)
+        with _Timed(d, "fwd"):
+            lib.rtsds_conv2d_fwd(ctypes.byref(d), _P(x), _P(wq), _P(bias), _P(y), act, _P(ws), ws.numel(),
+                                 stream())
         ctx.d, ctx.act, ctx.has_bias = d, act, bias is not None
+        ctx.params = (weight, bias)
         ctx.save_for_backward(x, wq, y if act else None)
         return y
 
@@ -87,19 +116,28 @@ class ConvFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = empty_nhwc(d.n, d.c, d.h, d.w, x.dtype, x.device)
             ws = workspace(lib.rtsds_conv2d_dgrad_workspace(ctypes.byref(d)), x.device)
-            with _Timed(d):
+            with _Timed(d, "dgrad"):
                 lib.rtsds_conv2d_dgrad(ctypes.byref(d), _P(g), _P(wq), _P(dx), 0, _P(ws), ws.numel(),
                                        stream())
         if ctx.needs_input_grad[1] or ctx.needs_input_grad[2]:
-            dw = torch.empty((d.k, d.c, d.kh, d.kw), dtype=torch.float32, device=x.device,
-                             memory_format=CL)
-            db = torch.empty(d.k, dtype=torch.float32, device=x.device) if ctx.has_bias else None
+            weight, bias = ctx.params
+            sinks = _sinks(weight, bias if ctx.needs_input_grad[2] else None) if ctx.needs_input_grad[1] else None
             ws = workspace(lib.rtsds_conv2d_wgrad_workspace(ctypes.byref(d)), x.device)
-            with _Timed(d):
-                lib.rtsds_conv2d_wgrad(ctypes.byref(d), _P(x), _P(g), _P(dw), _P(db), _P(ws),
-                                       ws.numel(), stream())
-            if not ctx.needs_input_grad[1]:
+            if sinks is not None:
+                with _Timed(d, "wgrad"):
+                    lib.rtsds_conv2d_wgrad(ctypes.byref(d), _P(x), _P(g), _P(sinks[0]), _P(sinks[1]), 1,
+                                           _P(ws), ws.numel(), stream())
                 dw = None
+                db = None
+            else:
+                dw = torch.empty((d.k, d.c, d.kh, d.kw), dtype=torch.float32, device=x.device,
+                                 memory_format=CL)
+                db = torch.empty(d.k, dtype=torch.float32, device=x.device) if ctx.has_bias else None
+                with _Timed(d, "wgrad"):
+                    lib.rtsds_conv2d_wgrad(ctypes.byref(d), _P(x), _P(g), _P(dw), _P(db), 0, _P(ws),
+                                           ws.numel(), stream())
+                if not ctx.needs_input_grad[1]:
+                    dw = None
         return dx, dw, db, None, None, None, None, None
 
 
@@ -125,11 +163,13 @@ class ConvSumFn(torch.autograd.Function):
             d = _conv_desc(x, k, kh, kw, stride, padding, dilation)
             if y is None:
                 y = empty_nhwc(d.n, k, d.ho, d.wo, x.dtype, x.device)
-            with _Timed(d):
+            ws = workspace(lib.rtsds_conv2d_fwd_workspace(ctypes.byref(d)), x.device)
+            with _Timed(d, "fwd"):
                 lib.rtsds_conv2d_fwd(ctypes.byref(d), _P(x), _P(wqs[i]), _P(biases[i]), _P(y),
-                                     0x100 if i else 0, stream())
+                                     0x100 if i else 0, _P(ws), ws.numel(), stream())
             descs.append(d)
         ctx.descs = descs
+        ctx.params = tuple(weights) + tuple(biases)
         ctx.has_bias = [b is not None for b in biases]
         ctx.save_for_backward(x, *wqs)
         return y
@@ -146,16 +186,24 @@ class ConvSumFn(torch.autograd.Function):
                 if dx is None:
                     dx = empty_nhwc(d.n, d.c, d.h, d.w, x.dtype, x.device)
                 ws = workspace(lib.rtsds_conv2d_dgrad_workspace(ctypes.byref(d)), x.device)
-                with _Timed(d):
+                with _Timed(d, "dgrad"):
                     lib.rtsds_conv2d_dgrad(ctypes.byref(d), _P(dy), _P(wqs[i]), _P(dx), 1 if i else 0,
                                            _P(ws), ws.numel(), stream())
             if ctx.needs_input_grad[2 + i] or ctx.needs_input_grad[2 + m + i]:
+                w_i, b_i = ctx.params[i], ctx.params[m + i]
+                sinks = (_sinks(w_i, b_i if ctx.needs_input_grad[2 + m + i] else None)
+                         if ctx.needs_input_grad[2 + i] else None)
+                ws = workspace(lib.rtsds_conv2d_wgrad_workspace(ctypes.byref(d)), x.device)
+                if sinks is not None:
+                    with _Timed(d, "wgrad"):
+                        lib.rtsds_conv2d_wgrad(ctypes.byref(d), _P(x), _P(dy), _P(sinks[0]), _P(sinks[1]),
+                                               1, _P(ws), ws.numel(), stream())
+                    continue
                 dw = torch.empty((d.k, d.c, d.kh, d.kw), dtype=torch.float32, device=x.device,
                                  memory_format=CL)
                 db = torch.empty(d.k, dtype=torch.float32, device=x.device) if ctx.has_bias[i] else None
-                ws = workspace(lib.rtsds_conv2d_wgrad_workspace(ctypes.byref(d)), x.device)
-                with _Timed(d):
-                    lib.rtsds_conv2d_wgrad(ctypes.byref(d), _P(x), _P(dy), _P(dw), _P(db), _P(ws),
+                with _Timed(d, "wgrad"):
+                    lib.rtsds_conv2d_wgrad(ctypes.byref(d), _P(x), _P(dy), _P(dw), _P(db), 0, _P(ws),
                                            ws.numel(), stream())
                 dws[i] = dw if ctx.needs_input_grad[2 + i] else None
                 dbs[i] = db
@@ -182,6 +230,7 @@ class BatchNormFn(torch.autograd.Function):
                          _P(running_var), _P(sm), _P(si), float(momentum), float(eps), int(training),
                          act, dcode(x), _P(ws), ws.numel(), stream())
         ctx.meta = (rows, c, int(training), act, res is not None)
+        ctx.gamma, ctx.beta = gamma, beta
         ctx.save_for_backward(x, y, gamma, sm, si)
         return y
 
@@ -194,12 +243,19 @@ class BatchNormFn(torch.autograd.Function):
                                            ctx.needs_input_grad[2], ctx.needs_input_grad[3])
         dx = torch.empty_like(x, memory_format=CL) if need_dx else None
         dres = torch.empty_like(x, memory_format=CL) if (has_res and need_r) else None
-        dg = torch.empty(c, dtype=torch.float32, device=x.device) if need_g else None
-        db = torch.empty(c, dtype=torch.float32, device=x.device) if need_b else None
+        sinks = _sinks(ctx.gamma if need_g else None, ctx.beta if need_b else None) if (need_g or need_b) else None
+        if sinks is not None:
+            dg, db, acc = sinks[0], sinks[1], 1
+        else:
+            dg = torch.empty(c, dtype=torch.float32, device=x.device) if need_g else None
+            db = torch.empty(c, dtype=torch.float32, device=x.device) if need_b else None
+            acc = 0
         ws = workspace(lib.rtsds_bn_workspace(rows, c), x.device)
         lib.rtsds_bn_bwd(_P(dy), _P(x), _P(y), _P(dx), _P(dres), _P(dg), _P(db), rows, c,
-                         _P(gamma), _P(sm), _P(si), training, act, dcode(x), _P(ws), ws.numel(),
+                         _P(gamma), _P(sm), _P(si), training, act, acc, dcode(x), _P(ws), ws.numel(),
                          stream())
+        if acc:
+            dg = db = None
         return dx, dg, db, dres, None, None, None, None, None, None
 
 

@@ -23,6 +23,20 @@ from ._lib import lib
 from .runtime import stream
 
 
+def allreduce_flat(buffers):
+    """Sum flat gradient buffers over the data-parallel group (RCCL over xGMI for HIP
+    tensors, gloo for CPU tests) -- one collective per buffer, replacing DataParallel's
+    per-module reduce (utils.py:104-105).  Returns the 1/world scale the caller applies
+    (folded into the Adam kernel), 1.0 when not distributed."""
+    if not (dist.is_available() and dist.is_initialized()):
+        return 1.0
+    world = dist.get_world_size()
+    if world > 1:
+        for b in buffers:
+            dist.all_reduce(b)
+    return 1.0 / world
+
+
 class _Arena:
     def __init__(self, params):
         dev = params[0].device
@@ -57,6 +71,7 @@ class _Arena:
             if p.dim() == 4:
                 p._rt_shadow = self.shadow[off:off + n].as_strided(p.shape, p.stride())
                 p._rt_shadow_key = (p.data_ptr(), p._version)
+            p._rt_arena = (self, i)
             if p.requires_grad:
                 p.register_post_accumulate_grad_hook(self._hook(i))
 
@@ -64,6 +79,14 @@ class _Arena:
         def mark(_p):
             self.touched[i] = True
         return mark
+
+    def sink(self, i):
+        """Gradient view a backward kernel may accumulate into directly (marks the parameter
+        as having received a gradient this step); None if .grad left the arena."""
+        if not self.grad_ptr_ok(i):
+            return None
+        self.touched[i] = True
+        return self.params[i].grad
 
     def grad_ptr_ok(self, i):
         p = self.params[i]
@@ -110,7 +133,6 @@ class Adam(torch.optim.Optimizer):
     def step(self, closure=None):
         loss = closure() if closure is not None else None
         arenas = self._ensure()
-        world = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
         for a in arenas:
             for i in range(len(a.params)):
                 if a.touched[i] and not a.grad_ptr_ok(i):
@@ -118,8 +140,7 @@ class Adam(torch.optim.Optimizer):
                         warnings.warn("rtsds_amd.Adam: gradient left the arena; copying back")
                         self._warned = True
                     a.rebind_grad(i)
-            if world > 1:
-                dist.all_reduce(a.gflat)
+        gscale = allreduce_flat([a.gflat for a in arenas])
         for g, a in zip(self.param_groups, arenas):
             b1, b2 = g["betas"]
             # contiguous runs of touched parameters with equal step counts -> one launch each
@@ -138,7 +159,7 @@ class Adam(torch.optim.Optimizer):
                                     a.m.data_ptr() + 4 * lo, a.v.data_ptr() + 4 * lo,
                                     a.shadow.data_ptr() + 2 * lo, hi - lo, float(g["lr"]), float(b1),
                                     float(b2), float(g["eps"]), float(g["weight_decay"]), step,
-                                    1.0 / world, stream())
+                                    gscale, stream())
                 for k in range(i, j + 1):
                     a.steps[k] = step
                 i = j + 1

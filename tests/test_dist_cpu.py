@@ -1,0 +1,56 @@
+"""Data-parallel plumbing on CPU (gloo, world size 2): environment-driven init and the flat
+gradient all-reduce + 1/world scaling the fused Adam applies (rtsds_amd/optim.py)."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from rtsds_amd.optim import allreduce_flat
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    from rtsds_amd.utils import init_distributed
+    r, local, w = init_distributed("gloo")
+    assert (r, w) == (rank, world)
+    g = torch.arange(10, dtype=torch.float32) * (rank + 1)
+    scale = allreduce_flat([g])
+    q.put((rank, g.tolist(), scale))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2])
+def test_gloo_flat_allreduce(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    want = [float(i * sum(r + 1 for r in range(world))) for i in range(10)]
+    for rank, vals, scale in res:
+        assert vals == want
+        assert scale == pytest.approx(1.0 / world)
+
+
+def test_single_process_is_identity():
+    g = torch.ones(4)
+    assert allreduce_flat([g]) == 1.0
+    assert g.tolist() == [1.0] * 4
