@@ -52,10 +52,14 @@ typedef struct {
  * Implicit GEMM on MFMA (bf16: v_mfma_f32_16x16x32_bf16, f32: v_mfma_f32_16x16x4_f32).  */
 
 /* y = act(conv(x, w) + bias [+ y if act & RTSDS_ACCUMULATE]).  bias may be NULL (fp32 [k]).
+ * bn_stats (may be NULL; act must be NONE): receives the following BatchNorm's per-tile
+ * partial statistics, fp32 [rtsds_conv2d_fwd_stats_tiles(d)][k][count, mean, M2], consumed
+ * by rtsds_bn_fwd(stats_part=...) -- the statistics pass over y is then skipped.
  * ws >= rtsds_conv2d_fwd_workspace(d) (non-zero only when Cin needs channel padding).   */
 size_t rtsds_conv2d_fwd_workspace(const rtsds_conv_desc* d);
+int rtsds_conv2d_fwd_stats_tiles(const rtsds_conv_desc* d);
 int rtsds_conv2d_fwd(const rtsds_conv_desc* d, const void* x, const void* w, const float* bias,
-                     void* y, int act, void* ws, size_t ws_bytes, void* stream);
+                     void* y, int act, float* bn_stats, void* ws, size_t ws_bytes, void* stream);
 /* dx (+)= conv_transpose(dy, w) (accumulate != 0: dx += ...).  Needs ws >=
  * rtsds_conv2d_dgrad_workspace(d).  Strides 1 and 2 only.                               */
 size_t rtsds_conv2d_dgrad_workspace(const rtsds_conv_desc* d);
@@ -77,10 +81,13 @@ int rtsds_conv2d_wgrad(const rtsds_conv_desc* d, const void* x, const void* dy, 
  * (PyTorch semantics).  Forward (eval): running stats are used, save_* untouched.
  * y = act(gamma * (x - mean) * invstd + beta [+ res]).  gamma/beta may be NULL (1 / 0).   */
 size_t rtsds_bn_workspace(long rows, int c);
+/* stats_part (may be NULL): [stats_nrb][c][count, mean, M2] partials from the producing
+ * conv (rtsds_conv2d_fwd bn_stats) -- training mode then skips its own statistics pass.   */
 int rtsds_bn_fwd(const void* x, const void* res, void* y, long rows, int c, const float* gamma,
                  const float* beta, float* running_mean, float* running_var, float* save_mean,
-                 float* save_invstd, float momentum, float eps, int training, int act, int dtype,
-                 void* ws, size_t ws_bytes, void* stream);
+                 float* save_invstd, float momentum, float eps, int training, int act,
+                 const float* stats_part, int stats_nrb, int dtype, void* ws, size_t ws_bytes,
+                 void* stream);
 /* Backward of the fused BN(+res)(+act) above, given y (post-activation output) for the
  * activation mask.  dx, dres (may be NULL), dgamma/dbeta (fp32, may be NULL; overwritten, or
  * added to when accumulate_params != 0).  training=0: eval-mode backward (constant stats). */

@@ -319,10 +319,15 @@ extern "C" size_t rtsds_bn_workspace(long rows, int c) {
 template <typename T, int VEC>
 static void bn_fwd_launch(const void* x, const void* res, void* y, long rows, int c, const float* gamma, const float* beta,
                           float* rm, float* rv, float* sm, float* si, float mom, float eps, int training, int act,
-                          float* part, float* scale, float* shift, hipStream_t st) {
+                          const float* pre, int pre_nrb, float* part, float* scale, float* shift, hipStream_t st) {
   if (training) {
-    const int rb = bn_rb(rows, c, VEC);
-    hipLaunchKernelGGL((bn_stats_kernel<T, VEC>), dim3(rb, rt_cdiv(c, 256 * VEC)), dim3(256), 0, st, (const T*)x, part, rows, c);
+    int rb = pre_nrb;
+    if (pre) {
+      part = (float*)pre;  // statistics already produced by the conv epilogue
+    } else {
+      rb = bn_rb(rows, c, VEC);
+      hipLaunchKernelGGL((bn_stats_kernel<T, VEC>), dim3(rb, rt_cdiv(c, 256 * VEC)), dim3(256), 0, st, (const T*)x, part, rows, c);
+    }
     hipLaunchKernelGGL(bn_finalize_kernel, dim3(c), dim3(64), 0, st, part, rb, c, rows, gamma, beta, rm, rv,
                        sm, si, scale, shift, mom, eps);
   } else {
@@ -336,7 +341,8 @@ static void bn_fwd_launch(const void* x, const void* res, void* y, long rows, in
 
 extern "C" int rtsds_bn_fwd(const void* x, const void* res, void* y, long rows, int c, const float* gamma, const float* beta,
                             float* running_mean, float* running_var, float* save_mean, float* save_invstd, float momentum,
-                            float eps, int training, int act, int dtype, void* ws, size_t ws_bytes, void* stream) {
+                            float eps, int training, int act, const float* stats_part, int stats_nrb, int dtype, void* ws,
+                            size_t ws_bytes, void* stream) {
   if (rows <= 0 || c <= 0) return RTSDS_ERR_SHAPE;
   if (ws_bytes < rtsds_bn_workspace(rows, c)) return RTSDS_ERR_WORKSPACE;
   if (!training && (!running_mean || !running_var)) return RTSDS_ERR_UNSUPPORTED;
@@ -347,11 +353,11 @@ extern "C" int rtsds_bn_fwd(const void* x, const void* res, void* y, long rows, 
   float* scale = part + (size_t)kBnMaxRB * c * 3;
   float* shift = scale + c;
   if (dtype == RTSDS_BF16) {
-    if (c % 8 == 0) bn_fwd_launch<bf16, 8>(x, res, y, rows, c, gamma, beta, running_mean, running_var, save_mean, save_invstd, momentum, eps, training, act, part, scale, shift, st);
-    else bn_fwd_launch<bf16, 1>(x, res, y, rows, c, gamma, beta, running_mean, running_var, save_mean, save_invstd, momentum, eps, training, act, part, scale, shift, st);
+    if (c % 8 == 0) bn_fwd_launch<bf16, 8>(x, res, y, rows, c, gamma, beta, running_mean, running_var, save_mean, save_invstd, momentum, eps, training, act, stats_part, stats_nrb, part, scale, shift, st);
+    else bn_fwd_launch<bf16, 1>(x, res, y, rows, c, gamma, beta, running_mean, running_var, save_mean, save_invstd, momentum, eps, training, act, stats_part, stats_nrb, part, scale, shift, st);
   } else if (dtype == RTSDS_F32) {
-    if (c % 4 == 0) bn_fwd_launch<float, 4>(x, res, y, rows, c, gamma, beta, running_mean, running_var, save_mean, save_invstd, momentum, eps, training, act, part, scale, shift, st);
-    else bn_fwd_launch<float, 1>(x, res, y, rows, c, gamma, beta, running_mean, running_var, save_mean, save_invstd, momentum, eps, training, act, part, scale, shift, st);
+    if (c % 4 == 0) bn_fwd_launch<float, 4>(x, res, y, rows, c, gamma, beta, running_mean, running_var, save_mean, save_invstd, momentum, eps, training, act, stats_part, stats_nrb, part, scale, shift, st);
+    else bn_fwd_launch<float, 1>(x, res, y, rows, c, gamma, beta, running_mean, running_var, save_mean, save_invstd, momentum, eps, training, act, stats_part, stats_nrb, part, scale, shift, st);
   } else return RTSDS_ERR_UNSUPPORTED;
   return hipGetLastError() == hipSuccess ? RTSDS_OK : RTSDS_ERR_LAUNCH;
 }

@@ -27,8 +27,14 @@ struct ConvArgs {
   int n, h, w, c, ho, wo, k, kh, kw, sh, sw, ph, pw, dh, dw;
   FastDiv f_howo, f_wo, f_hw, f_w, f_c, f_k, f_kw;
   int tiles_per_split;
+  // DGRAD stride-phase decomposition (normal mode: tkw=kw, r0=0, rstep=1, psh=1, off=0,
+  // hp=h, wp=w): output rows enumerate the pixels ih = th*psh + offh of one parity phase,
+  // and the reduction runs over that phase's taps r = r0 + rr*rstep only.
+  int tkw, r0h, r0w, rstep, psh, offh, offw, hp, wp;
+  FastDiv f_tkw;
   int act;
   int accum;          // FWD/DGRAD: y += result
+  float* stats;       // FWD: per-M-tile BatchNorm partials [mtile][N][count, mean, M2] (or null)
   long split_stride;  // elements between WGRAD split slabs
 };
 
@@ -109,13 +115,25 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(const ConvArgs P) {
   constexpr int KS = Mma<T>::KS;
   static_assert(WM * WN == 4, "4 waves");
   static_assert(BK % KS == 0, "BK");
-  static_assert(!RC || BK == (sizeof(T) == 2 ? 32 : 16), "RC BK");
+  static_assert(!RC || BK % (sizeof(T) == 2 ? 32 : 16) == 0, "RC BK");
 
   __shared__ __attribute__((aligned(16))) T smem[2 * (A_EL + B_EL)];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm0 = (wave / WN) * WTM, wn0 = (wave % WN) * WTN;
-  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  // XCD-aware remap (cdna_hip_programming.md T1, bijective form): workgroups b and b+8 run on
+  // one XCD, so give each XCD a contiguous run of tiles -- M-adjacent tiles share input halo
+  // rows and the same weight tile in that XCD's L2.
+  int mt, nt;
+  {
+    const int gx = gridDim.x, nwg = gx * gridDim.y;
+    const int bid = blockIdx.y * gx + blockIdx.x;
+    const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+    const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+    mt = wg % gx;
+    nt = wg / gx;
+  }
+  const int m0 = mt * BM, n0 = nt * BN;
   const T* __restrict__ ga = (const T*)P.a;
   const T* __restrict__ gb = (const T*)P.b;
 
@@ -147,8 +165,9 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(const ConvArgs P) {
         a_h[i] = oh * P.sh - P.ph;
         a_w[i] = ow * P.sw - P.pw;
       } else {
-        const int img = fdiv(mm, P.f_hw), rem = mm - img * P.h * P.w;
-        const int ih = fdiv(rem, P.f_w), iw = rem - ih * P.w;
+        const int img = fdiv(mm, P.f_hw), rem = mm - img * P.hp * P.wp;
+        const int th = fdiv(rem, P.f_w), tw = rem - th * P.wp;
+        const int ih = th * P.psh + P.offh, iw = tw * P.psh + P.offw;
         a_off[i] = (long)img * P.ho * P.wo * P.k;
         a_h[i] = ih + P.ph;
         a_w[i] = iw + P.pw;
@@ -178,8 +197,14 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(const ConvArgs P) {
       if (ALA == 2) {
         tap_u = k0 / Cr;
         ci_u = k0 - tap_u * Cr;
-        r_u = tap_u / P.kw;
-        s_u = tap_u - r_u * P.kw;
+        if (MODE == MODE_FWD) {
+          r_u = tap_u / P.kw;
+          s_u = tap_u - r_u * P.kw;
+        } else {
+          const int rr = tap_u / P.tkw;
+          r_u = P.r0h + rr * P.rstep;
+          s_u = P.r0w + (tap_u - rr * P.tkw) * P.rstep;
+        }
       }
 #pragma unroll
       for (int i = 0; i < NA; ++i) {
@@ -196,8 +221,14 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(const ConvArgs P) {
             okk = kk < P.K;
             const int tap = fdiv(kk, MODE == MODE_FWD ? P.f_c : P.f_k);
             ci = kk - tap * Cr;
-            r = fdiv(tap, P.f_kw);
-            s = tap - r * P.kw;
+            if (MODE == MODE_FWD) {
+              r = fdiv(tap, P.f_kw);
+              s = tap - r * P.kw;
+            } else {
+              const int rr = fdiv(tap, P.f_tkw);
+              r = P.r0h + rr * P.rstep;
+              s = P.r0w + (tap - rr * P.tkw) * P.rstep;
+            }
           }
           int hh, ww;
           bool ok = a_ok[i] && okk;
@@ -421,28 +452,86 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(const ConvArgs P) {
         for (int e = 0; e < 4; ++e) {
           const int gm = m0 + wm0 + i * 16 + er + e;
           if (gm >= P.M) continue;
+          long orow = gm;
+          if (MODE == MODE_DGRAD && P.psh != 1) {
+            const int img = fdiv(gm, P.f_hw), rem = gm - img * P.hp * P.wp;
+            const int th = fdiv(rem, P.f_w), tw = rem - th * P.wp;
+            orow = ((long)img * P.h + th * P.psh + P.offh) * P.w + tw * P.psh + P.offw;
+          }
           float v = acc[i][j][e] + bv;
-          if (P.accum) v += to_f(out[(long)gm * P.N + gn]);
+          if (P.accum) v += to_f(out[orow * P.N + gn]);
           if (P.act == RTSDS_ACT_RELU) v = fmaxf(v, 0.f);
           else if (P.act == RTSDS_ACT_LEAKY) v = v > 0.f ? v : 0.2f * v;
           else if (P.act == RTSDS_ACT_SIGMOID) v = 1.f / (1.f + expf(-v));
-          out[(long)gm * P.N + gn] = from_f<T>(v);
+          out[orow * P.N + gn] = from_f<T>(v);
         }
+    }
+    if (MODE == MODE_FWD && P.stats != nullptr) {
+      // BatchNorm batch statistics fused into the producing conv: exact two-pass mean / M2 of
+      // this tile's rows per output channel, from the fp32 accumulators (merged across tiles
+      // with Chan's formula by bn_finalize_kernel).
+      __syncthreads();
+      float* red = (float*)smem;  // [WM][BN]
+      const int wmi = wave / WN;
+      const int nvalid = min(BM, P.M - m0);
+      float mean[FN];
+#pragma unroll
+      for (int pass = 0; pass < 2; ++pass) {
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          const int gn = n0 + wn0 + j * 16 + ec;
+          const float bv = (P.bias && gn < P.N) ? P.bias[gn] : 0.f;
+          float sacc = 0.f;
+#pragma unroll
+          for (int i = 0; i < FM; ++i)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const int gm = m0 + wm0 + i * 16 + er + e;
+              const float v = acc[i][j][e] + bv;
+              const float t = pass == 0 ? v : (v - mean[j]) * (v - mean[j]);
+              if (gm < P.M) sacc += t;
+            }
+          sacc += __shfl_xor(sacc, 16, 64);
+          sacc += __shfl_xor(sacc, 32, 64);
+          if (lane < 16) red[wmi * BN + wn0 + j * 16 + ec] = sacc;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          const int col = wn0 + j * 16 + ec;
+          float tot = 0.f;
+#pragma unroll
+          for (int w = 0; w < WM; ++w) tot += red[w * BN + col];
+          if (pass == 0) {
+            mean[j] = tot / (float)nvalid;
+          } else if (wmi == 0 && lane < 16 && n0 + col < P.N) {
+            float* o = P.stats + ((long)mt * P.N + n0 + col) * 3;
+            o[0] = (float)nvalid;
+            o[1] = mean[j];
+            o[2] = tot;
+          }
+        }
+        __syncthreads();
+      }
     }
   }
 }
 
 // ---- small helper kernels -------------------------------------------------------------
-// W[co][r][s][ci] -> Wt[ci][r][s][co_p] (DGRAD's B operand), zero for co >= co_n.
+// W[co][r][s][ci] -> Wt[ci][rr][ss][co_p] (DGRAD's B operand) over the taps
+// r = r0h + rr*rstep (rr < tkh), s = r0w + ss*rstep (ss < tkw); zero for co >= co_n.
 template <typename T>
-__global__ void repack_wt_kernel(const T* __restrict__ w, T* __restrict__ wt, int co_n, int co_p, int taps, int ci_n) {
+__global__ void repack_wt_kernel(const T* __restrict__ w, T* __restrict__ wt, int co_n, int co_p, int kh, int kw, int ci_n,
+                                 int tkh, int tkw, int r0h, int r0w, int rstep) {
+  const int taps = tkh * tkw;
   const long total = (long)co_p * taps * ci_n;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
     const int co = (int)(i % co_p);
     const long rest = i / co_p;
     const int tap = (int)(rest % taps);
     const int ci = (int)(rest / taps);
-    wt[i] = co < co_n ? w[((long)co * taps + tap) * ci_n + ci] : (T)0.0f;
+    const int r = r0h + (tap / tkw) * rstep, sc = r0w + (tap % tkw) * rstep;
+    wt[i] = co < co_n ? w[(((long)co * kh + r) * kw + sc) * ci_n + ci] : (T)0.0f;
   }
 }
 
@@ -529,6 +618,9 @@ static ConvArgs make_args(const rtsds_conv_desc* d) {
   p.f_c = fastdiv_make(d->c);
   p.f_k = fastdiv_make(d->k);
   p.f_kw = fastdiv_make(d->kw);
+  p.tkw = d->kw; p.f_tkw = p.f_kw;
+  p.r0h = p.r0w = 0; p.rstep = 1; p.psh = 1; p.offh = p.offw = 0;
+  p.hp = d->h; p.wp = d->w;
   p.tiles_per_split = 1 << 30;
   return p;
 }
@@ -581,32 +673,48 @@ static void launch(const ConvArgs& p, int splits, hipStream_t st) {
 // Tile selection for FWD / DGRAD (occupancy-aware): the widest tile that still puts >= 256
 // workgroups on the 256 CUs.  bf16: 128x128 / 128x64 / 256x32 (19- and 1-channel outputs),
 // falling back to 64x64 / 128x32 for small-M layers (ResNet layer4, pooled vectors).
-template <typename T, int MODE, int ALA>
-static void dispatch_mn(const ConvArgs& p, hipStream_t st) {
-  constexpr int BK = sizeof(T) == 2 ? 32 : 16;
-  auto blocks = [&](int bm, int bn) { return (long)rt_cdiv(p.M, bm) * rt_cdiv(p.N, bn); };
-  if (sizeof(T) == 2) {
-    if (p.N <= 32) {
-      if (blocks(256, 32) >= 256) launch<T, MODE, 256, 32, BK, 4, 1, ALA, 1>(p, 1, st);
-      else launch<T, MODE, 128, 32, BK, 4, 1, ALA, 1>(p, 1, st);
-    } else if (p.N <= 64) {
-      if (blocks(128, 64) >= 256) launch<T, MODE, 128, 64, BK, 2, 2, ALA, 1>(p, 1, st);
-      else launch<T, MODE, 64, 64, BK, 2, 2, ALA, 1>(p, 1, st);
-    } else {
-      if (blocks(128, 128) >= 256) launch<T, MODE, 128, 128, BK, 2, 2, ALA, 1>(p, 1, st);
-      else launch<T, MODE, 64, 64, BK, 2, 2, ALA, 1>(p, 1, st);
-    }
+static void pick_tile(long M, int N, bool b16, int& bm, int& bn) {
+  auto blocks = [&](int a, int b) { return ((M + a - 1) / a) * (long)((N + b - 1) / b); };
+  if (b16) {
+    if (N <= 32) { bn = 32; bm = blocks(256, 32) >= 256 ? 256 : 128; }
+    else if (N <= 64) { bn = 64; bm = blocks(128, 64) >= 256 ? 128 : 64; }
+    else if (blocks(128, 128) >= 256) { bm = 128; bn = 128; }
+    else { bm = 64; bn = 64; }
   } else {
-    if (p.N <= 32) launch<T, MODE, 128, 32, BK, 4, 1, ALA, 1>(p, 1, st);
-    else launch<T, MODE, 64, 64, BK, 2, 2, ALA, 1>(p, 1, st);
+    if (N <= 32) { bm = 128; bn = 32; } else { bm = 64; bn = 64; }
   }
+}
+
+// BK per tile: 64 where the tile is MFMA-dense (128x128, 64x64: one barrier per 64-deep
+// K-step), 32 for 128x64 / narrow-N tiles whose LDS footprint would otherwise cut occupancy.
+template <typename T, int MODE, int BM, int BN, int BK, int WM, int WN>
+static void launch_al(const ConvArgs& p, int cr, hipStream_t st) {
+  if (cr % BK == 0) launch<T, MODE, BM, BN, BK, WM, WN, 2, 1>(p, 1, st);
+  else launch<T, MODE, BM, BN, BK, WM, WN, 1, 1>(p, 1, st);
 }
 
 template <typename T, int MODE>
 static void dispatch_align(const ConvArgs& p, int cr, hipStream_t st) {
-  constexpr int BK = sizeof(T) == 2 ? 32 : 16;
-  if (cr % BK == 0) dispatch_mn<T, MODE, 2>(p, st);
-  else dispatch_mn<T, MODE, 1>(p, st);
+  int bm, bn;
+  pick_tile(p.M, p.N, sizeof(T) == 2, bm, bn);
+  if constexpr (sizeof(T) == 2) {
+    if (bn == 32 && bm == 256) launch_al<T, MODE, 256, 32, 32, 4, 1>(p, cr, st);
+    else if (bn == 32) launch_al<T, MODE, 128, 32, 32, 4, 1>(p, cr, st);
+    else if (bn == 64 && bm == 128) launch_al<T, MODE, 128, 64, 32, 2, 2>(p, cr, st);
+    else if (bn == 64) launch_al<T, MODE, 64, 64, 64, 2, 2>(p, cr, st);
+    else launch_al<T, MODE, 128, 128, 64, 2, 2>(p, cr, st);
+  } else {
+    if (bn == 32) launch_al<T, MODE, 128, 32, 16, 4, 1>(p, cr, st);
+    else launch_al<T, MODE, 64, 64, 16, 2, 2>(p, cr, st);
+  }
+}
+
+// Number of M tiles (= BatchNorm partial-statistics rows) the forward launch of d uses.
+extern "C" int rtsds_conv2d_fwd_stats_tiles(const rtsds_conv_desc* d) {
+  int bm, bn;
+  const long M = (long)d->n * d->ho * d->wo;
+  pick_tile(M, d->k, d->dtype == RTSDS_BF16, bm, bn);
+  return (int)((M + bm - 1) / bm);
 }
 
 // FWD workspace: channel-padded copies of x and w when Cin is not a vector multiple.
@@ -618,7 +726,7 @@ extern "C" size_t rtsds_conv2d_fwd_workspace(const rtsds_conv_desc* d) {
 }
 
 extern "C" int rtsds_conv2d_fwd(const rtsds_conv_desc* d0, const void* x, const void* w, const float* bias,
-                                void* y, int act, void* ws, size_t ws_bytes, void* stream) {
+                                void* y, int act, float* bn_stats, void* ws, size_t ws_bytes, void* stream) {
   int e = check_desc(d0);
   if (e) return e;
   if (ws_bytes < rtsds_conv2d_fwd_workspace(d0)) return RTSDS_ERR_WORKSPACE;
@@ -639,6 +747,8 @@ extern "C" int rtsds_conv2d_fwd(const rtsds_conv_desc* d0, const void* x, const 
   p.a = x; p.b = w; p.bias = bias; p.out = y;
   p.act = act & 0xff;
   p.accum = (act & RTSDS_ACCUMULATE) ? 1 : 0;
+  if (bn_stats && (p.act || p.accum)) return RTSDS_ERR_UNSUPPORTED;
+  p.stats = bn_stats;
   p.M = d.n * d.ho * d.wo;
   p.N = d.k;
   p.K = d.kh * d.kw * d.c;
@@ -656,6 +766,28 @@ extern "C" size_t rtsds_conv2d_dgrad_workspace(const rtsds_conv_desc* d) {
   return b;
 }
 
+static void repack_launch(int dtype, const void* w, void* wt, int co_n, int co_p, int kh, int kw, int ci_n, int tkh, int tkw,
+                          int r0h, int r0w, int rstep, hipStream_t st) {
+  const long wn = (long)co_p * tkh * tkw * ci_n;
+  if (wn <= 0) return;
+  const int blocks = (int)std::min<long>(4096, (wn + 255) / 256);
+  if (dtype == RTSDS_BF16)
+    hipLaunchKernelGGL(repack_wt_kernel<bf16>, dim3(blocks), dim3(256), 0, st, (const bf16*)w, (bf16*)wt, co_n, co_p, kh, kw, ci_n,
+                       tkh, tkw, r0h, r0w, rstep);
+  else
+    hipLaunchKernelGGL(repack_wt_kernel<float>, dim3(blocks), dim3(256), 0, st, (const float*)w, (float*)wt, co_n, co_p, kh, kw, ci_n,
+                       tkh, tkw, r0h, r0w, rstep);
+}
+
+// Taps of one dgrad stride phase along an axis: input index i = t*2 + off receives from
+// kernel taps r with (i + pad - r*dil) even.
+static void phase_taps(int a, int pad, int dil, int ksz, int size, int& off, int& cnt_pix, int& r0, int& rstep, int& tk) {
+  off = ((a - pad) % 2 + 2) % 2;
+  cnt_pix = size > off ? (size - off + 1) / 2 : 0;
+  if (dil % 2) { r0 = a; rstep = 2; tk = ksz > a ? (ksz - a + 1) / 2 : 0; }
+  else { r0 = 0; rstep = 1; tk = a == 0 ? ksz : 0; }
+}
+
 extern "C" int rtsds_conv2d_dgrad(const rtsds_conv_desc* d0, const void* dy, const void* w, void* dx,
                                   int accumulate, void* ws, size_t ws_bytes, void* stream) {
   int e = check_desc(d0);
@@ -664,30 +796,51 @@ extern "C" int rtsds_conv2d_dgrad(const rtsds_conv_desc* d0, const void* dy, con
   if (ws_bytes < rtsds_conv2d_dgrad_workspace(d0)) return RTSDS_ERR_WORKSPACE;
   hipStream_t st = (hipStream_t)stream;
   rtsds_conv_desc d = *d0;
-  const int taps = d.kh * d.kw;
   const int kp = pad_c(d.k, d.dtype);
   const size_t es = esize(d.dtype);
   void* wt = ws;
-  const long wn = (long)kp * taps * d.c;
-  const int blocks = (int)std::min<long>(4096, (wn + 255) / 256);
-  if (d.dtype == RTSDS_BF16)
-    hipLaunchKernelGGL(repack_wt_kernel<bf16>, dim3(blocks), dim3(256), 0, st, (const bf16*)w, (bf16*)wt, d.k, kp, taps, d.c);
-  else
-    hipLaunchKernelGGL(repack_wt_kernel<float>, dim3(blocks), dim3(256), 0, st, (const float*)w, (float*)wt, d.k, kp, taps, d.c);
   if (kp != d.k) {
-    void* dyp = (char*)ws + al256((size_t)kp * taps * d.c * es);
+    void* dyp = (char*)ws + al256((size_t)kp * d.kh * d.kw * d.c * es);
     pad_any(d.dtype, dy, dyp, (long)d.n * d.ho * d.wo, d.k, kp, st);
     dy = dyp;
-    d.k = kp;
   }
-  ConvArgs p = make_args(&d);
-  p.a = dy; p.b = wt; p.bias = nullptr; p.out = dx; p.act = 0;
-  p.accum = accumulate ? 1 : 0;
-  p.M = d.n * d.h * d.w;
-  p.N = d.c;
-  p.K = taps * d.k;
-  if (d.dtype == RTSDS_BF16) dispatch_align<bf16, MODE_DGRAD>(p, d.k, st);
-  else dispatch_align<float, MODE_DGRAD>(p, d.k, st);
+  const int k_real = d.k;
+  d.k = kp;
+  if (d.sh == 2 && d.sw == 2) {
+    // stride-2: four parity phases, each a dense GEMM over only the taps that reach it
+    for (int a = 0; a < 2; ++a)
+      for (int b = 0; b < 2; ++b) {
+        int offh, hp, r0h, rsh, tkh, offw, wp, r0w, rsw, tkw;
+        phase_taps(a, d.ph, d.dh, d.kh, d.h, offh, hp, r0h, rsh, tkh);
+        phase_taps(b, d.pw, d.dw, d.kw, d.w, offw, wp, r0w, rsw, tkw);
+        if (hp == 0 || wp == 0) continue;
+        repack_launch(d.dtype, w, wt, k_real, kp, d.kh, d.kw, d.c, tkh, tkw, r0h, r0w, rsh, st);
+        ConvArgs p = make_args(&d);
+        p.a = dy; p.b = wt; p.bias = nullptr; p.out = dx; p.act = 0;
+        p.accum = accumulate ? 1 : 0;
+        p.hp = hp; p.wp = wp; p.psh = 2; p.offh = offh; p.offw = offw;
+        p.r0h = r0h; p.r0w = r0w; p.rstep = rsh;
+        p.tkw = tkw > 0 ? tkw : 1;
+        p.f_tkw = fastdiv_make(p.tkw);
+        p.f_hw = fastdiv_make(hp * wp);
+        p.f_w = fastdiv_make(wp);
+        p.M = d.n * hp * wp;
+        p.N = d.c;
+        p.K = tkh * tkw * kp;
+        if (d.dtype == RTSDS_BF16) dispatch_align<bf16, MODE_DGRAD>(p, kp, st);
+        else dispatch_align<float, MODE_DGRAD>(p, kp, st);
+      }
+  } else {
+    repack_launch(d.dtype, w, wt, k_real, kp, d.kh, d.kw, d.c, d.kh, d.kw, 0, 0, 1, st);
+    ConvArgs p = make_args(&d);
+    p.a = dy; p.b = wt; p.bias = nullptr; p.out = dx; p.act = 0;
+    p.accum = accumulate ? 1 : 0;
+    p.M = d.n * d.h * d.w;
+    p.N = d.c;
+    p.K = d.kh * d.kw * kp;
+    if (d.dtype == RTSDS_BF16) dispatch_align<bf16, MODE_DGRAD>(p, kp, st);
+    else dispatch_align<float, MODE_DGRAD>(p, kp, st);
+  }
   return hipGetLastError() == hipSuccess ? RTSDS_OK : RTSDS_ERR_LAUNCH;
 }
 
@@ -705,7 +858,7 @@ static WgradPlan wgrad_plan(const rtsds_conv_desc* d) {
   w.cp = pad_c(d->c, d->dtype);
   const int M = w.kp, N = d->kh * d->kw * w.cp;
   const long R = (long)d->n * d->ho * d->wo;
-  const int BK = b16 ? 32 : 16;
+  const int BK = b16 ? 64 : 16;
   w.bm = b16 ? (M <= 64 ? 64 : 128) : 64;
   w.bn = b16 ? (N <= 64 ? 64 : 128) : 64;
   const long tiles = (long)rt_cdiv(M, w.bm) * rt_cdiv(N, w.bn);
@@ -730,8 +883,8 @@ extern "C" size_t rtsds_conv2d_wgrad_workspace(const rtsds_conv_desc* d) {
 
 template <typename T>
 static void wgrad_launch(const ConvArgs& p, int bm, int bn, int splits, hipStream_t st) {
-  constexpr int BK = sizeof(T) == 2 ? 32 : 16;
-  if (sizeof(T) == 2) {
+  constexpr int BK = sizeof(T) == 2 ? 64 : 16;
+  if constexpr (sizeof(T) == 2) {
     if (bm == 64 && bn == 64) launch<T, MODE_WGRAD, 64, 64, BK, 2, 2, 1, 1>(p, splits, st);
     else if (bm == 64) launch<T, MODE_WGRAD, 64, 128, BK, 2, 2, 1, 1>(p, splits, st);
     else if (bn == 64) launch<T, MODE_WGRAD, 128, 64, BK, 2, 2, 1, 1>(p, splits, st);

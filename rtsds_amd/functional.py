@@ -85,7 +85,7 @@ class ConvFn(torch.autograd.Function):
     parameter itself or its bf16 shadow); gradients are returned for ``weight``."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, wq, stride, padding, dilation, act):
+    def forward(ctx, x, weight, bias, wq, stride, padding, dilation, act, stats):
         require_hip(x, weight)
         x = nhwc(x)
         k, _, kh, kw = weight.shape
@@ -93,8 +93,8 @@ class ConvFn(torch.autograd.Function):
         y = empty_nhwc(d.n, k, d.ho, d.wo, x.dtype, x.device)
         ws = workspace(lib.rtsds_conv2d_fwd_workspace(ctypes.byref(d)), x.device)
         with _Timed(d, "fwd"):
-            lib.rtsds_conv2d_fwd(ctypes.byref(d), _P(x), _P(wq), _P(bias), _P(y), act, _P(ws), ws.numel(),
-                                 stream())
+            lib.rtsds_conv2d_fwd(ctypes.byref(d), _P(x), _P(wq), _P(bias), _P(y), act, _P(stats), _P(ws),
+                                 ws.numel(), stream())
         ctx.d, ctx.act, ctx.has_bias = d, act, bias is not None
         ctx.params = (weight, bias)
         ctx.save_for_backward(x, wq, y if act else None)
@@ -138,11 +138,23 @@ class ConvFn(torch.autograd.Function):
                                            ws.numel(), stream())
                 if not ctx.needs_input_grad[1]:
                     dw = None
-        return dx, dw, db, None, None, None, None, None
+        return dx, dw, db, None, None, None, None, None, None
 
 
-def conv2d(x, weight, bias, wq, stride=(1, 1), padding=(0, 0), dilation=(1, 1), act=0):
-    return ConvFn.apply(x, weight, bias, wq, tuple(stride), tuple(padding), tuple(dilation), act)
+def conv2d(x, weight, bias, wq, stride=(1, 1), padding=(0, 0), dilation=(1, 1), act=0, bn_stats=False):
+    """bn_stats=True: the conv epilogue also emits the following BatchNorm's per-tile batch
+    statistics, attached to the output as ``_rt_bn_stats`` and consumed by batch_norm()."""
+    stats = nrb = None
+    if bn_stats and act == 0:
+        n, _, h, w = x.shape
+        k, _, kh, kw = weight.shape
+        d = _conv_desc(x, k, kh, kw, stride, padding, dilation)
+        nrb = lib.rtsds_conv2d_fwd_stats_tiles(ctypes.byref(d))
+        stats = torch.empty(nrb * k * 3, dtype=torch.float32, device=x.device)
+    y = ConvFn.apply(x, weight, bias, wq, tuple(stride), tuple(padding), tuple(dilation), act, stats)
+    if stats is not None:
+        y._rt_bn_stats = (stats, nrb)
+    return y
 
 
 class ConvSumFn(torch.autograd.Function):
@@ -166,7 +178,7 @@ class ConvSumFn(torch.autograd.Function):
             ws = workspace(lib.rtsds_conv2d_fwd_workspace(ctypes.byref(d)), x.device)
             with _Timed(d, "fwd"):
                 lib.rtsds_conv2d_fwd(ctypes.byref(d), _P(x), _P(wqs[i]), _P(biases[i]), _P(y),
-                                     0x100 if i else 0, _P(ws), ws.numel(), stream())
+                                     0x100 if i else 0, None, _P(ws), ws.numel(), stream())
             descs.append(d)
         ctx.descs = descs
         ctx.params = tuple(weights) + tuple(biases)
@@ -215,7 +227,8 @@ class BatchNormFn(torch.autograd.Function):
     """BatchNorm2d (+ residual add) (+ ReLU/LeakyReLU) fused, train or eval statistics."""
 
     @staticmethod
-    def forward(ctx, x, gamma, beta, res, running_mean, running_var, training, momentum, eps, act):
+    def forward(ctx, x, gamma, beta, res, running_mean, running_var, training, momentum, eps, act,
+                stats, stats_nrb):
         require_hip(x)
         x = nhwc(x)
         if res is not None:
@@ -228,7 +241,8 @@ class BatchNormFn(torch.autograd.Function):
         ws = workspace(lib.rtsds_bn_workspace(rows, c), x.device)
         lib.rtsds_bn_fwd(_P(x), _P(res), _P(y), rows, c, _P(gamma), _P(beta), _P(running_mean),
                          _P(running_var), _P(sm), _P(si), float(momentum), float(eps), int(training),
-                         act, dcode(x), _P(ws), ws.numel(), stream())
+                         act, _P(stats) if training else None, int(stats_nrb or 0), dcode(x), _P(ws),
+                         ws.numel(), stream())
         ctx.meta = (rows, c, int(training), act, res is not None)
         ctx.gamma, ctx.beta = gamma, beta
         ctx.save_for_backward(x, y, gamma, sm, si)
@@ -256,13 +270,15 @@ class BatchNormFn(torch.autograd.Function):
                          stream())
         if acc:
             dg = db = None
-        return dx, dg, db, dres, None, None, None, None, None, None
+        return dx, dg, db, dres, None, None, None, None, None, None, None, None
 
 
 def batch_norm(x, gamma, beta, running_mean, running_var, training, momentum, eps, act=0,
                residual=None):
+    st = getattr(x, "_rt_bn_stats", None) if training else None
+    stats, nrb = st if st is not None else (None, None)
     return BatchNormFn.apply(x, gamma, beta, residual, running_mean, running_var, training,
-                             momentum, eps, act)
+                             momentum, eps, act, stats, nrb)
 
 
 # ----------------------------------------------------------------------------- layout / dtype

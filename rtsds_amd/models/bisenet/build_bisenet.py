@@ -12,7 +12,7 @@ import torch
 from torch import nn
 
 from rtsds_amd import functional as F
-from rtsds_amd.nn import AdaptiveAvgPool2d, BatchNorm2d, Conv2d, ReLU, Sigmoid, to_input
+from rtsds_amd.nn import AdaptiveAvgPool2d, BatchNorm2d, Conv2d, ReLU, Sigmoid, conv_bn, to_input
 from .build_contextpath import build_contextpath
 
 
@@ -27,7 +27,7 @@ class ConvBlock(torch.nn.Module):
         self.relu = ReLU()
 
     def forward(self, input):
-        return self.bn(self.conv1(input), act="relu")
+        return conv_bn(self.conv1, self.bn, input, "relu")
 
 
 class Spatial_path(torch.nn.Module):
@@ -59,7 +59,7 @@ class AttentionRefinementModule(torch.nn.Module):
         pooled = self.avgpool(input)
         assert self.in_channels == pooled.size(1), \
             "in_channels and out_channels should all be {}".format(pooled.size(1))
-        att = self.bn(self.conv(pooled), act="sigmoid")
+        att = conv_bn(self.conv, self.bn, pooled, "sigmoid")
         return F.channel_scale(input, att)
 
 

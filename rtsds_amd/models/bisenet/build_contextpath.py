@@ -13,7 +13,7 @@ import torch
 from torch import nn
 
 from rtsds_amd import functional as F
-from rtsds_amd.nn import BatchNorm2d, Conv2d, MaxPool2d, ReLU
+from rtsds_amd.nn import BatchNorm2d, Conv2d, MaxPool2d, ReLU, conv_bn
 
 
 class BasicBlock(nn.Module):
@@ -32,10 +32,10 @@ class BasicBlock(nn.Module):
     def forward(self, x):
         skip = x
         if self.downsample is not None:
-            skip = self.downsample[1](self.downsample[0](x))
-        t = self.bn1(self.conv1(x), act="relu")
+            skip = conv_bn(self.downsample[0], self.downsample[1], x)
+        t = conv_bn(self.conv1, self.bn1, x, "relu")
         # bn2 + residual add + ReLU in one pass
-        return self.bn2(self.conv2(t), act="relu", residual=skip)
+        return conv_bn(self.conv2, self.bn2, t, "relu", skip)
 
 
 class Bottleneck(nn.Module):
@@ -57,10 +57,10 @@ class Bottleneck(nn.Module):
     def forward(self, x):
         skip = x
         if self.downsample is not None:
-            skip = self.downsample[1](self.downsample[0](x))
-        t = self.bn1(self.conv1(x), act="relu")
-        t = self.bn2(self.conv2(t), act="relu")
-        return self.bn3(self.conv3(t), act="relu", residual=skip)
+            skip = conv_bn(self.downsample[0], self.downsample[1], x)
+        t = conv_bn(self.conv1, self.bn1, x, "relu")
+        t = conv_bn(self.conv2, self.bn2, t, "relu")
+        return conv_bn(self.conv3, self.bn3, t, "relu", skip)
 
 
 class ResNet(nn.Module):
@@ -112,7 +112,7 @@ class _ContextPath(nn.Module):
 
     def forward(self, x):
         """x: NHWC compute-dtype batch -> (1/16 features, 1/32 features, GAP(1/32))."""
-        t = self.maxpool1(self.bn1(self.conv1(x), act="relu"))
+        t = self.maxpool1(conv_bn(self.conv1, self.bn1, x, "relu"))
         f3 = self.layer3(self.layer2(self.layer1(t)))
         f4 = self.layer4(f3)
         return f3, f4, F.global_avg_pool(f4)

@@ -11,7 +11,7 @@ import torch
 import torch.nn as nn
 
 from rtsds_amd import functional as F
-from rtsds_amd.nn import BatchNorm2d, Conv2d, MaxPool2d, ReLU, to_input
+from rtsds_amd.nn import BatchNorm2d, Conv2d, MaxPool2d, ReLU, conv_bn, to_input
 from rtsds_amd.nn import _shadow
 
 affine_par = True
@@ -40,10 +40,10 @@ class Bottleneck(nn.Module):
         self.stride = stride
 
     def forward(self, x):
-        skip = x if self.downsample is None else self.downsample[1](self.downsample[0](x))
-        t = self.bn1(self.conv1(x), act="relu")
-        t = self.bn2(self.conv2(t), act="relu")
-        return self.bn3(self.conv3(t), act="relu", residual=skip)
+        skip = x if self.downsample is None else conv_bn(self.downsample[0], self.downsample[1], x)
+        t = conv_bn(self.conv1, self.bn1, x, "relu")
+        t = conv_bn(self.conv2, self.bn2, t, "relu")
+        return conv_bn(self.conv3, self.bn3, t, "relu", skip)
 
 
 class ClassifierModule(nn.Module):
@@ -102,7 +102,7 @@ class ResNetMulti(nn.Module):
     def forward(self, x):
         _, _, H, W = x.size()
         t = to_input(x)
-        t = self.maxpool(self.bn1(self.conv1(t), act="relu"))
+        t = self.maxpool(conv_bn(self.conv1, self.bn1, t, "relu"))
         t = self.layer4(self.layer3(self.layer2(self.layer1(t))))
         t = self.layer6(t)
         t = F.interpolate_bilinear(t, size=(H, W))

@@ -48,10 +48,12 @@ class Conv2d(nn.Conv2d):
             self.weight.data = self.weight.data.contiguous(memory_format=CL)
         return out
 
-    def forward(self, x, act=None):
+    def forward(self, x, act=None, bn_stats=False):
+        """``bn_stats``: also emit the batch statistics of a directly following train-mode
+        BatchNorm from the conv epilogue (see functional.conv2d)."""
         wq = _shadow(self.weight, x.dtype)
         return F.conv2d(x, self.weight, self.bias, wq, self.stride, self.padding, self.dilation,
-                        ACT[act])
+                        ACT[act], bn_stats)
 
 
 class BatchNorm2d(nn.BatchNorm2d):
@@ -114,6 +116,13 @@ class MaxPool2d(nn.Module):
 
     def forward(self, x):
         return F.max_pool2d(x, self.kernel_size, self.stride, self.padding, self.ceil_mode)
+
+
+def conv_bn(conv, bn, x, act=None, residual=None):
+    """bn(conv(x)) with the BatchNorm's batch statistics produced by the conv epilogue
+    (train mode) instead of a separate pass over the conv output."""
+    use_batch = bn.training or not bn.track_running_stats
+    return bn(conv(x, bn_stats=use_batch), act=act, residual=residual)
 
 
 def to_input(x):

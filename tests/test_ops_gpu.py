@@ -50,6 +50,9 @@ CONV_CASES = [
     (8, 256, 1, 1, 256, 1, 1, 0, 1, True),     # ARM 1x1 on pooled vectors
     (2, 1024, 8, 16, 19, 3, 1, 1, 1, False),   # FFM conv (K=9216, N=19)
     (2, 256, 8, 8, 512, 3, 2, 1, 1, False),    # layer4 conv1
+    (1, 32, 13, 17, 64, 3, 2, 1, 1, False),    # stride-2 dgrad phases, odd sizes
+    (2, 8, 9, 11, 16, 4, 2, 1, 1, True),       # k4 s2 phases, odd sizes
+    (2, 16, 7, 9, 32, 1, 2, 0, 1, False),      # 1x1 s2: odd phases receive nothing
 ]
 
 
