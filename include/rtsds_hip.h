@@ -76,24 +76,28 @@ int rtsds_conv2d_wgrad(const rtsds_conv_desc* d, const void* x, const void* dy, 
  * Replaces nn.BatchNorm2d at build_bisenet.py:13,39; torchvision ResNet bn*; deeplabv2.py:14-27,
  * 75,101 (frozen affine, train-mode batch statistics).  x, y, res, dy, dx: NHWC [rows][c]
  * with rows = n*h*w.
- * Forward (training): mean/invstd of the batch are written to save_mean / save_invstd and
- * the running buffers are updated in place with the unbiased variance, momentum m
- * (PyTorch semantics).  Forward (eval): running stats are used, save_* untouched.
+ * Forward (training): mean/invstd of the batch are written to save_mean / save_invstd, the
+ * running buffers are updated in place with the unbiased variance, momentum m, and
+ * *num_batches_tracked (int64, may be NULL) is incremented on the device (PyTorch
+ * semantics).  Forward (eval): running stats are used and copied to save_* when non-NULL.
  * y = act(gamma * (x - mean) * invstd + beta [+ res]).  gamma/beta may be NULL (1 / 0).   */
 size_t rtsds_bn_workspace(long rows, int c);
 /* stats_part (may be NULL): [stats_nrb][c][count, mean, M2] partials from the producing
  * conv (rtsds_conv2d_fwd bn_stats) -- training mode then skips its own statistics pass.   */
 int rtsds_bn_fwd(const void* x, const void* res, void* y, long rows, int c, const float* gamma,
-                 const float* beta, float* running_mean, float* running_var, float* save_mean,
+                 const float* beta, float* running_mean, float* running_var,
+                 long long* num_batches_tracked, float* save_mean,
                  float* save_invstd, float momentum, float eps, int training, int act,
                  const float* stats_part, int stats_nrb, int dtype, void* ws, size_t ws_bytes,
                  void* stream);
-/* Backward of the fused BN(+res)(+act) above, given y (post-activation output) for the
- * activation mask.  dx, dres (may be NULL), dgamma/dbeta (fp32, may be NULL; overwritten, or
- * added to when accumulate_params != 0).  training=0: eval-mode backward (constant stats). */
+/* Backward of the fused BN(+res)(+act) above.  y (post-activation output) gives the
+ * activation mask; it may be NULL without a residual for act NONE/RELU/LEAKY, when the mask
+ * is recomputed bit-exactly from x, gamma, beta and save_*.  dx, dres (may be NULL),
+ * dgamma/dbeta (fp32, may be NULL; overwritten, or added to when accumulate_params != 0).
+ * training=0: eval-mode backward (constant stats).                                        */
 int rtsds_bn_bwd(const void* dy, const void* x, const void* y, void* dx, void* dres,
                  float* dgamma, float* dbeta, long rows, int c, const float* gamma,
-                 const float* save_mean, const float* save_invstd, int training, int act,
+                 const float* beta, const float* save_mean, const float* save_invstd, int training, int act,
                  int accumulate_params, int dtype, void* ws, size_t ws_bytes, void* stream);
 
 /* ---------------------------------------------------------------- layout / dtype

@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "librtsds_hip.so")
 
 F32, BF16 = 0, 1
-ACT_NONE, ACT_RELU, ACT_LEAKY = 0, 1, 2
+ACT_NONE, ACT_RELU, ACT_LEAKY, ACT_SIGMOID = 0, 1, 2, 3
 ACCUMULATE = 0x100
 ERRORS = {1: "bad shape", 2: "unsupported configuration", 3: "HIP launch failure", 4: "workspace too small"}
 
@@ -38,9 +38,9 @@ SIGNATURES = {
     "rtsds_conv2d_wgrad_workspace": (c_size_t, [ctypes.POINTER(ConvDesc)]),
     "rtsds_conv2d_wgrad": (c_int, [ctypes.POINTER(ConvDesc), P, P, P, P, c_int, P, c_size_t, P]),
     "rtsds_bn_workspace": (c_size_t, [c_long, c_int]),
-    "rtsds_bn_fwd": (c_int, [P, P, P, c_long, c_int, P, P, P, P, P, P, c_float, c_float, c_int,
+    "rtsds_bn_fwd": (c_int, [P, P, P, c_long, c_int, P, P, P, P, P, P, P, c_float, c_float, c_int,
                              c_int, P, c_int, c_int, P, c_size_t, P]),
-    "rtsds_bn_bwd": (c_int, [P, P, P, P, P, P, P, c_long, c_int, P, P, P, c_int, c_int, c_int, c_int,
+    "rtsds_bn_bwd": (c_int, [P, P, P, P, P, P, P, c_long, c_int, P, P, P, P, c_int, c_int, c_int, c_int,
                              P, c_size_t, P]),
     "rtsds_nchw_to_nhwc": (c_int, [P, P, c_int, c_int, c_int, c_int, c_int, P]),
     "rtsds_cast": (c_int, [P, c_int, P, c_int, c_long, P]),

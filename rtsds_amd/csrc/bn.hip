@@ -9,7 +9,7 @@
 #include "common.h"
 #include <algorithm>
 
-static const int kBnMaxRB = 512;  // row blocks of the partial-statistics pass
+static const int kBnMaxRB = 2048;  // row blocks of the partial-statistics pass
 
 // Threads of a 256-block are laid out [row group][channel vector]; TPR = threads per row.
 template <int VEC> struct BnLayout {
@@ -44,6 +44,13 @@ RT_DEV void store_vec(T* p, const float* v, int cvalid) {
     for (int j = 0; j < VEC; ++j)
       if (j < cvalid) p[j] = from_f<T>(v[j]);
   }
+}
+
+// scale/shift of y = x*scale + shift.  Written with explicit fma so the backward can
+// recompute exactly the forward's pre-activation (ReLU mask without reading y).
+RT_DEV void bn_coef(float g, float b, float m, float inv, float& sc, float& sh) {
+  sc = g * inv;
+  sh = fmaf(-m, sc, b);
 }
 
 RT_DEV void chan_merge(float& na, float& ma, float& Ma, float nb, float mb, float Mb) {
@@ -114,6 +121,56 @@ __global__ void __launch_bounds__(256) bn_stats_kernel(const T* __restrict__ x, 
   }
 }
 
+// Optional pre-merge when there are many row-block partials (the conv epilogue emits one per
+// 128-row M-tile): out[s][c][W] merges part[b][c][W] for b = s*4 + wave (+= 4*S).  Lanes run
+// across channels, so every wave-load is a contiguous 64-channel record run; loads of four
+// partials are issued before they are merged.  W = 3: (count, mean, M2) Chan merge;
+// W = 2: plain sums.  Fixed merge order -> deterministic.
+template <int W>
+RT_DEV void rec_merge(float* a, const float* b) {
+  if constexpr (W == 3) chan_merge(a[0], a[1], a[2], b[0], b[1], b[2]);
+  else { a[0] += b[0]; a[1] += b[1]; }
+}
+template <int W>
+__global__ void __launch_bounds__(256) bn_premerge_kernel(const float* __restrict__ part, int nrb, int c, float* __restrict__ out) {
+  __shared__ float red[4][64][W];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int ch = blockIdx.x * 64 + lane, S = gridDim.y, s = blockIdx.y;
+  float acc[W];
+#pragma unroll
+  for (int k = 0; k < W; ++k) acc[k] = 0.f;
+  if (ch < c) {
+    int b = s * 4 + w;
+    const int stride = 4 * S;
+    for (; b + 3 * stride < nrb; b += 4 * stride) {
+      float t[4][W];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int k = 0; k < W; ++k) t[u][k] = part[((long)(b + u * stride) * c + ch) * W + k];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) rec_merge<W>(acc, t[u]);
+    }
+    for (; b < nrb; b += stride) {
+      float t[W];
+#pragma unroll
+      for (int k = 0; k < W; ++k) t[k] = part[((long)b * c + ch) * W + k];
+      rec_merge<W>(acc, t);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < W; ++k) red[w][lane][k] = acc[k];
+  __syncthreads();
+  if (w == 0 && ch < c) {
+#pragma unroll
+    for (int q = 1; q < 4; ++q) rec_merge<W>(acc, red[q][lane]);
+#pragma unroll
+    for (int k = 0; k < W; ++k) out[((long)s * c + ch) * W + k] = acc[k];
+  }
+}
+static const int kBnMergeMax = 256;   // stage-2 partial count bound
+static int bn_premerge_s(int nrb) { return nrb <= kBnMergeMax ? 0 : std::min(kBnMergeMax, (nrb + 15) / 16); }
+
 // Pass 2 (forward): one wave per channel merges the row-block partials (Chan, lane-strided,
 // then a shuffle tree), updates running stats and emits scale/shift.
 RT_DEV void chan_merge_shfl(float& n, float& m, float& M) {
@@ -125,8 +182,9 @@ RT_DEV void chan_merge_shfl(float& n, float& m, float& M) {
 }
 __global__ void __launch_bounds__(64) bn_finalize_kernel(const float* __restrict__ part, int nrb, int c, long rows, const float* gamma,
                                    const float* beta, float* rmean, float* rvar, float* smean, float* sinv,
-                                   float* scale, float* shift, float momentum, float eps) {
+                                   float* scale, float* shift, float momentum, float eps, long long* nbt) {
   const int ch = blockIdx.x, lane = threadIdx.x;
+  if (nbt && ch == 0 && lane == 0) *nbt += 1;  // num_batches_tracked.add_(1)
   float n = 0.f, m = 0.f, M = 0.f;
   for (int b = lane; b < nrb; b += 64) {
     const float* p = part + ((long)b * c + ch) * 3;
@@ -144,8 +202,7 @@ __global__ void __launch_bounds__(64) bn_finalize_kernel(const float* __restrict
     rvar[ch] = (1.f - momentum) * rvar[ch] + momentum * unb;
   }
   const float g = gamma ? gamma[ch] : 1.f, b = beta ? beta[ch] : 0.f;
-  scale[ch] = g * inv;
-  shift[ch] = b - m * g * inv;
+  bn_coef(g, b, m, inv, scale[ch], shift[ch]);
 }
 
 __global__ void bn_eval_coef_kernel(int c, const float* gamma, const float* beta, const float* rmean, const float* rvar,
@@ -156,8 +213,7 @@ __global__ void bn_eval_coef_kernel(int c, const float* gamma, const float* beta
   if (smean) smean[ch] = rmean[ch];
   if (sinv) sinv[ch] = inv;
   const float g = gamma ? gamma[ch] : 1.f, b = beta ? beta[ch] : 0.f;
-  scale[ch] = g * inv;
-  shift[ch] = b - rmean[ch] * g * inv;
+  bn_coef(g, b, rmean[ch], inv, scale[ch], shift[ch]);
 }
 
 RT_DEV float act_f(float v, int act) {
@@ -173,70 +229,145 @@ RT_DEV float act_grad(float y, int act) {
   return 1.f;
 }
 
-// Pass 3 (forward): y = act(x * scale + shift [+ res]).
+// Per-channel coefficients for a thread's VEC channels.  Coefficient arrays live in the
+// 256-B aligned workspace and VEC > 1 only when c % VEC == 0, so VEC % 4 == 0 loads are 16 B.
+template <int VEC>
+RT_DEV void load_coef(const float* __restrict__ p, int ch0, int c, float* v) {
+  if constexpr (VEC % 4 == 0) {
+#pragma unroll
+    for (int q = 0; q < VEC / 4; ++q) {
+      const f32x4 t = *(const f32x4*)(p + ch0 + 4 * q);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[4 * q + e] = t[e];
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) v[j] = p[min(ch0 + j, c - 1)];
+  }
+}
+
+// Pass 3 (forward): y = act(x * scale + shift [+ res]).  Same [row group][channel vector]
+// layout as the statistics pass: each thread owns one channel vector for its whole row
+// sweep, so the coefficients sit in registers and there is no per-element index division.
 template <typename T, int VEC>
 __global__ void __launch_bounds__(256) bn_apply_kernel(const T* __restrict__ x, const T* __restrict__ res, T* __restrict__ y,
                                                         const float* __restrict__ scale, const float* __restrict__ shift,
                                                         long rows, int c, int act) {
-  const int cvn = (c + VEC - 1) / VEC;
-  const long total = rows * cvn;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    const long r = i / cvn;
-    const int ch0 = (int)(i - r * cvn) * VEC;
-    const long off = r * c + ch0;
-    float v[VEC], rv[VEC];
-    load_vec<T, VEC>(x + off, v, c - ch0);
-    if (res) load_vec<T, VEC>(res + off, rv, c - ch0);
+  const int cbase = blockIdx.y * 256 * VEC;
+  const int cl = min(c - cbase, 256 * VEC);
+  const BnLayout<VEC> L(cl);
+  const int tid = threadIdx.x, cv = tid % L.tpr, rg = tid / L.tpr;
+  if (rg >= L.rpi || cv * VEC >= cl) return;
+  const int ch0 = cbase + cv * VEC, cvalid = c - ch0;
+  float sc[VEC], sh[VEC];
+  load_coef<VEC>(scale, ch0, c, sc);
+  load_coef<VEC>(shift, ch0, c, sh);
+  const long step = (long)gridDim.x * L.rpi;
+  long r = (long)blockIdx.x * L.rpi + rg;
+  for (; r + step < rows; r += 2 * step) {  // two independent rows in flight per thread
+    float v0[VEC], v1[VEC], r0[VEC], r1[VEC];
+    load_vec<T, VEC>(x + r * c + ch0, v0, cvalid);
+    load_vec<T, VEC>(x + (r + step) * c + ch0, v1, cvalid);
+    if (res) {
+      load_vec<T, VEC>(res + r * c + ch0, r0, cvalid);
+      load_vec<T, VEC>(res + (r + step) * c + ch0, r1, cvalid);
+    }
 #pragma unroll
     for (int j = 0; j < VEC; ++j) {
-      const int ch = min(ch0 + j, c - 1);
-      float o = fmaf(v[j], scale[ch], shift[ch]);
-      if (res) o += rv[j];
-      v[j] = act_f(o, act);
+      float a = fmaf(v0[j], sc[j], sh[j]), b = fmaf(v1[j], sc[j], sh[j]);
+      if (res) { a += r0[j]; b += r1[j]; }
+      v0[j] = act_f(a, act);
+      v1[j] = act_f(b, act);
     }
-    store_vec<T, VEC>(y + off, v, c - ch0);
+    store_vec<T, VEC>(y + r * c + ch0, v0, cvalid);
+    store_vec<T, VEC>(y + (r + step) * c + ch0, v1, cvalid);
+  }
+  if (r < rows) {
+    float v0[VEC], r0[VEC];
+    load_vec<T, VEC>(x + r * c + ch0, v0, cvalid);
+    if (res) load_vec<T, VEC>(res + r * c + ch0, r0, cvalid);
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) {
+      float a = fmaf(v0[j], sc[j], sh[j]);
+      if (res) a += r0[j];
+      v0[j] = act_f(a, act);
+    }
+    store_vec<T, VEC>(y + r * c + ch0, v0, cvalid);
+  }
+}
+
+// Activation derivative from either the saved output y, or -- when y is not kept (no
+// residual, monotone activation with act'(v) determined by sign(v)) -- from the recomputed
+// pre-activation x*scale+shift, which is bit-identical to the forward's.
+template <typename T, int VEC>
+RT_DEV void bn_act_grad(float* g, const T* y, const float* xv, const float* sc, const float* sh, int act, int cvalid) {
+  if (!act) return;
+  if (y) {
+    float yv[VEC];
+    load_vec<T, VEC>(y, yv, cvalid);
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) g[j] *= act_grad(yv[j], act);
+  } else {
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) {
+      const bool pos = fmaf(xv[j], sc[j], sh[j]) > 0.f;
+      g[j] = pos ? g[j] : (act == RTSDS_ACT_LEAKY ? 0.2f * g[j] : 0.f);
+    }
+  }
+}
+
+template <int VEC>
+RT_DEV void bn_bwd_coef(int ch0, int c, const float* gamma, const float* beta, const float* mean, const float* sinv,
+                        float* mu, float* sc, float* sh) {
+#pragma unroll
+  for (int j = 0; j < VEC; ++j) {
+    const int ch = min(ch0 + j, c - 1);
+    mu[j] = mean[ch];
+    bn_coef(gamma ? gamma[ch] : 1.f, beta ? beta[ch] : 0.f, mu[j], sinv[ch], sc[j], sh[j]);
   }
 }
 
 // Backward pass 1: part[(rb*c+ch)*2 + {0,1}] = (sum g, sum g*(x-mean)) with g = dy*act'(y).
 template <typename T, int VEC>
 __global__ void __launch_bounds__(256) bn_bwd_stats_kernel(const T* __restrict__ dy, const T* __restrict__ x,
-                                                            const T* __restrict__ y, const float* __restrict__ mean,
-                                                            float* __restrict__ part, long rows, int c, int act) {
-  __shared__ float sh[2][256][VEC];
+                                                            const T* __restrict__ y, const float* __restrict__ gamma,
+                                                            const float* __restrict__ beta, const float* __restrict__ mean,
+                                                            const float* __restrict__ sinv, float* __restrict__ part,
+                                                            long rows, int c, int act) {
+  __shared__ float red[2][256][VEC];
   const int cbase = blockIdx.y * 256 * VEC;
   const int cl = min(c - cbase, 256 * VEC);
   const BnLayout<VEC> L(cl);
   const int tid = threadIdx.x, cv = tid % L.tpr, rg = tid / L.tpr;
   const int ch0 = cbase + cv * VEC;
   const bool active = rg < L.rpi && cv * VEC < cl;
-  float sg[VEC], sgx[VEC], mu[VEC];
+  float sg[VEC], sgx[VEC], mu[VEC], sc[VEC], sh[VEC];
 #pragma unroll
-  for (int j = 0; j < VEC; ++j) { sg[j] = 0.f; sgx[j] = 0.f; mu[j] = active ? mean[min(ch0 + j, c - 1)] : 0.f; }
+  for (int j = 0; j < VEC; ++j) { sg[j] = 0.f; sgx[j] = 0.f; }
   if (active) {
+    bn_bwd_coef<VEC>(ch0, c, gamma, beta, mean, sinv, mu, sc, sh);
     for (long r = (long)blockIdx.x * L.rpi + rg; r < rows; r += (long)gridDim.x * L.rpi) {
-      float g[VEC], xv[VEC], yv[VEC];
+      float g[VEC], xv[VEC];
       load_vec<T, VEC>(dy + r * c + ch0, g, c - ch0);
       load_vec<T, VEC>(x + r * c + ch0, xv, c - ch0);
-      if (act) load_vec<T, VEC>(y + r * c + ch0, yv, c - ch0);
+      bn_act_grad<T, VEC>(g, y ? y + r * c + ch0 : nullptr, xv, sc, sh, act, c - ch0);
 #pragma unroll
       for (int j = 0; j < VEC; ++j) {
-        const float gg = act ? g[j] * act_grad(yv[j], act) : g[j];
-        sg[j] += gg;
-        sgx[j] = fmaf(gg, xv[j] - mu[j], sgx[j]);
+        sg[j] += g[j];
+        sgx[j] = fmaf(g[j], xv[j] - mu[j], sgx[j]);
       }
     }
   }
 #pragma unroll
-  for (int j = 0; j < VEC; ++j) { sh[0][tid][j] = sg[j]; sh[1][tid][j] = sgx[j]; }
+  for (int j = 0; j < VEC; ++j) { red[0][tid][j] = sg[j]; red[1][tid][j] = sgx[j]; }
   __syncthreads();
   if (rg == 0 && cv * VEC < cl) {
 #pragma unroll
     for (int j = 0; j < VEC; ++j) {
-      float a = sh[0][tid][j], b = sh[1][tid][j];
+      float a = red[0][tid][j], b = red[1][tid][j];
       for (int gi = 1; gi < L.rpi; ++gi) {
-        a += sh[0][gi * L.tpr + cv][j];
-        b += sh[1][gi * L.tpr + cv][j];
+        a += red[0][gi * L.tpr + cv][j];
+        b += red[1][gi * L.tpr + cv][j];
       }
       if (ch0 + j < c) {
         float* o = part + ((long)blockIdx.x * c + ch0 + j) * 2;
@@ -247,9 +378,10 @@ __global__ void __launch_bounds__(256) bn_bwd_stats_kernel(const T* __restrict__
 }
 
 // Backward pass 2: coefficients  dx = A*g + B*(x-mean) + C  per channel (one wave each).
+// coef = [A | B | C | mean | scale | shift] x c  (the last three for the mask recompute).
 __global__ void __launch_bounds__(64) bn_bwd_finalize_kernel(const float* __restrict__ part, int nrb, int c, long rows, const float* gamma,
-                                       const float* smean, const float* sinv, float* dgamma, float* dbeta,
-                                       float* coefA, float* coefB, float* coefC, int training, int accumulate) {
+                                       const float* beta, const float* smean, const float* sinv, float* dgamma, float* dbeta,
+                                       float* coef, int training, int accumulate) {
   const int ch = blockIdx.x, lane = threadIdx.x;
   float sg = 0.f, sgx = 0.f;
   for (int b = lane; b < nrb; b += 64) {
@@ -264,83 +396,150 @@ __global__ void __launch_bounds__(64) bn_bwd_finalize_kernel(const float* __rest
   if (dbeta) dbeta[ch] = accumulate ? dbeta[ch] + sg : sg;
   const float a = g * inv;
   const float invn = 1.f / (float)rows;
-  coefA[ch] = a;
-  coefB[ch] = training ? -a * inv * inv * sgx * invn : 0.f;
-  coefC[ch] = training ? -a * sg * invn : 0.f;
-  (void)smean;
+  coef[ch] = a;
+  coef[c + ch] = training ? -a * inv * inv * sgx * invn : 0.f;
+  coef[2 * c + ch] = training ? -a * sg * invn : 0.f;
+  coef[3 * c + ch] = smean[ch];
+  bn_coef(g, beta ? beta[ch] : 0.f, smean[ch], inv, coef[4 * c + ch], coef[5 * c + ch]);
 }
 
-// Backward pass 3: dx = A*g + B*(x - mean) + C;  dres = g.
+// Backward pass 3: dx = A*g + B*(x - mean) + C;  dres = g.  Layout as bn_apply_kernel.
 template <typename T, int VEC>
 __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const T* __restrict__ dy, const T* __restrict__ x,
                                                             const T* __restrict__ y, T* __restrict__ dx, T* __restrict__ dres,
-                                                            const float* __restrict__ mean, const float* __restrict__ A,
-                                                            const float* __restrict__ B, const float* __restrict__ C,
-                                                            long rows, int c, int act) {
-  const int cvn = (c + VEC - 1) / VEC;
-  const long total = rows * cvn;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    const long r = i / cvn;
-    const int ch0 = (int)(i - r * cvn) * VEC;
-    const long off = r * c + ch0;
-    float g[VEC], xv[VEC], yv[VEC], o[VEC];
-    load_vec<T, VEC>(dy + off, g, c - ch0);
-    load_vec<T, VEC>(x + off, xv, c - ch0);
-    if (act) load_vec<T, VEC>(y + off, yv, c - ch0);
+                                                            const float* __restrict__ coef, long rows, int c, int act) {
+  const int cbase = blockIdx.y * 256 * VEC;
+  const int cl = min(c - cbase, 256 * VEC);
+  const BnLayout<VEC> L(cl);
+  const int tid = threadIdx.x, cv = tid % L.tpr, rg = tid / L.tpr;
+  if (rg >= L.rpi || cv * VEC >= cl) return;
+  const int ch0 = cbase + cv * VEC, cvalid = c - ch0;
+  float a[VEC], b[VEC], k[VEC], mu[VEC], sc[VEC], sh[VEC];
+  load_coef<VEC>(coef, ch0, c, a);
+  load_coef<VEC>(coef + c, ch0, c, b);
+  load_coef<VEC>(coef + 2 * c, ch0, c, k);
+  load_coef<VEC>(coef + 3 * c, ch0, c, mu);
+  if (act && !y) {
+    load_coef<VEC>(coef + 4 * c, ch0, c, sc);
+    load_coef<VEC>(coef + 5 * c, ch0, c, sh);
+  }
+  const long step = (long)gridDim.x * L.rpi;
+  long r = (long)blockIdx.x * L.rpi + rg;
+  for (; r + step < rows; r += 2 * step) {  // two independent rows in flight per thread
+    const long o0 = r * c + ch0, o1 = o0 + step * c;
+    float g0[VEC], x0[VEC], g1[VEC], x1[VEC];
+    load_vec<T, VEC>(dy + o0, g0, cvalid);
+    load_vec<T, VEC>(x + o0, x0, cvalid);
+    load_vec<T, VEC>(dy + o1, g1, cvalid);
+    load_vec<T, VEC>(x + o1, x1, cvalid);
+    bn_act_grad<T, VEC>(g0, y ? y + o0 : nullptr, x0, sc, sh, act, cvalid);
+    bn_act_grad<T, VEC>(g1, y ? y + o1 : nullptr, x1, sc, sh, act, cvalid);
 #pragma unroll
     for (int j = 0; j < VEC; ++j) {
-      const int ch = min(ch0 + j, c - 1);
-      if (act) g[j] *= act_grad(yv[j], act);
-      o[j] = fmaf(A[ch], g[j], fmaf(B[ch], xv[j] - mean[ch], C[ch]));
+      x0[j] = fmaf(a[j], g0[j], fmaf(b[j], x0[j] - mu[j], k[j]));
+      x1[j] = fmaf(a[j], g1[j], fmaf(b[j], x1[j] - mu[j], k[j]));
     }
-    if (dx) store_vec<T, VEC>(dx + off, o, c - ch0);
-    if (dres) store_vec<T, VEC>(dres + off, g, c - ch0);
+    if (dx) {
+      store_vec<T, VEC>(dx + o0, x0, cvalid);
+      store_vec<T, VEC>(dx + o1, x1, cvalid);
+    }
+    if (dres) {
+      store_vec<T, VEC>(dres + o0, g0, cvalid);
+      store_vec<T, VEC>(dres + o1, g1, cvalid);
+    }
+  }
+  if (r < rows) {
+    const long off = r * c + ch0;
+    float g[VEC], xv[VEC];
+    load_vec<T, VEC>(dy + off, g, cvalid);
+    load_vec<T, VEC>(x + off, xv, cvalid);
+    bn_act_grad<T, VEC>(g, y ? y + off : nullptr, xv, sc, sh, act, cvalid);
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) xv[j] = fmaf(a[j], g[j], fmaf(b[j], xv[j] - mu[j], k[j]));
+    if (dx) store_vec<T, VEC>(dx + off, xv, cvalid);
+    if (dres) store_vec<T, VEC>(dres + off, g, cvalid);
   }
 }
 
 // ------------------------------------------------------------------ host
-static int bn_rb(long rows, int c, int vec) {
+static long bn_need(long rows, int c, int vec) {
   int tpr = (c + vec - 1) / vec;
   if (tpr > 256) tpr = 256;
   const int rpi = 256 / tpr;
-  long need = (rows + rpi - 1) / rpi;
-  // ~1-2k blocks overall, at least 4 row-iterations per thread when rows are large
+  return (rows + rpi - 1) / rpi;
+}
+// Row blocks of the reduction passes: enough to fill the chip (8+ waves per CU), at least
+// 4 row-iterations per thread, at most kBnMaxRB partials to merge.
+static int bn_rb(long rows, int c, int vec) {
+  const long need = bn_need(rows, c, vec);
   long rb = std::min<long>(need, kBnMaxRB);
   rb = std::max<long>(1, std::min<long>(rb, (need + 3) / 4));
   return (int)rb;
 }
+// Row blocks of the elementwise passes: ~2 rows per thread.
+static int bn_apply_rb(long rows, int c, int vec) {
+  const long need = bn_need(rows, c, vec);
+  return (int)std::max<long>(1, std::min<long>((need + 1) / 2, 1L << 24));
+}
 
+static size_t bn_part_floats(long rows, int c) { return (size_t)bn_rb(rows, c, 1) * c * 3; }
+
+// Workspace: [row-block partials | pre-merged partials | 8 coefficient arrays], each part
+// 256-B aligned (coefficient arrays are read with 16-B vector loads).
+static size_t al64f(size_t n) { return (n + 63) & ~(size_t)63; }
+struct BnWs {
+  float *part, *merged, *coef;
+};
+static BnWs bn_ws(void* ws, long rows, int c) {
+  BnWs w;
+  w.part = (float*)ws;
+  w.merged = w.part + al64f(bn_part_floats(rows, c));
+  w.coef = w.merged + al64f((size_t)kBnMergeMax * c * 3);
+  return w;
+}
 extern "C" size_t rtsds_bn_workspace(long rows, int c) {
-  (void)rows;
-  // partials (3 floats x RB x c) + 5 per-channel coefficient arrays
-  return (size_t)kBnMaxRB * c * 3 * 4 + (size_t)c * 5 * 4 + 256;
+  if (rows <= 0 || c <= 0) return 256;
+  // partials (3 floats x RB x c; VEC=1 gives the most row blocks) + pre-merge + 8 x c
+  return (al64f(bn_part_floats(rows, c)) + al64f((size_t)kBnMergeMax * c * 3) + al64f((size_t)c * 8)) * 4 + 256;
+}
+
+// Merge nrb partials down to <= kBnMergeMax when needed; returns the (pointer, count) to finalize.
+template <int W>
+static const float* bn_premerge(const float* part, int& nrb, int c, float* merged, hipStream_t st) {
+  const int S = bn_premerge_s(nrb);
+  if (!S) return part;
+  hipLaunchKernelGGL(bn_premerge_kernel<W>, dim3(rt_cdiv(c, 64), S), dim3(256), 0, st, part, nrb, c, merged);
+  nrb = S;
+  return merged;
 }
 
 template <typename T, int VEC>
 static void bn_fwd_launch(const void* x, const void* res, void* y, long rows, int c, const float* gamma, const float* beta,
                           float* rm, float* rv, float* sm, float* si, float mom, float eps, int training, int act,
-                          const float* pre, int pre_nrb, float* part, float* scale, float* shift, hipStream_t st) {
+                          const float* pre, int pre_nrb, long long* nbt, const BnWs& w, hipStream_t st) {
+  float* scale = w.coef;
+  float* shift = w.coef + c;
   if (training) {
     int rb = pre_nrb;
-    if (pre) {
-      part = (float*)pre;  // statistics already produced by the conv epilogue
-    } else {
+    const float* part = pre;  // statistics already produced by the conv epilogue, or:
+    if (!pre) {
       rb = bn_rb(rows, c, VEC);
-      hipLaunchKernelGGL((bn_stats_kernel<T, VEC>), dim3(rb, rt_cdiv(c, 256 * VEC)), dim3(256), 0, st, (const T*)x, part, rows, c);
+      hipLaunchKernelGGL((bn_stats_kernel<T, VEC>), dim3(rb, rt_cdiv(c, 256 * VEC)), dim3(256), 0, st, (const T*)x, w.part, rows, c);
+      part = w.part;
     }
+    part = bn_premerge<3>(part, rb, c, w.merged, st);
     hipLaunchKernelGGL(bn_finalize_kernel, dim3(c), dim3(64), 0, st, part, rb, c, rows, gamma, beta, rm, rv,
-                       sm, si, scale, shift, mom, eps);
+                       sm, si, scale, shift, mom, eps, nbt);
   } else {
     hipLaunchKernelGGL(bn_eval_coef_kernel, dim3(rt_cdiv(c, 256)), dim3(256), 0, st, c, gamma, beta, rm, rv, scale, shift, sm, si, eps);
   }
-  const long total = rows * ((c + VEC - 1) / VEC);
-  const int blocks = (int)std::min<long>(8192, (total + 255) / 256);
-  hipLaunchKernelGGL((bn_apply_kernel<T, VEC>), dim3(blocks), dim3(256), 0, st, (const T*)x, (const T*)res, (T*)y, scale, shift,
-                     rows, c, act);
+  hipLaunchKernelGGL((bn_apply_kernel<T, VEC>), dim3(bn_apply_rb(rows, c, VEC), rt_cdiv(c, 256 * VEC)), dim3(256), 0, st,
+                     (const T*)x, (const T*)res, (T*)y, scale, shift, rows, c, act);
 }
 
 extern "C" int rtsds_bn_fwd(const void* x, const void* res, void* y, long rows, int c, const float* gamma, const float* beta,
-                            float* running_mean, float* running_var, float* save_mean, float* save_invstd, float momentum,
+                            float* running_mean, float* running_var, long long* num_batches_tracked, float* save_mean,
+                            float* save_invstd, float momentum,
                             float eps, int training, int act, const float* stats_part, int stats_nrb, int dtype, void* ws,
                             size_t ws_bytes, void* stream) {
   if (rows <= 0 || c <= 0) return RTSDS_ERR_SHAPE;
@@ -349,53 +548,51 @@ extern "C" int rtsds_bn_fwd(const void* x, const void* res, void* y, long rows, 
   if (training && (!save_mean || !save_invstd)) return RTSDS_ERR_UNSUPPORTED;
   if (c > 65535 * 256) return RTSDS_ERR_UNSUPPORTED;
   hipStream_t st = (hipStream_t)stream;
-  float* part = (float*)ws;
-  float* scale = part + (size_t)kBnMaxRB * c * 3;
-  float* shift = scale + c;
+  const BnWs w = bn_ws(ws, rows, c);
+  long long* nbt = training ? num_batches_tracked : nullptr;
   if (dtype == RTSDS_BF16) {
-    if (c % 8 == 0) bn_fwd_launch<bf16, 8>(x, res, y, rows, c, gamma, beta, running_mean, running_var, save_mean, save_invstd, momentum, eps, training, act, stats_part, stats_nrb, part, scale, shift, st);
-    else bn_fwd_launch<bf16, 1>(x, res, y, rows, c, gamma, beta, running_mean, running_var, save_mean, save_invstd, momentum, eps, training, act, stats_part, stats_nrb, part, scale, shift, st);
+    if (c % 8 == 0) bn_fwd_launch<bf16, 8>(x, res, y, rows, c, gamma, beta, running_mean, running_var, save_mean, save_invstd, momentum, eps, training, act, stats_part, stats_nrb, nbt, w, st);
+    else bn_fwd_launch<bf16, 1>(x, res, y, rows, c, gamma, beta, running_mean, running_var, save_mean, save_invstd, momentum, eps, training, act, stats_part, stats_nrb, nbt, w, st);
   } else if (dtype == RTSDS_F32) {
-    if (c % 4 == 0) bn_fwd_launch<float, 4>(x, res, y, rows, c, gamma, beta, running_mean, running_var, save_mean, save_invstd, momentum, eps, training, act, stats_part, stats_nrb, part, scale, shift, st);
-    else bn_fwd_launch<float, 1>(x, res, y, rows, c, gamma, beta, running_mean, running_var, save_mean, save_invstd, momentum, eps, training, act, stats_part, stats_nrb, part, scale, shift, st);
+    if (c % 4 == 0) bn_fwd_launch<float, 4>(x, res, y, rows, c, gamma, beta, running_mean, running_var, save_mean, save_invstd, momentum, eps, training, act, stats_part, stats_nrb, nbt, w, st);
+    else bn_fwd_launch<float, 1>(x, res, y, rows, c, gamma, beta, running_mean, running_var, save_mean, save_invstd, momentum, eps, training, act, stats_part, stats_nrb, nbt, w, st);
   } else return RTSDS_ERR_UNSUPPORTED;
   return hipGetLastError() == hipSuccess ? RTSDS_OK : RTSDS_ERR_LAUNCH;
 }
 
 template <typename T, int VEC>
 static void bn_bwd_launch(const void* dy, const void* x, const void* y, void* dx, void* dres, float* dgamma, float* dbeta,
-                          long rows, int c, const float* gamma, const float* smean, const float* sinv, int training,
-                          int act, int accumulate, float* part, float* A, float* B, float* C, hipStream_t st) {
-  const int rb = bn_rb(rows, c, VEC);
-  hipLaunchKernelGGL((bn_bwd_stats_kernel<T, VEC>), dim3(rb, rt_cdiv(c, 256 * VEC)), dim3(256), 0, st, (const T*)dy, (const T*)x, (const T*)y, smean,
-                     part, rows, c, act);
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(c), dim3(64), 0, st, part, rb, c, rows, gamma, smean, sinv,
-                     dgamma, dbeta, A, B, C, training, accumulate);
+                          long rows, int c, const float* gamma, const float* beta, const float* smean, const float* sinv, int training,
+                          int act, int accumulate, const BnWs& w, hipStream_t st) {
+  int rb = bn_rb(rows, c, VEC);
+  float* part = w.part;
+  hipLaunchKernelGGL((bn_bwd_stats_kernel<T, VEC>), dim3(rb, rt_cdiv(c, 256 * VEC)), dim3(256), 0, st, (const T*)dy, (const T*)x, (const T*)y, gamma, beta,
+                     smean, sinv, part, rows, c, act);
+  const float* mp = bn_premerge<2>(part, rb, c, w.merged, st);
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(c), dim3(64), 0, st, mp, rb, c, rows, gamma, beta, smean, sinv,
+                     dgamma, dbeta, w.coef, training, accumulate);
   if (dx || dres) {
-    const long total = rows * ((c + VEC - 1) / VEC);
-    const int blocks = (int)std::min<long>(8192, (total + 255) / 256);
-    hipLaunchKernelGGL((bn_bwd_apply_kernel<T, VEC>), dim3(blocks), dim3(256), 0, st, (const T*)dy, (const T*)x, (const T*)y,
-                       (T*)dx, (T*)dres, smean, A, B, C, rows, c, act);
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<T, VEC>), dim3(bn_apply_rb(rows, c, VEC), rt_cdiv(c, 256 * VEC)), dim3(256), 0, st,
+                       (const T*)dy, (const T*)x, (const T*)y, (T*)dx, (T*)dres, w.coef, rows, c, act);
   }
 }
 
 extern "C" int rtsds_bn_bwd(const void* dy, const void* x, const void* y, void* dx, void* dres, float* dgamma, float* dbeta,
-                            long rows, int c, const float* gamma, const float* save_mean, const float* save_invstd,
-                            int training, int act, int accumulate_params, int dtype, void* ws, size_t ws_bytes, void* stream) {
+                            long rows, int c, const float* gamma, const float* beta, const float* save_mean,
+                            const float* save_invstd, int training, int act, int accumulate_params, int dtype, void* ws,
+                            size_t ws_bytes, void* stream) {
   if (rows <= 0 || c <= 0) return RTSDS_ERR_SHAPE;
   if (ws_bytes < rtsds_bn_workspace(rows, c)) return RTSDS_ERR_WORKSPACE;
-  if (act && !y) return RTSDS_ERR_UNSUPPORTED;
+  if (!y && !(act == RTSDS_ACT_NONE || act == RTSDS_ACT_RELU || act == RTSDS_ACT_LEAKY)) return RTSDS_ERR_UNSUPPORTED;
+  if (!y && act && dres) return RTSDS_ERR_UNSUPPORTED;  // residual: the mask needs y
   hipStream_t st = (hipStream_t)stream;
-  float* part = (float*)ws;
-  float* A = part + (size_t)kBnMaxRB * c * 3;
-  float* B = A + c;
-  float* C = B + c;
+  const BnWs w = bn_ws(ws, rows, c);
   if (dtype == RTSDS_BF16) {
-    if (c % 8 == 0) bn_bwd_launch<bf16, 8>(dy, x, y, dx, dres, dgamma, dbeta, rows, c, gamma, save_mean, save_invstd, training, act, accumulate_params, part, A, B, C, st);
-    else bn_bwd_launch<bf16, 1>(dy, x, y, dx, dres, dgamma, dbeta, rows, c, gamma, save_mean, save_invstd, training, act, accumulate_params, part, A, B, C, st);
+    if (c % 8 == 0) bn_bwd_launch<bf16, 8>(dy, x, y, dx, dres, dgamma, dbeta, rows, c, gamma, beta, save_mean, save_invstd, training, act, accumulate_params, w, st);
+    else bn_bwd_launch<bf16, 1>(dy, x, y, dx, dres, dgamma, dbeta, rows, c, gamma, beta, save_mean, save_invstd, training, act, accumulate_params, w, st);
   } else if (dtype == RTSDS_F32) {
-    if (c % 4 == 0) bn_bwd_launch<float, 4>(dy, x, y, dx, dres, dgamma, dbeta, rows, c, gamma, save_mean, save_invstd, training, act, accumulate_params, part, A, B, C, st);
-    else bn_bwd_launch<float, 1>(dy, x, y, dx, dres, dgamma, dbeta, rows, c, gamma, save_mean, save_invstd, training, act, accumulate_params, part, A, B, C, st);
+    if (c % 4 == 0) bn_bwd_launch<float, 4>(dy, x, y, dx, dres, dgamma, dbeta, rows, c, gamma, beta, save_mean, save_invstd, training, act, accumulate_params, w, st);
+    else bn_bwd_launch<float, 1>(dy, x, y, dx, dres, dgamma, dbeta, rows, c, gamma, beta, save_mean, save_invstd, training, act, accumulate_params, w, st);
   } else return RTSDS_ERR_UNSUPPORTED;
   return hipGetLastError() == hipSuccess ? RTSDS_OK : RTSDS_ERR_LAUNCH;
 }

@@ -10,7 +10,7 @@ import ctypes
 import numpy as np
 import torch
 
-from ._lib import ConvDesc, lib
+from ._lib import ACT_SIGMOID, ConvDesc, lib
 from .runtime import CL, dcode, empty_nhwc, nhwc, require_hip, stream, workspace
 
 _P = lambda t: None if t is None else t.data_ptr()  # noqa: E731
@@ -228,7 +228,7 @@ class BatchNormFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, gamma, beta, res, running_mean, running_var, training, momentum, eps, act,
-                stats, stats_nrb):
+                stats, stats_nrb, nbt):
         require_hip(x)
         x = nhwc(x)
         if res is not None:
@@ -240,17 +240,20 @@ class BatchNormFn(torch.autograd.Function):
         si = torch.empty(c, dtype=torch.float32, device=x.device)
         ws = workspace(lib.rtsds_bn_workspace(rows, c), x.device)
         lib.rtsds_bn_fwd(_P(x), _P(res), _P(y), rows, c, _P(gamma), _P(beta), _P(running_mean),
-                         _P(running_var), _P(sm), _P(si), float(momentum), float(eps), int(training),
+                         _P(running_var), _P(nbt), _P(sm), _P(si), float(momentum), float(eps), int(training),
                          act, _P(stats) if training else None, int(stats_nrb or 0), dcode(x), _P(ws),
                          ws.numel(), stream())
         ctx.meta = (rows, c, int(training), act, res is not None)
         ctx.gamma, ctx.beta = gamma, beta
-        ctx.save_for_backward(x, y, gamma, sm, si)
+        # Without a residual the ReLU/LeakyReLU mask is recomputed from x in the backward
+        # (bit-identical pre-activation), so y is neither kept nor re-read.
+        keep_y = res is not None or act == ACT_SIGMOID
+        ctx.save_for_backward(x, y if keep_y else None, gamma, beta, sm, si)
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, y, gamma, sm, si = ctx.saved_tensors
+        x, y, gamma, beta, sm, si = ctx.saved_tensors
         rows, c, training, act, has_res = ctx.meta
         dy = nhwc(dy)
         need_dx, need_g, need_b, need_r = (ctx.needs_input_grad[0], ctx.needs_input_grad[1],
@@ -266,19 +269,20 @@ class BatchNormFn(torch.autograd.Function):
             acc = 0
         ws = workspace(lib.rtsds_bn_workspace(rows, c), x.device)
         lib.rtsds_bn_bwd(_P(dy), _P(x), _P(y), _P(dx), _P(dres), _P(dg), _P(db), rows, c,
-                         _P(gamma), _P(sm), _P(si), training, act, acc, dcode(x), _P(ws), ws.numel(),
+                         _P(gamma), _P(beta), _P(sm), _P(si), training, act, acc, dcode(x), _P(ws), ws.numel(),
                          stream())
         if acc:
             dg = db = None
-        return dx, dg, db, dres, None, None, None, None, None, None, None, None
+        return dx, dg, db, dres, None, None, None, None, None, None, None, None, None
 
 
 def batch_norm(x, gamma, beta, running_mean, running_var, training, momentum, eps, act=0,
-               residual=None):
+               residual=None, num_batches_tracked=None):
+    """``num_batches_tracked`` (int64, optional) is incremented by the finalize kernel."""
     st = getattr(x, "_rt_bn_stats", None) if training else None
     stats, nrb = st if st is not None else (None, None)
     return BatchNormFn.apply(x, gamma, beta, residual, running_mean, running_var, training,
-                             momentum, eps, act, stats, nrb)
+                             momentum, eps, act, stats, nrb, num_batches_tracked)
 
 
 # ----------------------------------------------------------------------------- layout / dtype

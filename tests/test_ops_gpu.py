@@ -114,7 +114,8 @@ def test_conv_fused_act(dt, act):
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("shape,act,res", [((4, 64, 8, 12), 1, False), ((2, 128, 5, 7), 1, True),
                                            ((8, 512, 1, 1), 3, False), ((2, 19, 9, 9), 1, False),
-                                           ((3, 2048, 3, 3), 0, True)])
+                                           ((3, 2048, 3, 3), 0, True), ((2, 24, 7, 9), 2, False),
+                                           ((8, 64, 48, 64), 1, False), ((4, 32, 40, 40), 2, True)])
 def test_batchnorm_train(shape, act, res, dt):
     g = torch.Generator().manual_seed(11)
     x = torch.randn(shape, generator=g, dtype=torch.float64) * 3 + 50  # large mean
@@ -132,7 +133,7 @@ def test_batchnorm_train(shape, act, res, dt):
     yr = TF.batch_norm(xr, rm, rv, gr, br, True, 0.1, 1e-5)
     if res:
         yr = yr + rr
-    yr = [yr, TF.relu(yr), None, torch.sigmoid(yr)][act]
+    yr = [yr, TF.relu(yr), TF.leaky_relu(yr, 0.2), torch.sigmoid(yr)][act]
     gy = torch.randn(shape, generator=g, dtype=torch.float64)
     yr.backward(gy)
 
@@ -162,10 +163,28 @@ def test_batchnorm_eval(dt):
     gam, bet = torch.randn(64, generator=g, dtype=torch.float64), torch.randn(64, generator=g, dtype=torch.float64)
     if dt == torch.bfloat16:
         x = x.bfloat16().double()
-    yr = TF.relu(TF.batch_norm(x, rm, rv, gam, bet, False, 0.1, 1e-5))
-    y = F.batch_norm(_dev(x, dt), gam.float().to(DEV), bet.float().to(DEV), rm.float().to(DEV),
+    xr = x.clone().requires_grad_()
+    yr = TF.relu(TF.batch_norm(xr, rm, rv, gam, bet, False, 0.1, 1e-5))
+    gy = torch.randn(x.shape, generator=g, dtype=torch.float64)
+    yr.backward(gy)
+    xd = _dev(x, dt).requires_grad_()
+    y = F.batch_norm(xd, gam.float().to(DEV), bet.float().to(DEV), rm.float().to(DEV),
                      rv.float().to(DEV), False, 0.1, 1e-5, 1, None)
+    y.backward(_dev(gy, dt))
     _close(y, yr, dt, "y", 1e-4 if dt == torch.float32 else None)
+    _close(xd.grad, xr.grad, dt, "dx", 1e-4 if dt == torch.float32 else None)
+
+
+def test_batchnorm_module_counter():
+    """num_batches_tracked is advanced by the finalize kernel in train mode only."""
+    from rtsds_amd import nn as rnn
+    bn = rnn.BatchNorm2d(16).to(DEV)
+    x = torch.randn(2, 16, 4, 4, device=DEV).contiguous(memory_format=torch.channels_last)
+    for _ in range(3):
+        bn(x, act="relu")
+    bn.eval()
+    bn(x)
+    assert int(bn.num_batches_tracked) == 3
 
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
