@@ -188,6 +188,29 @@ int rtsds_argmax(const void* x, long sn, long sc, long shw, int64_t* out, const 
 int rtsds_confusion(const int64_t* label, const int64_t* pred, unsigned long long* hist, long total,
                     int nc, void* stream);
 
+/* ---------------------------------------------------------------- fused upsample + CE
+ * Replaces, for nheads (<= 4) low-resolution NHWC logit maps of the same geometry
+ * [n][hl][wl][c] (c <= 32), the chain F.interpolate(bilinear, align_corners=False) to
+ * [n][c][H][W] -> nn.CrossEntropyLoss(ignore_index) per head -> (head 0) argmax == target
+ * pixel count: build_bisenet.py:151-152,158-159,166, deeplabv2.py:126, train.py:86-106.
+ * logits / dlogits: host arrays of nheads device pointers.  scale_h/w: ATen source scales
+ * (in/out for size=, 1/scale_factor for scale_factor=; upsampling only, <= 1).
+ * Forward writes loss[nheads] (mean over non-ignored pixels; may be NULL) and *loss_sum (their
+ * sum in head order; may be NULL), adds the head-0 argmax matches to *correct (may be NULL)
+ * and, when want_grad, keeps unscaled low-res gradient partials in ws.  Backward:
+ * dlogits[h] = grad_loss[h * grad_stride] * d loss[h] / d logits[h] from those partials (ws
+ * must be the forward's; grad_stride 0 = one upstream gradient for loss_sum).  Full-resolution logits are never materialised.  workspace()
+ * returns 0 for geometries the fused path does not cover.                                 */
+size_t rtsds_upce_workspace(int nheads, int n, int hl, int wl, int c, int H, int W, float scale_h,
+                            float scale_w);
+int rtsds_upce_fwd(int nheads, const void* const* logits, const int64_t* target, int n, int hl,
+                   int wl, int c, int H, int W, float scale_h, float scale_w, int ignore_index,
+                   float* loss, float* loss_sum, unsigned long long* correct, int want_grad,
+                   int dtype, void* ws, size_t ws_bytes, void* stream);
+int rtsds_upce_bwd(int nheads, const float* grad_loss, int grad_stride, void* const* dlogits,
+                   int n, int hl, int wl, int c, int H, int W, float scale_h, float scale_w,
+                   int dtype, const void* ws, size_t ws_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -55,6 +55,30 @@ RT_DEV float wave_max(float v) {
   return v;
 }
 
+// Bilinear (align_corners=False) source index, ATen semantics: src = scale*(dst+0.5)-0.5
+// clamped at 0; i0 = floor, i1 = min(i0+1, in-1); l0/l1 the weights of i0/i1.  scale = in/out
+// for size=..., 1/scale_factor for scale_factor=... (computed by the host in fp32 exactly as
+// ATen's area_pixel_compute_scale does).  Shared by the resize kernels and the fused
+// upsample+cross-entropy so both see identical taps and weights.
+RT_DEV void bil_src(int o, float scale, int in, int& i0, int& i1, float& l0, float& l1) {
+  float src = scale * ((float)o + 0.5f) - 0.5f;
+  if (src < 0.f) src = 0.f;
+  i0 = (int)src;
+  if (i0 > in - 1) i0 = in - 1;
+  i1 = i0 + (i0 < in - 1 ? 1 : 0);
+  l1 = src - (float)i0;
+  l0 = 1.f - l1;
+}
+
+// Blend of the 4 taps (p00 = (h0,w0), p01 = (h0,w1), p10 = (h1,w0), p11 = (h1,w1)): vertical
+// first, explicit fma order -- the fused upsample+CE computes the identical expression from
+// per-row vertical blends, so both paths produce the same logits bit for bit.
+RT_DEV float bil_mix(float p00, float p01, float p10, float p11, float lh0, float lh1, float lw0, float lw1) {
+  const float v0 = fmaf(lh1, p10, lh0 * p00);
+  const float v1 = fmaf(lh1, p11, lh0 * p01);
+  return fmaf(lw1, v1, lw0 * v0);
+}
+
 #define RT_CHECK_LAUNCH()                                      \
   do {                                                          \
     if (hipPeekAtLastError() != hipSuccess) return RTSDS_ERR_LAUNCH; \

@@ -408,18 +408,7 @@ extern "C" int rtsds_chscale_bwd(const void* dy, const void* x, const void* a, v
 }
 
 // ------------------------------------------------------------------ bilinear (align_corners=False)
-// ATen's source index: src = scale*(dst+0.5)-0.5 clamped at 0; i0 = floor, i1 = min(i0+1, in-1).
-// scale = in/out for size=..., 1/scale_factor for scale_factor=... (both computed by the host
-// in fp32 exactly as ATen's area_pixel_compute_scale does).
-RT_DEV void bil_src(int o, float scale, int in, int& i0, int& i1, float& l0, float& l1) {
-  float src = scale * ((float)o + 0.5f) - 0.5f;
-  if (src < 0.f) src = 0.f;
-  i0 = (int)src;
-  if (i0 > in - 1) i0 = in - 1;
-  i1 = i0 + (i0 < in - 1 ? 1 : 0);
-  l1 = src - (float)i0;
-  l0 = 1.f - l1;
-}
+// bil_src (ATen source index, align_corners=False): common.h
 // Forward: one thread per (output pixel, channel chunk of CH); the 4 taps and weights are
 // computed once per chunk.  CH = 16-B vector when the channel layout allows it, else the whole
 // pixel (c <= 64, e.g. the 19-class heads) or single channels.
@@ -453,12 +442,12 @@ __global__ void bilinear_fwd_kernel(const T* __restrict__ x, T* __restrict__ y, 
       V16 r;
 #pragma unroll
       for (int j = 0; j < V; ++j)
-        r[j] = from_f<T>(lh0 * (lw0 * to_f(a[j]) + lw1 * to_f(bb[j])) + lh1 * (lw0 * to_f(cc[j]) + lw1 * to_f(dd[j])));
+        r[j] = from_f<T>(bil_mix(to_f(a[j]), to_f(bb[j]), to_f(cc[j]), to_f(dd[j]), lh0, lh1, lw0, lw1));
       *(V16*)(o + c0) = r;
     } else {
       const int cs = MODE == 1 ? 0 : chunk, ce = MODE == 1 ? c : chunk + 1;
       for (int ch = cs; ch < ce; ++ch)
-        o[ch] = from_f<T>(lh0 * (lw0 * to_f(p00[ch]) + lw1 * to_f(p01[ch])) + lh1 * (lw0 * to_f(p10[ch]) + lw1 * to_f(p11[ch])));
+        o[ch] = from_f<T>(bil_mix(to_f(p00[ch]), to_f(p01[ch]), to_f(p10[ch]), to_f(p11[ch]), lh0, lh1, lw0, lw1));
     }
   }
 }

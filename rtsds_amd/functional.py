@@ -620,6 +620,90 @@ def cross_entropy(x, target, ignore_index=-100):
     return CrossEntropyFn.apply(x, target, ignore_index)
 
 
+class UpsampleCrossEntropyFn(torch.autograd.Function):
+    """sum_h CrossEntropy(interpolate_bilinear(head_h, (H, W)), target) without materialising
+    the full-resolution logits (rtsds_upce_*; the chain it replaces is cited in the header).
+    Also adds head 0's argmax==target pixel count into ``correct`` when given."""
+
+    @staticmethod
+    def forward(ctx, target, geo, ignore_index, correct, *heads):
+        n, c, hl, wl, H, W, sh, sw = geo
+        xs = [nhwc(h) for h in heads]
+        k = len(xs)
+        dt = dcode(xs[0])
+        nbytes = lib.rtsds_upce_workspace(k, n, hl, wl, c, H, W, sh, sw)
+        ws = workspace(nbytes, xs[0].device)
+        ptrs = (ctypes.c_void_p * k)(*[x.data_ptr() for x in xs])
+        per_head = torch.empty(k, dtype=torch.float32, device=xs[0].device)
+        total = torch.empty((), dtype=torch.float32, device=xs[0].device)
+        want = any(ctx.needs_input_grad[4:])
+        lib.rtsds_upce_fwd(k, ptrs, _P(target), n, hl, wl, c, H, W, sh, sw, ignore_index, _P(per_head),
+                           _P(total), _P(correct), int(want), dt, _P(ws), ws.numel(), stream())
+        ctx.geo, ctx.k, ctx.dt, ctx.dtype = geo, k, dt, xs[0].dtype
+        ctx.ws = ws
+        ctx.per_head = per_head
+        return total
+
+    @staticmethod
+    def backward(ctx, g):
+        n, c, hl, wl, H, W, sh, sw = ctx.geo
+        ws = ctx.ws
+        dxs = [empty_nhwc(n, c, hl, wl, ctx.dtype, ws.device) for _ in range(ctx.k)]
+        ptrs = (ctypes.c_void_p * ctx.k)(*[d.data_ptr() for d in dxs])
+        g = g.contiguous().float()
+        lib.rtsds_upce_bwd(ctx.k, _P(g), 0, ptrs, n, hl, wl, c, H, W, sh, sw, ctx.dt, _P(ws), ws.numel(),
+                           stream())
+        ctx.ws = None
+        return (None, None, None, None, *dxs)
+
+
+def interpolate_geometry(x, geo):
+    """interpolate_bilinear with a precomputed upsample_geometry()."""
+    ho, wo, sh, sw = geo
+    return BilinearFn.apply(x, ho, wo, sh, sw)
+
+
+def upsample_geometry(x, size=None, scale_factor=None):
+    """(H, W, scale_h, scale_w) of interpolate_bilinear(x, size | scale_factor)."""
+    hi, wi = x.shape[-2:]
+    if size is not None:
+        ho, wo = int(size[0]), int(size[1])
+        return ho, wo, _src_scale(hi, ho, None), _src_scale(wi, wo, None)
+    ho, wo = int(np.floor(hi * scale_factor)), int(np.floor(wi * scale_factor))
+    s = _src_scale(hi, ho, scale_factor)
+    return ho, wo, s, s
+
+
+def upsample_cross_entropy_supported(heads, geo, ignore_index):
+    h0 = heads[0]
+    n, c, hl, wl = h0.shape
+    ho, wo, sh, sw = geo
+    if len(heads) > 4 or any(tuple(h.shape) != tuple(h0.shape) or h.dtype != h0.dtype for h in heads):
+        return False
+    return lib.rtsds_upce_workspace(len(heads), n, hl, wl, c, ho, wo, sh, sw) > 0
+
+
+def upsample_cross_entropy(heads, target, geo, ignore_index=-100, correct=None):
+    """Sum over heads (in order) of cross_entropy(interpolate_bilinear(head, ...), target),
+    fused; ``geo`` from upsample_geometry().  ``correct``: optional int64 device counter that
+    receives head 0's pixel-accuracy matches.  Returns (total_loss, per_head_losses)."""
+    require_hip(target, *heads)
+    t = target.squeeze(1) if target.dim() == 4 else target
+    t = t.contiguous()
+    if t.dtype != torch.int64:
+        t = t.long()
+    n, c, hl, wl = heads[0].shape
+    ho, wo, sh, sw = geo
+    if tuple(t.shape) != (n, ho, wo):
+        raise RuntimeError(f"rtsds_amd: target shape {tuple(t.shape)} != {(n, ho, wo)}")
+    if not upsample_cross_entropy_supported(heads, geo, ignore_index):
+        raise RuntimeError("rtsds_amd: fused upsample+CE does not cover this geometry")
+    full = (n, c, hl, wl, ho, wo, sh, sw)
+    fn = UpsampleCrossEntropyFn
+    total = fn.apply(t, full, int(ignore_index), correct, *heads)
+    return total
+
+
 class BCEWithLogitsFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, target):

@@ -122,7 +122,10 @@ class BiSeNet(torch.nn.Module):
                 nn.init.constant_(m.weight, 1)
                 nn.init.constant_(m.bias, 0)
 
-    def forward(self, input):
+    def _heads(self, input):
+        """Everything up to the final resizes: [(low-res logits, resize geometry), ...] --
+        the main head (conv before up8, see below) then, in training, the two supervision
+        heads (build_bisenet.py:151-166)."""
         x = to_input(input)
         sx = self.saptial_path(x)
         f3, f4, tail = self.context_path(x)
@@ -131,17 +134,33 @@ class BiSeNet(torch.nn.Module):
         hw = sx.shape[-2:]
         cx1 = F.interpolate_bilinear(cx1, size=hw)
         cx2 = F.interpolate_bilinear(cx2, size=hw)
+        heads = []
         if self.training:
             full = input.shape[-2:]
-            cx1_sup = F.interpolate_bilinear(self.supervision1(cx1), size=full)
-            cx2_sup = F.interpolate_bilinear(self.supervision2(cx2), size=full)
+            s1, s2 = self.supervision1(cx1), self.supervision2(cx2)
+            aux = [(s1, F.upsample_geometry(s1, size=full)), (s2, F.upsample_geometry(s2, size=full))]
         result = self.feature_fusion_module(sx, F.cat([cx1, cx2]))
         if self.with_interpolation:
             # reference: conv(up8(result)) (build_bisenet.py:165-167).  A 1x1 conv mixes channels
             # per pixel and bilinear resize mixes pixels per channel with weights summing to 1,
             # so up8(conv(result)) is the same function (bias included) at 1/64 of the conv work
             # and without the full-resolution intermediate.
-            result = F.interpolate_bilinear(self.conv(result), scale_factor=8)
+            main = self.conv(result)
+            heads.append((main, F.upsample_geometry(main, scale_factor=8)))
+        else:
+            heads.append((result, None))
         if self.training:
-            return result, cx1_sup, cx2_sup
-        return result
+            heads += aux
+        return heads
+
+    def forward_lowres(self, input):
+        """Training-loop entry used by rtsds_amd.train: the heads before their final bilinear
+        resize, so the resize can be fused into the loss (functional.upsample_cross_entropy).
+        forward() is exactly these heads, resized."""
+        return self._heads(input)
+
+    def forward(self, input):
+        outs = [t if geo is None else F.interpolate_geometry(t, geo) for t, geo in self._heads(input)]
+        if self.training:
+            return tuple(outs)
+        return outs[0]

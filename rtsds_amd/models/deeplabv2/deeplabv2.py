@@ -99,13 +99,19 @@ class ResNetMulti(nn.Module):
             layers.append(block(self.inplanes, planes, dilation=dilation))
         return nn.Sequential(*layers)
 
-    def forward(self, x):
+    def forward_lowres(self, x):
+        """[(stride-8 logits, resize geometry)] -- forward() before its final bilinear resize
+        (deeplabv2.py:126), so the training loop can fuse the resize into the loss."""
         _, _, H, W = x.size()
         t = to_input(x)
         t = self.maxpool(conv_bn(self.conv1, self.bn1, t, "relu"))
         t = self.layer4(self.layer3(self.layer2(self.layer1(t))))
         t = self.layer6(t)
-        t = F.interpolate_bilinear(t, size=(H, W))
+        return [(t, F.upsample_geometry(t, size=(H, W)))]
+
+    def forward(self, x):
+        (t, geo), = self.forward_lowres(x)
+        t = F.interpolate_geometry(t, geo)
         if self.training == True:  # noqa: E712  (reference contract, deeplabv2.py:128)
             return t, None, None
         return t

@@ -9,7 +9,7 @@ instead of the reference's 6-9 separate syncs; the logged values are identical.
 import torch
 
 from . import functional as F
-from . import utils
+from . import losses, utils
 from .callbacks import Callback
 from .validation import val_GTA5
 
@@ -26,12 +26,43 @@ def _unpack(outputs):
     return outputs, None, None
 
 
+def _fused_heads(model, criterion, inputs):
+    """Low-res heads + shared resize geometry when the final resizes can be fused into the
+    cross-entropy (the model exposes forward_lowres, the criterion is the unweighted-mean CE,
+    all heads share one upsample geometry), else None."""
+    if not (isinstance(criterion, losses.CrossEntropyLoss) and hasattr(model, "forward_lowres")):
+        return None
+    heads = model.forward_lowres(inputs)
+    geos = {geo for _, geo in heads}
+    if len(geos) != 1 or None in geos:
+        return [F.interpolate_geometry(t, geo) if geo is not None else t for t, geo in heads], None
+    geo = geos.pop()
+    ts = [t for t, _ in heads]
+    if not F.upsample_cross_entropy_supported(ts, geo, criterion.ignore_index):
+        return [F.interpolate_geometry(t, geo) for t in ts], None
+    return ts, geo
+
+
 def seg_step(model, criterion, optimizer, inputs, targets):
     """One train.train iteration body: zero_grad, forward, CE(main)+CE(aux1)+CE(aux2),
     backward, optimizer step, device-side pixel-accuracy count.  Returns device tensors
-    (loss, correct) -- no host sync."""
+    (loss, correct) -- no host sync.  When the model exposes its pre-resize heads, the
+    bilinear resizes, the three cross-entropies and the accuracy argmax run as one fused
+    kernel (functional.upsample_cross_entropy) -- same losses and gradients, no
+    full-resolution logits."""
     optimizer.zero_grad()
-    main_output, aux1, aux2 = _unpack(model(inputs))
+    fused = _fused_heads(model, criterion, inputs)
+    if fused is not None and fused[1] is not None:
+        correct = torch.zeros(1, dtype=torch.int64, device=fused[0][0].device)
+        loss = F.upsample_cross_entropy(fused[0], targets, fused[1], criterion.ignore_index, correct)
+        loss.backward()
+        optimizer.step()
+        return loss.detach(), correct
+    if fused is not None:
+        outs = list(fused[0]) + [None] * (3 - len(fused[0]))
+        main_output, aux1, aux2 = outs[:3]
+    else:
+        main_output, aux1, aux2 = _unpack(model(inputs))
     loss = criterion(main_output, targets)
     if aux1 is not None:
         loss = loss + criterion(aux1, targets)

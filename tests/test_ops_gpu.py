@@ -284,6 +284,71 @@ def test_softmax_ce_argmax(dt):
     assert int(correct.item()) == int((ref == t).sum())
 
 
+def _upce_reference(heads, t, geo_args, ignore):
+    """fp64 torch: sum_h CE(interpolate(head_h)), grads, and head-0 argmax matches."""
+    hr = [h.clone().requires_grad_() for h in heads]
+    ups = [TF.interpolate(h, mode="bilinear", align_corners=False, **geo_args) for h in hr]
+    loss = None
+    for u in ups:
+        l = TF.cross_entropy(u, t, ignore_index=ignore)
+        loss = l if loss is None else loss + l
+    loss.backward()
+    return loss.detach(), [h.grad for h in hr], int((ups[0].detach().argmax(1) == t).sum()), ups[0].detach()
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("case", [
+    (2, 19, 8, 16, {"scale_factor": 8}, 3),          # BiSeNet heads, x8 (scale_factor form)
+    (2, 19, 8, 16, {"size": (64, 128)}, 3),          # size form (aux heads)
+    (1, 19, 13, 17, {"size": (97, 129)}, 2),         # non-integer scale, ragged tiles
+    (2, 5, 7, 9, {"scale_factor": 4}, 1),            # other factor, few classes
+    (1, 19, 9, 33, {"size": (72, 264)}, 1),          # several column tiles
+])
+def test_upsample_cross_entropy_fused(case, dt):
+    """Fused resize+CE+accuracy (rtsds_upce_*) vs torch fp64 interpolate -> CrossEntropyLoss."""
+    n, c, hl, wl, geo_args, k = case
+    g = torch.Generator().manual_seed(21)
+    heads = [torch.randn(n, c, hl, wl, generator=g, dtype=torch.float64) * 2 for _ in range(k)]
+    if dt == torch.bfloat16:
+        heads = [h.bfloat16().double() for h in heads]
+    hd = [_dev(h, dt).requires_grad_() for h in heads]
+    geo = F.upsample_geometry(hd[0], **geo_args)
+    H, W = geo[0], geo[1]
+    t = torch.randint(0, c + 1, (n, H, W), generator=g)
+    t[t == c] = 255  # ignore label
+    lr, gr, corr_r, up0 = _upce_reference(heads, t, geo_args, 255)
+    assert F.upsample_cross_entropy_supported(hd, geo, 255)
+    correct = torch.zeros(1, dtype=torch.int64, device=DEV)
+    loss = F.upsample_cross_entropy(hd, t.to(DEV), geo, 255, correct)
+    loss.backward(torch.tensor(1.5, device=DEV))
+    _close(loss, lr, torch.float32, "loss", 1e-5 if dt == torch.float32 else 1e-4)
+    for i in range(k):
+        _close(hd[i].grad, gr[i] * 1.5, dt, f"dhead{i}", 1e-4 if dt == torch.float32 else 2e-2)
+    # accuracy: exact against fp64 except pixels whose top-2 logits tie within fp32 noise
+    top2 = up0.topk(2, dim=1).values
+    near = int(((top2[:, 0] - top2[:, 1]) < 1e-4).sum())
+    assert abs(int(correct.item()) - corr_r) <= near
+    if dt == torch.float32:  # bit-identical to the unfused HIP chain (same taps/weights/expression)
+        up = F.interpolate_geometry(_dev(heads[0], dt), geo)
+        c2 = torch.zeros(1, dtype=torch.int64, device=DEV)
+        F.argmax_channels(up, t.to(DEV), c2, want_map=False)
+        assert int(c2.item()) == int(correct.item())
+
+
+def test_upsample_cross_entropy_no_grad_and_fallback():
+    x = _dev(torch.randn(2, 19, 8, 16), torch.float32)
+    geo = F.upsample_geometry(x, scale_factor=8)
+    t = torch.randint(0, 20, (2, 64, 128), device=DEV)
+    with torch.no_grad():
+        l = F.upsample_cross_entropy([x], t, geo, 19)
+    ref = F.cross_entropy(F.interpolate_geometry(x, geo), t, 19)
+    _close(l, ref, torch.float32, "loss", 1e-5)
+    # downsampling and > 32 classes are outside the fused path
+    assert not F.upsample_cross_entropy_supported([x], F.upsample_geometry(x, size=(4, 8)), 19)
+    big = _dev(torch.randn(1, 40, 8, 8), torch.float32)
+    assert not F.upsample_cross_entropy_supported([big], F.upsample_geometry(big, scale_factor=8), 19)
+
+
 def test_bce():
     g = torch.Generator().manual_seed(6)
     x = torch.randn(8, 1, 1, 1, generator=g, dtype=torch.float64) * 4
