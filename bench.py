@@ -142,6 +142,10 @@ def main():
         rows.sort(reverse=True)
         for r in rows:
             print(f"{r[0]*1000:8.1f} us  {r[1]:5s} {r[2]:45s} {r[3]:7.2f} GF {r[4]:7.1f} TF/s", file=sys.stderr)
+        for tag in ("fwd", "dgrad", "wgrad"):
+            sel = [r for r in rows if r[1] == tag]
+            print(f"total {tag:5s} {sum(r[0] for r in sel):8.3f} ms over {len(sel)} convs", file=sys.stderr)
+        print(f"total conv  {conv_ms:8.3f} ms, {conv_flop / 1e9:.1f} GF", file=sys.stderr)
     achieved = conv_flop / (conv_ms * 1e-3) / 1e12
 
     # ---- inference FPS (eval forward, no grad)

@@ -15,6 +15,7 @@
 // v_mfma_f32_16x16x4_f32 (exact f32 FMA chain).
 #include "common.h"
 #include <algorithm>
+#include <cstdlib>
 
 enum { MODE_FWD = 0, MODE_DGRAD = 1, MODE_WGRAD = 2 };
 
@@ -86,6 +87,24 @@ RT_DEV float frag_rc(const float* s, int pitch, int col0, int ks, int lane) {
   return s[(ks * 4 + (lane >> 4)) * pitch + col0 + (lane & 15)];
 }
 
+// GL (global_load_lds) staging: the KC tile [rows][64] bf16 is written lane-linearly by the
+// LDS-DMA (one wave-instruction = 8 rows of 128 B), so its bank swizzle is applied to the
+// per-lane SOURCE chunk and undone on the read: row r keeps logical 16-B chunk c at physical
+// slot c ^ ((r >> 1) & 7).  For the KC fragment read (lanes 0-15 rows at chunk c, 16-31 at
+// c+1, ...) every ds_read_b128 lane group then covers 16 distinct 16-B bank slots.
+RT_DEV int gl_swz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
+RT_DEV bf16x8 frag_kc_gl(const bf16* s, int row0, int ks, int lane) {
+  const int row = row0 + (lane & 15);
+  return *(const bf16x8*)(s + row * 64 + gl_swz(row, ks * 4 + (lane >> 4)) * 8);
+}
+// 16 zero bytes: the DMA source of padding / out-of-range gathers.
+__device__ __attribute__((aligned(16))) bf16 g_conv_zero[8];
+template <int N> RT_DEV void wait_vmcnt() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+RT_DEV void gl_barrier() {
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
 template <typename T> RT_DEV typename VecT<T>::v16 vzero() {
   typename VecT<T>::v16 z;
 #pragma unroll
@@ -99,12 +118,18 @@ template <typename T> RT_DEV typename VecT<T>::v16 vzero() {
 //         never straddle a tap), 0 = scalar gather.
 //   KC B: 1 = K % V == 0 (vector rows), 0 = scalar.
 //   RC A/B: 1 = channel count % V == 0, 0 = scalar.
-template <typename T, int MODE, int BM, int BN, int BK, int WM, int WN, int ALA, int ALB>
+//   GL: 1 = stage A and B with global_load_lds (bf16 FWD/DGRAD, BK = 64, ALA = 2) into the
+//       swizzled unpadded image above, the next K-tile's DMA in flight across the barrier
+//       (counted vmcnt, raw s_barrier); 0 = register-staged double buffer.
+template <typename T, int MODE, int BM, int BN, int BK, int WM, int WN, int ALA, int ALB, int GL>
 __global__ void __launch_bounds__(256) conv_gemm_kernel(const ConvArgs P) {
   typedef typename VecT<T>::v16 V16;
   constexpr int V = VecT<T>::N;
   constexpr bool RC = (MODE == MODE_WGRAD);
-  constexpr int KCP = KCPitch<T, BK>::v;
+  constexpr bool G = GL != 0;
+  static_assert(!G || (sizeof(T) == 2 && MODE != MODE_WGRAD && BK == 64 && ALA == 2 && ALB == 1 && BM % 32 == 0 &&
+                       BN % 32 == 0), "GL staging");
+  constexpr int KCP = G ? BK : KCPitch<T, BK>::v;
   constexpr int PA = RC ? RCPitch<BM>::v : KCP;
   constexpr int PB = RC ? RCPitch<BN>::v : KCP;
   constexpr int A_EL = RC ? BK * PA : BM * PA;
@@ -341,6 +366,54 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(const ConvArgs P) {
     }
   };
 
+  // ---- GL: global -> LDS DMA of K-tile kt into buffer buf (NA + NB instructions per thread)
+  auto gl_issue = [&](int kt, int buf) {
+    if constexpr (G) {
+      typedef __attribute__((address_space(3))) void* lds_t;
+      typedef const __attribute__((address_space(1))) void* glb_t;
+      const int k0 = kt * BK;
+      T* sa = smem + buf * (A_EL + B_EL);
+      T* sb = sa + A_EL;
+      const int Cr = (MODE == MODE_FWD) ? P.c : P.k;
+      const int tap_u = k0 / Cr, ci_u = k0 - tap_u * Cr;
+      int r_u, s_u;
+      if (MODE == MODE_FWD) {
+        r_u = tap_u / P.kw;
+        s_u = tap_u - r_u * P.kw;
+      } else {
+        const int rr = tap_u / P.tkw;
+        r_u = P.r0h + rr * P.rstep;
+        s_u = P.r0w + (tap_u - rr * P.tkw) * P.rstep;
+      }
+#pragma unroll
+      for (int i = 0; i < NA; ++i) {
+        const int row = i * 32 + wave * 8 + (lane >> 3);
+        const int ci = ci_u + gl_swz(row, lane & 7) * V;
+        const T* src = g_conv_zero;
+        if (MODE == MODE_FWD) {
+          const int hh = a_h[i] + r_u * P.dh, ww = a_w[i] + s_u * P.dw;
+          if (a_ok[i] && (unsigned)hh < (unsigned)P.h && (unsigned)ww < (unsigned)P.w)
+            src = ga + a_off[i] + ((long)hh * P.w + ww) * P.c + ci;
+        } else {
+          int hn = a_h[i] - r_u * P.dh, wn = a_w[i] - s_u * P.dw;
+          bool ok = a_ok[i];
+          if (P.sh == 2) { ok = ok && !(hn & 1); hn >>= 1; }
+          if (P.sw == 2) { ok = ok && !(wn & 1); wn >>= 1; }
+          if (ok && (unsigned)hn < (unsigned)P.ho && (unsigned)wn < (unsigned)P.wo)
+            src = ga + a_off[i] + ((long)hn * P.wo + wn) * P.k + ci;
+        }
+        __builtin_amdgcn_global_load_lds((glb_t)src, (lds_t)(sa + (i * 32 + wave * 8) * BK), 16, 0, 0);
+      }
+#pragma unroll
+      for (int i = 0; i < NB; ++i) {
+        const int row = i * 32 + wave * 8 + (lane >> 3);
+        const int nrow = n0 + row;
+        const T* src = nrow < P.N ? gb + (long)nrow * P.K + k0 + gl_swz(row, lane & 7) * V : g_conv_zero;
+        __builtin_amdgcn_global_load_lds((glb_t)src, (lds_t)(sb + (i * 32 + wave * 8) * BK), 16, 0, 0);
+      }
+    }
+  };
+
   // ---- register -> LDS stage
   auto store_tile = [&](int buf) {
     T* sa = smem + buf * (A_EL + B_EL);
@@ -394,7 +467,35 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(const ConvArgs P) {
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  if (kt0 < kt1) {
+  if (G && kt0 < kt1) {
+    gl_issue(kt0, 0);
+    for (int kt = kt0; kt < kt1; ++kt) {
+      const int buf = (kt - kt0) & 1;
+      if (kt + 1 < kt1) {
+        gl_issue(kt + 1, buf ^ 1);
+        wait_vmcnt<NA + NB>();  // tile kt landed; tile kt+1 stays in flight across the barrier
+      } else {
+        wait_vmcnt<0>();
+      }
+      gl_barrier();
+      const T* sa = smem + buf * (A_EL + B_EL);
+      const T* sb = sa + A_EL;
+#pragma unroll
+      for (int ks = 0; ks < BK / KS; ++ks) {
+        bf16x8 fa[FM], fb[FN];
+#pragma unroll
+        for (int i = 0; i < FM; ++i) fa[i] = frag_kc_gl((const bf16*)sa, wm0 + i * 16, ks, lane);
+#pragma unroll
+        for (int j = 0; j < FN; ++j) fb[j] = frag_kc_gl((const bf16*)sb, wn0 + j * 16, ks, lane);
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+      }
+      gl_barrier();  // every wave is done reading buf before it is refilled
+    }
+  } else if (kt0 < kt1) {
     load_tile(kt0);
     store_tile(0);
     __syncthreads();
@@ -441,78 +542,115 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(const ConvArgs P) {
       }
   } else {
     T* out = (T*)P.out;
-#pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      const int gn = n0 + wn0 + j * 16 + ec;
-      if (gn >= P.N) continue;
-      const float bv = P.bias ? P.bias[gn] : 0.f;
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int gm = m0 + wm0 + i * 16 + er + e;
-          if (gm >= P.M) continue;
-          long orow = gm;
-          if (MODE == MODE_DGRAD && P.psh != 1) {
-            const int img = fdiv(gm, P.f_hw), rem = gm - img * P.hp * P.wp;
-            const int th = fdiv(rem, P.f_w), tw = rem - th * P.wp;
-            orow = ((long)img * P.h + th * P.psh + P.offh) * P.w + tw * P.psh + P.offw;
-          }
-          float v = acc[i][j][e] + bv;
-          if (P.accum) v += to_f(out[orow * P.N + gn]);
-          if (P.act == RTSDS_ACT_RELU) v = fmaxf(v, 0.f);
-          else if (P.act == RTSDS_ACT_LEAKY) v = v > 0.f ? v : 0.2f * v;
-          else if (P.act == RTSDS_ACT_SIGMOID) v = 1.f / (1.f + expf(-v));
-          out[orow * P.N + gn] = from_f<T>(v);
-        }
-    }
-    if (MODE == MODE_FWD && P.stats != nullptr) {
-      // BatchNorm batch statistics fused into the producing conv: exact two-pass mean / M2 of
-      // this tile's rows per output channel, from the fp32 accumulators (merged across tiles
-      // with Chan's formula by bn_finalize_kernel).
-      __syncthreads();
-      float* red = (float*)smem;  // [WM][BN]
-      const int wmi = wave / WN;
-      const int nvalid = min(BM, P.M - m0);
-      float mean[FN];
-#pragma unroll
-      for (int pass = 0; pass < 2; ++pass) {
-#pragma unroll
-        for (int j = 0; j < FN; ++j) {
-          const int gn = n0 + wn0 + j * 16 + ec;
-          const float bv = (P.bias && gn < P.N) ? P.bias[gn] : 0.f;
-          float sacc = 0.f;
-#pragma unroll
-          for (int i = 0; i < FM; ++i)
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              const int gm = m0 + wm0 + i * 16 + er + e;
-              const float v = acc[i][j][e] + bv;
-              const float t = pass == 0 ? v : (v - mean[j]) * (v - mean[j]);
-              if (gm < P.M) sacc += t;
-            }
-          sacc += __shfl_xor(sacc, 16, 64);
-          sacc += __shfl_xor(sacc, 32, 64);
-          if (lane < 16) red[wmi * BN + wn0 + j * 16 + ec] = sacc;
-        }
+    auto act_f = [&](float v) {
+      if (P.act == RTSDS_ACT_RELU) return fmaxf(v, 0.f);
+      if (P.act == RTSDS_ACT_LEAKY) return v > 0.f ? v : 0.2f * v;
+      if (P.act == RTSDS_ACT_SIGMOID) return 1.f / (1.f + expf(-v));
+      return v;
+    };
+    auto out_row = [&](int gm) -> long {  // DGRAD phase rows scatter back to the full grid
+      if (MODE == MODE_DGRAD && P.psh != 1) {
+        const int img = fdiv(gm, P.f_hw), rem = gm - img * P.hp * P.wp;
+        const int th = fdiv(rem, P.f_w), tw = rem - th * P.wp;
+        return ((long)img * P.h + th * P.psh + P.offh) * P.w + tw * P.psh + P.offw;
+      }
+      return gm;
+    };
+    bool stored = false;
+    if constexpr (sizeof(T) == 2) {
+      if (!P.accum && P.N % V == 0) {
+        // Row-vectorised store: the 16x16 C fragments (4 rows x 1 column per lane) go through
+        // LDS as bf16 [BM][BN + 8] and leave as 16-B row chunks (8 global_store_dwordx4 per
+        // thread for a 128x128 tile instead of 64 scattered 2-byte stores).
+        constexpr int CP = BN + 8, CPR = BN / V;
+        static_assert(BM * CP <= 2 * (A_EL + B_EL), "epilogue staging fits the operand LDS");
+        T* cs = smem;
         __syncthreads();
 #pragma unroll
         for (int j = 0; j < FN; ++j) {
           const int col = wn0 + j * 16 + ec;
-          float tot = 0.f;
+          const float bv = (P.bias && n0 + col < P.N) ? P.bias[n0 + col] : 0.f;
 #pragma unroll
-          for (int w = 0; w < WM; ++w) tot += red[w * BN + col];
-          if (pass == 0) {
-            mean[j] = tot / (float)nvalid;
-          } else if (wmi == 0 && lane < 16 && n0 + col < P.N) {
-            float* o = P.stats + ((long)mt * P.N + n0 + col) * 3;
-            o[0] = (float)nvalid;
-            o[1] = mean[j];
-            o[2] = tot;
-          }
+          for (int i = 0; i < FM; ++i)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) cs[(wm0 + i * 16 + er + e) * CP + col] = from_f<T>(act_f(acc[i][j][e] + bv));
         }
         __syncthreads();
+#pragma unroll
+        for (int c = tid; c < BM * CPR; c += 256) {
+          const int row = c / CPR, cc = c - row * CPR;
+          const int gm = m0 + row, gn = n0 + cc * V;
+          if (gm < P.M && gn < P.N) *(V16*)(out + out_row(gm) * P.N + gn) = *(const V16*)(cs + row * CP + cc * V);
+        }
+        stored = true;
       }
+    }
+    if (!stored) {
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int gn = n0 + wn0 + j * 16 + ec;
+        if (gn >= P.N) continue;
+        const float bv = P.bias ? P.bias[gn] : 0.f;
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int gm = m0 + wm0 + i * 16 + er + e;
+            if (gm >= P.M) continue;
+            const long orow = out_row(gm);
+            float v = acc[i][j][e] + bv;
+            if (P.accum) v += to_f(out[orow * P.N + gn]);
+            out[orow * P.N + gn] = from_f<T>(act_f(v));
+          }
+      }
+    }
+  }
+  if (MODE == MODE_FWD && P.stats != nullptr) {
+    // BatchNorm batch statistics fused into the producing conv: exact two-pass mean / M2 of
+    // this tile's rows per output channel, from the fp32 accumulators (merged across tiles
+    // with Chan's formula by bn_finalize_kernel).
+    __syncthreads();
+    float* red = (float*)smem;  // [WM][BN]
+    const int wmi = wave / WN;
+    const int nvalid = min(BM, P.M - m0);
+    float mean[FN];
+#pragma unroll
+    for (int pass = 0; pass < 2; ++pass) {
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int gn = n0 + wn0 + j * 16 + ec;
+        const float bv = (P.bias && gn < P.N) ? P.bias[gn] : 0.f;
+        float sacc = 0.f;
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int gm = m0 + wm0 + i * 16 + er + e;
+            const float v = acc[i][j][e] + bv;
+            const float t = pass == 0 ? v : (v - mean[j]) * (v - mean[j]);
+            if (gm < P.M) sacc += t;
+          }
+        sacc += __shfl_xor(sacc, 16, 64);
+        sacc += __shfl_xor(sacc, 32, 64);
+        if (lane < 16) red[wmi * BN + wn0 + j * 16 + ec] = sacc;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int col = wn0 + j * 16 + ec;
+        float tot = 0.f;
+#pragma unroll
+        for (int w = 0; w < WM; ++w) tot += red[w * BN + col];
+        if (pass == 0) {
+          mean[j] = tot / (float)nvalid;
+        } else if (wmi == 0 && lane < 16 && n0 + col < P.N) {
+          float* o = P.stats + ((long)mt * P.N + n0 + col) * 3;
+          o[0] = (float)nvalid;
+          o[1] = mean[j];
+          o[2] = tot;
+        }
+      }
+      __syncthreads();
     }
   }
 }
@@ -697,10 +835,19 @@ static void pad_any(int dtype, const void* src, void* dst, long rows, int c, int
   else pad_launch<float>(src, dst, rows, c, cp, st);
 }
 
-template <typename T, int MODE, int BM, int BN, int BK, int WM, int WN, int ALA, int ALB>
+template <typename T, int MODE, int BM, int BN, int BK, int WM, int WN, int ALA, int ALB, int GL = 0>
 static void launch(const ConvArgs& p, int splits, hipStream_t st) {
   dim3 grid(rt_cdiv(p.M, BM), rt_cdiv(p.N, BN), splits);
-  hipLaunchKernelGGL((conv_gemm_kernel<T, MODE, BM, BN, BK, WM, WN, ALA, ALB>), grid, dim3(256), 0, st, p);
+  hipLaunchKernelGGL((conv_gemm_kernel<T, MODE, BM, BN, BK, WM, WN, ALA, ALB, GL>), grid, dim3(256), 0, st, p);
+}
+
+// LDS-DMA staging on (default) / off (RTSDS_CONV_GLDS=0, for A/B measurements).
+static bool glds_enabled() {
+  static const int on = [] {
+    const char* e = getenv("RTSDS_CONV_GLDS");
+    return (e && e[0] == '0') ? 0 : 1;
+  }();
+  return on != 0;
 }
 
 // Tile selection for FWD / DGRAD (occupancy-aware): the widest tile that still puts >= 256
@@ -722,6 +869,12 @@ static void pick_tile(long M, int N, bool b16, int& bm, int& bn) {
 // K-step), 32 for 128x64 / narrow-N tiles whose LDS footprint would otherwise cut occupancy.
 template <typename T, int MODE, int BM, int BN, int BK, int WM, int WN>
 static void launch_al(const ConvArgs& p, int cr, hipStream_t st) {
+  if constexpr (sizeof(T) == 2 && BK == 64 && BM % 32 == 0 && BN % 32 == 0) {
+    if (cr % BK == 0 && glds_enabled()) {
+      launch<T, MODE, BM, BN, BK, WM, WN, 2, 1, 1>(p, 1, st);
+      return;
+    }
+  }
   if (cr % BK == 0) launch<T, MODE, BM, BN, BK, WM, WN, 2, 1>(p, 1, st);
   else launch<T, MODE, BM, BN, BK, WM, WN, 1, 1>(p, 1, st);
 }

@@ -53,6 +53,7 @@ CONV_CASES = [
     (1, 32, 13, 17, 64, 3, 2, 1, 1, False),    # stride-2 dgrad phases, odd sizes
     (2, 8, 9, 11, 16, 4, 2, 1, 1, True),       # k4 s2 phases, odd sizes
     (2, 16, 7, 9, 32, 1, 2, 0, 1, False),      # 1x1 s2: odd phases receive nothing
+    (8, 128, 64, 64, 128, 3, 1, 1, 1, False),  # 128x128 LDS-DMA tiles (fwd and dgrad)
 ]
 
 
