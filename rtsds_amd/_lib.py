@@ -11,7 +11,8 @@ import os
 import torch  # noqa: F401  (must precede the dlopen below)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "librtsds_hip.so")
+# RTSDS_LIB: alternative in-tree build of the same ABI (kernel-variant A/B measurements)
+LIB_PATH = os.environ.get("RTSDS_LIB") or os.path.join(_HERE, "librtsds_hip.so")
 
 F32, BF16 = 0, 1
 ACT_NONE, ACT_RELU, ACT_LEAKY, ACT_SIGMOID = 0, 1, 2, 3

@@ -127,7 +127,7 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(const ConvArgs P) {
   constexpr int V = VecT<T>::N;
   constexpr bool RC = (MODE == MODE_WGRAD);
   constexpr bool G = GL != 0;
-  static_assert(!G || (sizeof(T) == 2 && MODE != MODE_WGRAD && BK == 64 && ALA == 2 && ALB == 1 && BM % 32 == 0 &&
+  static_assert(!G || (sizeof(T) == 2 && MODE != MODE_WGRAD && BK == 64 && ALA >= 1 && ALB == 1 && BM % 32 == 0 &&
                        BN % 32 == 0), "GL staging");
   constexpr int KCP = G ? BK : KCPitch<T, BK>::v;
   constexpr int PA = RC ? RCPitch<BM>::v : KCP;
@@ -142,7 +142,8 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(const ConvArgs P) {
   static_assert(BK % KS == 0, "BK");
   static_assert(!RC || BK % (sizeof(T) == 2 ? 32 : 16) == 0, "RC BK");
 
-  __shared__ __attribute__((aligned(16))) T smem[2 * (A_EL + B_EL)];
+  constexpr int NBUF = (GL >= 3) ? GL : 2;  // LDS operand buffers
+  __shared__ __attribute__((aligned(16))) T smem[NBUF * (A_EL + B_EL)];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm0 = (wave / WN) * WTM, wn0 = (wave % WN) * WTN;
@@ -375,28 +376,48 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(const ConvArgs P) {
       T* sa = smem + buf * (A_EL + B_EL);
       T* sb = sa + A_EL;
       const int Cr = (MODE == MODE_FWD) ? P.c : P.k;
-      const int tap_u = k0 / Cr, ci_u = k0 - tap_u * Cr;
-      int r_u, s_u;
-      if (MODE == MODE_FWD) {
-        r_u = tap_u / P.kw;
-        s_u = tap_u - r_u * P.kw;
-      } else {
-        const int rr = tap_u / P.tkw;
-        r_u = P.r0h + rr * P.rstep;
-        s_u = P.r0w + (tap_u - rr * P.tkw) * P.rstep;
+      // ALA 2: one filter tap per K-tile (wave-uniform); ALA 1: a tap per 16-B chunk.
+      int tap_u = 0, ci_u = 0, r_u = 0, s_u = 0;
+      if (ALA == 2) {
+        tap_u = k0 / Cr;
+        ci_u = k0 - tap_u * Cr;
+        if (MODE == MODE_FWD) {
+          r_u = tap_u / P.kw;
+          s_u = tap_u - r_u * P.kw;
+        } else {
+          const int rr = tap_u / P.tkw;
+          r_u = P.r0h + rr * P.rstep;
+          s_u = P.r0w + (tap_u - rr * P.tkw) * P.rstep;
+        }
       }
 #pragma unroll
       for (int i = 0; i < NA; ++i) {
         const int row = i * 32 + wave * 8 + (lane >> 3);
-        const int ci = ci_u + gl_swz(row, lane & 7) * V;
+        const int chunk = gl_swz(row, lane & 7);
+        int ci = ci_u + chunk * V, r = r_u, sx = s_u;
+        bool okk = true;
+        if (ALA == 1) {
+          const int kk = k0 + chunk * V;
+          okk = kk < P.K;
+          const int tap = fdiv(kk, MODE == MODE_FWD ? P.f_c : P.f_k);
+          ci = kk - tap * Cr;
+          if (MODE == MODE_FWD) {
+            r = fdiv(tap, P.f_kw);
+            sx = tap - r * P.kw;
+          } else {
+            const int rr = fdiv(tap, P.f_tkw);
+            r = P.r0h + rr * P.rstep;
+            sx = P.r0w + (tap - rr * P.tkw) * P.rstep;
+          }
+        }
         const T* src = g_conv_zero;
         if (MODE == MODE_FWD) {
-          const int hh = a_h[i] + r_u * P.dh, ww = a_w[i] + s_u * P.dw;
-          if (a_ok[i] && (unsigned)hh < (unsigned)P.h && (unsigned)ww < (unsigned)P.w)
+          const int hh = a_h[i] + r * P.dh, ww = a_w[i] + sx * P.dw;
+          if (okk && a_ok[i] && (unsigned)hh < (unsigned)P.h && (unsigned)ww < (unsigned)P.w)
             src = ga + a_off[i] + ((long)hh * P.w + ww) * P.c + ci;
         } else {
-          int hn = a_h[i] - r_u * P.dh, wn = a_w[i] - s_u * P.dw;
-          bool ok = a_ok[i];
+          int hn = a_h[i] - r * P.dh, wn = a_w[i] - sx * P.dw;
+          bool ok = a_ok[i] && okk;
           if (P.sh == 2) { ok = ok && !(hn & 1); hn >>= 1; }
           if (P.sw == 2) { ok = ok && !(wn & 1); wn >>= 1; }
           if (ok && (unsigned)hn < (unsigned)P.ho && (unsigned)wn < (unsigned)P.wo)
@@ -408,7 +429,8 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(const ConvArgs P) {
       for (int i = 0; i < NB; ++i) {
         const int row = i * 32 + wave * 8 + (lane >> 3);
         const int nrow = n0 + row;
-        const T* src = nrow < P.N ? gb + (long)nrow * P.K + k0 + gl_swz(row, lane & 7) * V : g_conv_zero;
+        const int kk = k0 + gl_swz(row, lane & 7) * V;
+        const T* src = (nrow < P.N && kk < P.K) ? gb + (long)nrow * P.K + kk : g_conv_zero;
         __builtin_amdgcn_global_load_lds((glb_t)src, (lds_t)(sb + (i * 32 + wave * 8) * BK), 16, 0, 0);
       }
     }
@@ -467,17 +489,19 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(const ConvArgs P) {
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  if (G && kt0 < kt1) {
-    gl_issue(kt0, 0);
+  if (GL >= 3 && kt0 < kt1) {
+    // NBUF-deep ring, one barrier per K-step: tiles kt+1 .. kt+NBUF-2 stay in flight while
+    // tile kt is consumed; the barrier also retires every wave's reads of tile kt-1, whose
+    // buffer the DMA of tile kt+NBUF-1 then refills.
+#pragma unroll
+    for (int p2 = 0; p2 < NBUF - 1; ++p2)
+      if (kt0 + p2 < kt1) gl_issue(kt0 + p2, p2);
     for (int kt = kt0; kt < kt1; ++kt) {
-      const int buf = (kt - kt0) & 1;
-      if (kt + 1 < kt1) {
-        gl_issue(kt + 1, buf ^ 1);
-        wait_vmcnt<NA + NB>();  // tile kt landed; tile kt+1 stays in flight across the barrier
-      } else {
-        wait_vmcnt<0>();
-      }
+      const int it = kt - kt0, buf = it % NBUF;
+      if (kt + NBUF - 2 < kt1) wait_vmcnt<(NBUF - 2) * (NA + NB)>();
+      else wait_vmcnt<0>();
       gl_barrier();
+      if (kt + NBUF - 1 < kt1) gl_issue(kt + NBUF - 1, (it + NBUF - 1) % NBUF);
       const T* sa = smem + buf * (A_EL + B_EL);
       const T* sb = sa + A_EL;
 #pragma unroll
@@ -492,6 +516,46 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(const ConvArgs P) {
 #pragma unroll
           for (int j = 0; j < FN; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+      }
+    }
+  } else if (G && kt0 < kt1) {
+    gl_issue(kt0, 0);
+    for (int kt = kt0; kt < kt1; ++kt) {
+      const int buf = (kt - kt0) & 1;
+#ifndef RTSDS_CONV_MIDISSUE
+      if (kt + 1 < kt1) {
+        gl_issue(kt + 1, buf ^ 1);
+        wait_vmcnt<NA + NB>();  // tile kt landed; tile kt+1 stays in flight across the barrier
+      } else {
+        wait_vmcnt<0>();
+      }
+#else
+      wait_vmcnt<0>();
+#endif
+      gl_barrier();
+      const T* sa = smem + buf * (A_EL + B_EL);
+      const T* sb = sa + A_EL;
+#pragma unroll
+      for (int ks = 0; ks < BK / KS; ++ks) {
+        bf16x8 fa[FM], fb[FN];
+#pragma unroll
+        for (int i = 0; i < FM; ++i) fa[i] = frag_kc_gl((const bf16*)sa, wm0 + i * 16, ks, lane);
+#pragma unroll
+        for (int j = 0; j < FN; ++j) fb[j] = frag_kc_gl((const bf16*)sb, wn0 + j * 16, ks, lane);
+#ifdef RTSDS_CONV_PRIO
+        __builtin_amdgcn_s_setprio(1);
+#endif
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+#ifdef RTSDS_CONV_PRIO
+        __builtin_amdgcn_s_setprio(0);
+#endif
+#ifdef RTSDS_CONV_MIDISSUE
+        if (ks == 0 && kt + 1 < kt1) gl_issue(kt + 1, buf ^ 1);
+#endif
       }
       gl_barrier();  // every wave is done reading buf before it is refilled
     }
@@ -563,7 +627,7 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(const ConvArgs P) {
         // LDS as bf16 [BM][BN + 8] and leave as 16-B row chunks (8 global_store_dwordx4 per
         // thread for a 128x128 tile instead of 64 scattered 2-byte stores).
         constexpr int CP = BN + 8, CPR = BN / V;
-        static_assert(BM * CP <= 2 * (A_EL + B_EL), "epilogue staging fits the operand LDS");
+        static_assert(BM * CP <= NBUF * (A_EL + B_EL), "epilogue staging fits the operand LDS");
         T* cs = smem;
         __syncthreads();
 #pragma unroll
@@ -869,9 +933,13 @@ static void pick_tile(long M, int N, bool b16, int& bm, int& bn) {
 // K-step), 32 for 128x64 / narrow-N tiles whose LDS footprint would otherwise cut occupancy.
 template <typename T, int MODE, int BM, int BN, int BK, int WM, int WN>
 static void launch_al(const ConvArgs& p, int cr, hipStream_t st) {
-  if constexpr (sizeof(T) == 2 && BK == 64 && BM % 32 == 0 && BN % 32 == 0) {
-    if (cr % BK == 0 && glds_enabled()) {
-      launch<T, MODE, BM, BN, BK, WM, WN, 2, 1, 1>(p, 1, st);
+  if constexpr (sizeof(T) == 2 && BM % 32 == 0 && BN % 32 == 0) {
+    // LDS-DMA path: every bf16 tile at BK = 64 (16-B chunks never straddle a tap: cr % 8 == 0)
+    // (not for 3-channel images padded to 8: eight taps per K-tile gathered per chunk lose
+    // to the register path there)
+    if (glds_enabled() && cr % 32 == 0 && p.K % 8 == 0) {
+      if (cr % 64 == 0) launch<T, MODE, BM, BN, 64, WM, WN, 2, 1, 2>(p, 1, st);
+      else launch<T, MODE, BM, BN, 64, WM, WN, 1, 1, 2>(p, 1, st);
       return;
     }
   }
