@@ -28,6 +28,8 @@ struct ConvArgs {
   int n, h, w, c, ho, wo, k, kh, kw, sh, sw, ph, pw, dh, dw;
   FastDiv f_howo, f_wo, f_hw, f_w, f_c, f_k, f_kw;
   int tiles_per_split;
+  int wg_rows;        // WGRAD: 64-pixel K-tiles never straddle an image and map to whole / part
+                      // output rows (ho*wo % 64 == 0 and wo | 64 or 64 | wo) -> affine gathers
   // DGRAD stride-phase decomposition (normal mode: tkw=kw, r0=0, rstep=1, psh=1, off=0,
   // hp=h, wp=w): output rows enumerate the pixels ih = th*psh + offh of one parity phase,
   // and the reduction runs over that phase's taps r = r0 + rr*rstep only.
@@ -97,6 +99,33 @@ RT_DEV bf16x8 frag_kc_gl(const bf16* s, int row0, int ks, int lane) {
   const int row = row0 + (lane & 15);
   return *(const bf16x8*)(s + row * 64 + gl_swz(row, ks * 4 + (lane >> 4)) * 8);
 }
+// GL image of the RC (WGRAD) tiles: [64 pixel rows][COLS] bf16, unpadded, 16-B chunk c of row r
+// at physical chunk c ^ rc_swz(r).  The transposed fragment read (ds_read_b64_tr_b16: 8 rows
+// x 32 B per 32-lane group) then touches 16 distinct chunks = all 64 banks for 256-B rows.
+template <int COLS> RT_DEV int rc_swz(int row) {
+  return COLS >= 128 ? (row & 7) << 1 : ((row >> 1) & 3) << 1;
+}
+// Issued as inline asm: hipcc cannot tell the transposed-read builtin apart from the LDS-DMA
+// writes still in flight and would drain vmcnt(0) before every K-step's first read (losing the
+// prefetch).  The caller waits lgkmcnt(0) and re-ties the registers (rc_gl_wait) before use.
+RT_DEV uint32_t lds_addr(const void* p) {
+  return (uint32_t)(size_t)(const __attribute__((address_space(3))) void*)p;
+}
+template <int COLS>
+RT_DEV void frag_rc_gl_issue(const bf16* s, int col0, int ks, int lane, s16x4& t0, s16x4& t1) {
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  const int r0 = ks * 32 + 4 * g + q, r1 = r0 + 16;
+  const int c = (col0 + 4 * p) >> 3, h = (p & 1) * 4;  // 16-B chunk, bf16 offset within it
+  const uint32_t a0 = lds_addr(s + r0 * COLS + ((c ^ rc_swz<COLS>(r0)) << 3) + h);
+  const uint32_t a1 = lds_addr(s + r1 * COLS + ((c ^ rc_swz<COLS>(r1)) << 3) + h);
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(t0) : "v"(a0));
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(t1) : "v"(a1));
+}
+RT_DEV bf16x8 rc_gl_frag(s16x4 t0, s16x4 t1) {
+  typedef __attribute__((ext_vector_type(8))) short s16x8;
+  s16x8 r = {t0[0], t0[1], t0[2], t0[3], t1[0], t1[1], t1[2], t1[3]};
+  return __builtin_bit_cast(bf16x8, r);
+}
 // 16 zero bytes: the DMA source of padding / out-of-range gathers.
 __device__ __attribute__((aligned(16))) bf16 g_conv_zero[8];
 template <int N> RT_DEV void wait_vmcnt() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
@@ -127,11 +156,11 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(const ConvArgs P) {
   constexpr int V = VecT<T>::N;
   constexpr bool RC = (MODE == MODE_WGRAD);
   constexpr bool G = GL != 0;
-  static_assert(!G || (sizeof(T) == 2 && MODE != MODE_WGRAD && BK == 64 && ALA >= 1 && ALB == 1 && BM % 32 == 0 &&
-                       BN % 32 == 0), "GL staging");
+  static_assert(!G || (sizeof(T) == 2 && BK == 64 && ALA >= 1 && ALB == 1 && BM % 32 == 0 && BN % 32 == 0 &&
+                       (MODE != MODE_WGRAD || (BM >= 64 && BN >= 64))), "GL staging");
   constexpr int KCP = G ? BK : KCPitch<T, BK>::v;
-  constexpr int PA = RC ? RCPitch<BM>::v : KCP;
-  constexpr int PB = RC ? RCPitch<BN>::v : KCP;
+  constexpr int PA = RC ? (G ? BM : RCPitch<BM>::v) : KCP;
+  constexpr int PB = RC ? (G ? BN : RCPitch<BN>::v) : KCP;
   constexpr int A_EL = RC ? BK * PA : BM * PA;
   constexpr int B_EL = RC ? BK * PB : BN * PB;
   constexpr int CA = BM * BK / V, CB = BN * BK / V;      // 16-B chunks per tile
@@ -208,6 +237,27 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(const ConvArgs P) {
       b_ci = nn - tap * P.c;
       b_r = fdiv(tap, P.f_kw);
       b_s = tap - b_r * P.kw;
+    }
+  }
+
+  // GL WGRAD: the (tap, ci) column of each B chunk this lane stages is fixed for the whole
+  // reduction (the swizzled chunk depends only on the tile row).
+  int gb_r[G && RC ? NB : 1], gb_s[G && RC ? NB : 1], gb_ci[G && RC ? NB : 1];
+  int gb_dh[G && RC ? NB : 1], gb_dw[G && RC ? NB : 1];  // wg_rows: row -> (d oh, d ow) in the tile
+  bool gb_ok[G && RC ? NB : 1];
+  if constexpr (G && RC) {
+    constexpr int CPB = BN / V, RPB = 64 / CPB;
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const int row = (i * 4 + wave) * RPB + lane / CPB;
+      gb_dh[i] = P.wo >= 64 ? 0 : row / P.wo;
+      gb_dw[i] = P.wo >= 64 ? row : row - gb_dh[i] * P.wo;
+      const int nn = n0 + ((lane % CPB) ^ rc_swz<BN>(row)) * V;
+      gb_ok[i] = nn < P.N;
+      const int tap = fdiv(gb_ok[i] ? nn : 0, P.f_c);
+      gb_ci[i] = (gb_ok[i] ? nn : 0) - tap * P.c;
+      gb_r[i] = fdiv(tap, P.f_kw);
+      gb_s[i] = tap - gb_r[i] * P.kw;
     }
   }
 
@@ -369,7 +419,46 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(const ConvArgs P) {
 
   // ---- GL: global -> LDS DMA of K-tile kt into buffer buf (NA + NB instructions per thread)
   auto gl_issue = [&](int kt, int buf) {
-    if constexpr (G) {
+    if constexpr (G && RC) {
+      typedef __attribute__((address_space(3))) void* lds_t;
+      typedef const __attribute__((address_space(1))) void* glb_t;
+      const int k0 = kt * BK;
+      T* sa = smem + buf * (A_EL + B_EL);
+      T* sb = sa + A_EL;
+      constexpr int CPA = BM / V, RPA = 64 / CPA;  // chunks per row, rows per wave-instruction
+      constexpr int CPB = BN / V, RPB = 64 / CPB;
+#pragma unroll
+      for (int i = 0; i < NA; ++i) {  // dY rows (pixels) x Cout columns
+        const int rb = (i * 4 + wave) * RPA, row = rb + lane / CPA;
+        const int chunk = (lane % CPA) ^ rc_swz<BM>(row);
+        const int q = k0 + row, co = m0 + chunk * V;
+        const T* src = (q < P.K && co < P.M) ? ga + (long)q * P.k + co : g_conv_zero;
+        __builtin_amdgcn_global_load_lds((glb_t)src, (lds_t)(sa + rb * BM), 16, 0, 0);
+      }
+      // tile origin (img, oh0, ow0): wave-uniform
+      const int t_img = fdiv(k0, P.f_howo), t_rem = k0 - t_img * P.ho * P.wo;
+      const int t_oh = fdiv(t_rem, P.f_wo), t_ow = t_rem - t_oh * P.wo;
+      const T* t_base = gb + (long)t_img * P.h * P.w * P.c;
+#pragma unroll
+      for (int i = 0; i < NB; ++i) {  // input patches: rows = output pixels, columns = (r, s, ci)
+        const int rb = (i * 4 + wave) * RPB, row = rb + lane / CPB;
+        const int q = k0 + row;
+        const T* src = g_conv_zero;
+        if (P.wg_rows) {
+          const int hh = (t_oh + gb_dh[i]) * P.sh - P.ph + gb_r[i] * P.dh;
+          const int ww = (t_ow + gb_dw[i]) * P.sw - P.pw + gb_s[i] * P.dw;
+          if (gb_ok[i] && (unsigned)hh < (unsigned)P.h && (unsigned)ww < (unsigned)P.w)
+            src = t_base + ((long)hh * P.w + ww) * P.c + gb_ci[i];
+        } else if (gb_ok[i] && q < P.K) {
+          const int img = fdiv(q, P.f_howo), rem = q - img * P.ho * P.wo;
+          const int oh = fdiv(rem, P.f_wo), ow = rem - oh * P.wo;
+          const int hh = oh * P.sh - P.ph + gb_r[i] * P.dh, ww = ow * P.sw - P.pw + gb_s[i] * P.dw;
+          if ((unsigned)hh < (unsigned)P.h && (unsigned)ww < (unsigned)P.w)
+            src = gb + (long)img * P.h * P.w * P.c + ((long)hh * P.w + ww) * P.c + gb_ci[i];
+        }
+        __builtin_amdgcn_global_load_lds((glb_t)src, (lds_t)(sb + rb * BN), 16, 0, 0);
+      }
+    } else if constexpr (G) {
       typedef __attribute__((address_space(3))) void* lds_t;
       typedef const __attribute__((address_space(1))) void* glb_t;
       const int k0 = kt * BK;
@@ -507,10 +596,29 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(const ConvArgs P) {
 #pragma unroll
       for (int ks = 0; ks < BK / KS; ++ks) {
         bf16x8 fa[FM], fb[FN];
+        if constexpr (RC) {
+          s16x4 ta[FM][2], tb[FN][2];
 #pragma unroll
-        for (int i = 0; i < FM; ++i) fa[i] = frag_kc_gl((const bf16*)sa, wm0 + i * 16, ks, lane);
+          for (int i = 0; i < FM; ++i) frag_rc_gl_issue<BM>((const bf16*)sa, wm0 + i * 16, ks, lane, ta[i][0], ta[i][1]);
 #pragma unroll
-        for (int j = 0; j < FN; ++j) fb[j] = frag_kc_gl((const bf16*)sb, wn0 + j * 16, ks, lane);
+          for (int j = 0; j < FN; ++j) frag_rc_gl_issue<BN>((const bf16*)sb, wn0 + j * 16, ks, lane, tb[j][0], tb[j][1]);
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+          for (int i = 0; i < FM; ++i) {
+            asm volatile("" : "+v"(ta[i][0]), "+v"(ta[i][1]));
+            fa[i] = rc_gl_frag(ta[i][0], ta[i][1]);
+          }
+#pragma unroll
+          for (int j = 0; j < FN; ++j) {
+            asm volatile("" : "+v"(tb[j][0]), "+v"(tb[j][1]));
+            fb[j] = rc_gl_frag(tb[j][0], tb[j][1]);
+          }
+        } else {
+#pragma unroll
+          for (int i = 0; i < FM; ++i) fa[i] = frag_kc_gl((const bf16*)sa, wm0 + i * 16, ks, lane);
+#pragma unroll
+          for (int j = 0; j < FN; ++j) fb[j] = frag_kc_gl((const bf16*)sb, wn0 + j * 16, ks, lane);
+        }
 #pragma unroll
         for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -538,10 +646,29 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(const ConvArgs P) {
 #pragma unroll
       for (int ks = 0; ks < BK / KS; ++ks) {
         bf16x8 fa[FM], fb[FN];
+        if constexpr (RC) {
+          s16x4 ta[FM][2], tb[FN][2];
 #pragma unroll
-        for (int i = 0; i < FM; ++i) fa[i] = frag_kc_gl((const bf16*)sa, wm0 + i * 16, ks, lane);
+          for (int i = 0; i < FM; ++i) frag_rc_gl_issue<BM>((const bf16*)sa, wm0 + i * 16, ks, lane, ta[i][0], ta[i][1]);
 #pragma unroll
-        for (int j = 0; j < FN; ++j) fb[j] = frag_kc_gl((const bf16*)sb, wn0 + j * 16, ks, lane);
+          for (int j = 0; j < FN; ++j) frag_rc_gl_issue<BN>((const bf16*)sb, wn0 + j * 16, ks, lane, tb[j][0], tb[j][1]);
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+          for (int i = 0; i < FM; ++i) {
+            asm volatile("" : "+v"(ta[i][0]), "+v"(ta[i][1]));
+            fa[i] = rc_gl_frag(ta[i][0], ta[i][1]);
+          }
+#pragma unroll
+          for (int j = 0; j < FN; ++j) {
+            asm volatile("" : "+v"(tb[j][0]), "+v"(tb[j][1]));
+            fb[j] = rc_gl_frag(tb[j][0], tb[j][1]);
+          }
+        } else {
+#pragma unroll
+          for (int i = 0; i < FM; ++i) fa[i] = frag_kc_gl((const bf16*)sa, wm0 + i * 16, ks, lane);
+#pragma unroll
+          for (int j = 0; j < FN; ++j) fb[j] = frag_kc_gl((const bf16*)sb, wn0 + j * 16, ks, lane);
+        }
 #ifdef RTSDS_CONV_PRIO
         __builtin_amdgcn_s_setprio(1);
 #endif
@@ -592,18 +719,44 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(const ConvArgs P) {
   const int er = (lane >> 4) * 4, ec = lane & 15;
   if (MODE == MODE_WGRAD) {
     float* out = (float*)P.out + (long)blockIdx.z * P.split_stride;
+    if (P.N % 4 == 0) {
+      // fp32 slab rows leave as 16-B chunks: the C fragments are staged through LDS one
+      // wave-row band (WTM rows) at a time, [WTM][BN + 4] fp32.
+      constexpr int CP = BN + 4, CPR = BN / 4;
+      static_assert(WTM * CP * 4 <= (int)sizeof(smem), "slab staging fits the operand LDS");
+      float* cs = (float*)smem;
 #pragma unroll
-    for (int i = 0; i < FM; ++i)
+      for (int band = 0; band < WM; ++band) {
+        __syncthreads();
+        if (wave / WN == band) {
 #pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        const int gn = n0 + wn0 + j * 16 + ec;
-        if (gn >= P.N) continue;
+          for (int i = 0; i < FM; ++i)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int gm = m0 + wm0 + i * 16 + er + e;
-          if (gm < P.M) out[(long)gm * P.N + gn] = acc[i][j][e];
+            for (int j = 0; j < FN; ++j)
+#pragma unroll
+              for (int e = 0; e < 4; ++e) cs[(i * 16 + er + e) * CP + wn0 + j * 16 + ec] = acc[i][j][e];
+        }
+        __syncthreads();
+        for (int c = tid; c < WTM * CPR; c += 256) {
+          const int row = c / CPR, cc = c - row * CPR;
+          const int gm = m0 + band * WTM + row, gn = n0 + cc * 4;
+          if (gm < P.M && gn < P.N) *(f32x4*)(out + (long)gm * P.N + gn) = *(const f32x4*)(cs + row * CP + cc * 4);
         }
       }
+    } else {
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          const int gn = n0 + wn0 + j * 16 + ec;
+          if (gn >= P.N) continue;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int gm = m0 + wm0 + i * 16 + er + e;
+            if (gm < P.M) out[(long)gm * P.N + gn] = acc[i][j][e];
+          }
+        }
+    }
   } else {
     T* out = (T*)P.out;
     auto act_f = [&](float v) {
@@ -855,6 +1008,8 @@ static ConvArgs make_args(const rtsds_conv_desc* d) {
   p.r0h = p.r0w = 0; p.rstep = 1; p.psh = 1; p.offh = p.offw = 0;
   p.hp = d->h; p.wp = d->w;
   p.tiles_per_split = 1 << 30;
+  const int hw = d->ho * d->wo;
+  p.wg_rows = (hw % 64 == 0) && (d->wo % 64 == 0 || 64 % d->wo == 0);
   return p;
 }
 
@@ -1139,7 +1294,12 @@ template <typename T>
 static void wgrad_launch(const ConvArgs& p, int bm, int bn, int splits, hipStream_t st) {
   constexpr int BK = sizeof(T) == 2 ? 64 : 16;
   if constexpr (sizeof(T) == 2) {
-    if (bm == 64 && bn == 64) launch<T, MODE_WGRAD, 64, 64, BK, 2, 2, 1, 1>(p, splits, st);
+    if (glds_enabled()) {  // LDS-DMA staging (swizzled RC images)
+      if (bm == 64 && bn == 64) launch<T, MODE_WGRAD, 64, 64, BK, 2, 2, 1, 1, 2>(p, splits, st);
+      else if (bm == 64) launch<T, MODE_WGRAD, 64, 128, BK, 2, 2, 1, 1, 2>(p, splits, st);
+      else if (bn == 64) launch<T, MODE_WGRAD, 128, 64, BK, 2, 2, 1, 1, 2>(p, splits, st);
+      else launch<T, MODE_WGRAD, 128, 128, BK, 2, 2, 1, 1, 2>(p, splits, st);
+    } else if (bm == 64 && bn == 64) launch<T, MODE_WGRAD, 64, 64, BK, 2, 2, 1, 1>(p, splits, st);
     else if (bm == 64) launch<T, MODE_WGRAD, 64, 128, BK, 2, 2, 1, 1>(p, splits, st);
     else if (bn == 64) launch<T, MODE_WGRAD, 128, 64, BK, 2, 2, 1, 1>(p, splits, st);
     else launch<T, MODE_WGRAD, 128, 128, BK, 2, 2, 1, 1>(p, splits, st);
