@@ -21,28 +21,28 @@ template <int VEC> struct BnLayout {
   }
 };
 
+// VEC is either the 16-B vector width (dispatched only when c % VEC == 0, so an active thread's
+// channel vector is always complete) or 1.
 template <typename T, int VEC>
 RT_DEV void load_vec(const T* p, float* v, int cvalid) {
-  if (VEC == VecT<T>::N && cvalid >= VEC) {
+  static_assert(VEC == 1 || VEC == VecT<T>::N, "VEC");
+  if constexpr (VEC == VecT<T>::N) {
     typename VecT<T>::v16 t = *(const typename VecT<T>::v16*)p;
 #pragma unroll
     for (int j = 0; j < VEC; ++j) v[j] = to_f(t[j]);
   } else {
-#pragma unroll
-    for (int j = 0; j < VEC; ++j) v[j] = j < cvalid ? to_f(p[j]) : 0.f;
+    v[0] = cvalid > 0 ? to_f(p[0]) : 0.f;
   }
 }
 template <typename T, int VEC>
 RT_DEV void store_vec(T* p, const float* v, int cvalid) {
-  if (VEC == VecT<T>::N && cvalid >= VEC) {
+  if constexpr (VEC == VecT<T>::N) {
     typename VecT<T>::v16 t;
 #pragma unroll
     for (int j = 0; j < VEC; ++j) t[j] = from_f<T>(v[j]);
     *(typename VecT<T>::v16*)p = t;
   } else {
-#pragma unroll
-    for (int j = 0; j < VEC; ++j)
-      if (j < cvalid) p[j] = from_f<T>(v[j]);
+    if (cvalid > 0) p[0] = from_f<T>(v[0]);
   }
 }
 
@@ -346,15 +346,37 @@ __global__ void __launch_bounds__(256) bn_bwd_stats_kernel(const T* __restrict__
   for (int j = 0; j < VEC; ++j) { sg[j] = 0.f; sgx[j] = 0.f; }
   if (active) {
     bn_bwd_coef<VEC>(ch0, c, gamma, beta, mean, sinv, mu, sc, sh);
-    for (long r = (long)blockIdx.x * L.rpi + rg; r < rows; r += (long)gridDim.x * L.rpi) {
-      float g[VEC], xv[VEC];
-      load_vec<T, VEC>(dy + r * c + ch0, g, c - ch0);
-      load_vec<T, VEC>(x + r * c + ch0, xv, c - ch0);
-      bn_act_grad<T, VEC>(g, y ? y + r * c + ch0 : nullptr, xv, sc, sh, act, c - ch0);
+    const long step = (long)gridDim.x * L.rpi;
+#ifndef RTSDS_BN_U
+#define RTSDS_BN_U 2
+#endif
+    constexpr int U = RTSDS_BN_U;  // rows in flight per thread (loads issued before any use)
+    for (long r = (long)blockIdx.x * L.rpi + rg; r < rows; r += U * step) {
+      float g[U][VEC], xv[U][VEC], yv[U][VEC];
 #pragma unroll
-      for (int j = 0; j < VEC; ++j) {
-        sg[j] += g[j];
-        sgx[j] = fmaf(g[j], xv[j] - mu[j], sgx[j]);
+      for (int u = 0; u < U; ++u) {
+        const long rr = r + u * step;
+        if (rr < rows) {
+          load_vec<T, VEC>(dy + rr * c + ch0, g[u], c - ch0);
+          load_vec<T, VEC>(x + rr * c + ch0, xv[u], c - ch0);
+          if (y && act) load_vec<T, VEC>(y + rr * c + ch0, yv[u], c - ch0);
+        } else {
+#pragma unroll
+          for (int j = 0; j < VEC; ++j) { g[u][j] = 0.f; xv[u][j] = mu[j]; yv[u][j] = 0.f; }
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (act) {
+#pragma unroll
+          for (int j = 0; j < VEC; ++j)
+            g[u][j] *= y ? act_grad(yv[u][j], act) : (fmaf(xv[u][j], sc[j], sh[j]) > 0.f ? 1.f : (act == RTSDS_ACT_LEAKY ? 0.2f : 0.f));
+        }
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) {
+          sg[j] += g[u][j];
+          sgx[j] = fmaf(g[u][j], xv[u][j] - mu[j], sgx[j]);
+        }
       }
     }
   }
