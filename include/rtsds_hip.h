@@ -151,6 +151,15 @@ int rtsds_bilinear_bwd(const void* dy, void* dx, int n, int hi, int wi, int c, i
                        float scale_h, float scale_w, int dy_ld, int dy_off, int dtype, void* ws,
                        size_t ws_bytes, void* stream);
 
+/* ---------------------------------------------------------------- adaptive average pool
+ * F.adaptive_avg_pool2d(x, (ho, wo)) of adversarial_train_2 (train.py:410,438,445): window
+ * rows [floor(o*hi/ho), ceil((o+1)*hi/ho)), same for columns (ATen semantics), NHWC.
+ * Backward gathers each input pixel's share of every window containing it (no atomics).   */
+int rtsds_adaptive_avgpool_fwd(const void* x, void* y, int n, int hi, int wi, int c, int ho, int wo,
+                               int dtype, void* stream);
+int rtsds_adaptive_avgpool_bwd(const void* dy, void* dx, int n, int hi, int wi, int c, int ho, int wo,
+                               int dtype, void* stream);
+
 /* ---------------------------------------------------------------- softmax / losses
  * Logits addressed by element strides (sn, sc, shw) per (image, channel, pixel): NHWC and
  * NCHW both work.  Softmax over channels (train.py:225,245,256) writes NHWC with pitch

@@ -3,6 +3,7 @@
 * ``poly_lr``  -- utils.poly_lr_scheduler (reference utils.py:33-48)
 * ``seg_step`` -- one iteration of train.train (train.py:65-113)
 * ``da_step``  -- one iteration of train.adversarial_train (train.py:172-284)
+* ``da2_step`` -- one iteration of train.adversarial_train_2 (train.py:373-466)
 
 They are written against plain torch modules / optimizers so the same functions drive
 the oracle models; the HIP path has its own loop in ``rtsds_amd.train``.
@@ -71,4 +72,44 @@ def da_step(G, D, optG, optD, ce, bce, src, lbl, tgt, lambda_, iterations):
     correct = int(src_feat.argmax(1).eq(lbl).sum())
     return {"loss_gen_source": float(l_seg), "loss_adversarial": float(l_adv),
             "loss_disc_source": float(l_ds), "loss_disc_target": float(l_dt),
+            "correct": correct, "total": lbl.numel()}
+
+
+def da2_step(G, D, optG, optD, ce, bce, src, lbl, tgt, lambda_adv):
+    """train.py:373-466 (one inner iteration; LR scheduling is the caller's)."""
+    th, tw = tgt.shape[2], tgt.shape[3]
+    real = torch.ones(tgt.shape[0], 1, 1, 1)
+    fake = torch.zeros(tgt.shape[0], 1, 1, 1)
+    optG.zero_grad()
+    out = G(src)
+    if isinstance(out, tuple):
+        l_seg = ce(out[0], lbl)
+        for a in out[1:]:
+            if a is not None:
+                l_seg = l_seg + ce(a, lbl)
+        out = out[0]
+    else:
+        l_seg = ce(out, lbl)
+    correct = int(out.argmax(1).eq(lbl).sum())
+    t = G(tgt)
+    t = t[0] if isinstance(t, tuple) else t
+    t = F.adaptive_avg_pool2d(t, (th, tw))
+    l_adv = bce(D(F.softmax(t, dim=1)), fake)
+    g_loss = l_seg + lambda_adv * l_adv
+    g_loss.backward()
+    optG.step()
+    optD.zero_grad()
+    with torch.no_grad():
+        fs = G(src)
+        fs = F.adaptive_avg_pool2d(fs[0] if isinstance(fs, tuple) else fs, (th, tw))
+        rs = G(tgt)
+        rs = F.adaptive_avg_pool2d(rs[0] if isinstance(rs, tuple) else rs, (th, tw))
+    d_real = bce(D(F.softmax(rs, dim=1)), real)
+    d_fake = bce(D(F.softmax(fs, dim=1)), fake)
+    d_loss = d_real + d_fake
+    d_loss.backward()
+    optD.step()
+    return {"loss_gen_source": float(l_seg), "loss_adversarial": float(l_adv),
+            "loss_gen_total": float(g_loss), "loss_disc_target": float(d_real),
+            "loss_disc_source": float(d_fake), "loss_disc_total": float(d_loss),
             "correct": correct, "total": lbl.numel()}

@@ -71,6 +71,8 @@ SIGNATURES = {
                                 c_int, c_float, P]),
     "rtsds_argmax": (c_int, [P, c_long, c_long, c_long, P, P, P, c_int, c_long, c_int, c_int, P]),
     "rtsds_confusion": (c_int, [P, P, P, c_long, c_int, P]),
+    "rtsds_adaptive_avgpool_fwd": (c_int, [P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, P]),
+    "rtsds_adaptive_avgpool_bwd": (c_int, [P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, P]),
     "rtsds_upce_workspace": (c_size_t, [c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_float]),
     "rtsds_upce_fwd": (c_int, [c_int, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_float,
                                c_int, P, P, P, c_int, c_int, P, c_size_t, P]),

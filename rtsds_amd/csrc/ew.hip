@@ -407,6 +407,78 @@ extern "C" int rtsds_chscale_bwd(const void* dy, const void* x, const void* a, v
   RET_LAUNCH();
 }
 
+// ------------------------------------------------------------------ adaptive average pool
+// ATen start/end indices: [floor(o*in/out), ceil((o+1)*in/out)).
+RT_DEV int ap_start(int o, int out, int in) { return (int)(((long)o * in) / out); }
+RT_DEV int ap_end(int o, int out, int in) { return (int)(((long)(o + 1) * in + out - 1) / out); }
+
+// One thread per (output pixel, channel); channels fastest -> coalesced NHWC access.
+template <typename T>
+__global__ void adaptive_avgpool_fwd_kernel(const T* __restrict__ x, T* __restrict__ y, int n, int hi, int wi, int c,
+                                            int ho, int wo) {
+  const long total = (long)n * ho * wo * c;
+  GRID_STRIDE(i, total) {
+    const int ch = (int)(i % c);
+    long q = i / c;
+    const int ow = (int)(q % wo);
+    q /= wo;
+    const int oh = (int)(q % ho);
+    const int img = (int)(q / ho);
+    const int h0 = ap_start(oh, ho, hi), h1 = ap_end(oh, ho, hi);
+    const int w0 = ap_start(ow, wo, wi), w1 = ap_end(ow, wo, wi);
+    const T* b = x + (long)img * hi * wi * c + ch;
+    float s = 0.f;
+    for (int h = h0; h < h1; ++h)
+      for (int w = w0; w < w1; ++w) s += to_f(b[((long)h * wi + w) * c]);
+    y[i] = from_f<T>(s / (float)((h1 - h0) * (w1 - w0)));
+  }
+}
+// dx[i] = sum over windows o containing i of dy[o] / area(o).  Window o covers input index i
+// iff start(o) <= i < end(o); every such o lies in [floor(i*out/in) - 1, ceil((i+1)*out/in)],
+// and each candidate is tested exactly.
+template <typename T>
+__global__ void adaptive_avgpool_bwd_kernel(const T* __restrict__ dy, T* __restrict__ dx, int n, int hi, int wi, int c,
+                                            int ho, int wo) {
+  const long total = (long)n * hi * wi * c;
+  GRID_STRIDE(i, total) {
+    const int ch = (int)(i % c);
+    long q = i / c;
+    const int iw = (int)(q % wi);
+    q /= wi;
+    const int ih = (int)(q % hi);
+    const int img = (int)(q / hi);
+    // candidate output rows: o with start(o) <= ih < end(o)
+    const int oh_lo = max(0, (int)(((long)ih * ho) / hi) - 1), oh_hi = min(ho - 1, (int)(((long)(ih + 1) * ho + hi - 1) / hi));
+    const int ow_lo = max(0, (int)(((long)iw * wo) / wi) - 1), ow_hi = min(wo - 1, (int)(((long)(iw + 1) * wo + wi - 1) / wi));
+    const T* b = dy + (long)img * ho * wo * c + ch;
+    float s = 0.f;
+    for (int oh = oh_lo; oh <= oh_hi; ++oh) {
+      const int h0 = ap_start(oh, ho, hi), h1 = ap_end(oh, ho, hi);
+      if (ih < h0 || ih >= h1) continue;
+      for (int ow = ow_lo; ow <= ow_hi; ++ow) {
+        const int w0 = ap_start(ow, wo, wi), w1 = ap_end(ow, wo, wi);
+        if (iw < w0 || iw >= w1) continue;
+        s += to_f(b[((long)oh * wo + ow) * c]) / (float)((h1 - h0) * (w1 - w0));
+      }
+    }
+    dx[i] = from_f<T>(s);
+  }
+}
+extern "C" int rtsds_adaptive_avgpool_fwd(const void* x, void* y, int n, int hi, int wi, int c, int ho, int wo, int dtype,
+                                          void* stream) {
+  if (n <= 0 || hi <= 0 || wi <= 0 || c <= 0 || ho <= 0 || wo <= 0) return RTSDS_ERR_SHAPE;
+  DISPATCH_T(dtype, hipLaunchKernelGGL(adaptive_avgpool_fwd_kernel<T>, dim3(ew_blocks((long)n * ho * wo * c)), dim3(256), 0,
+                                       (hipStream_t)stream, (const T*)x, (T*)y, n, hi, wi, c, ho, wo));
+  RET_LAUNCH();
+}
+extern "C" int rtsds_adaptive_avgpool_bwd(const void* dy, void* dx, int n, int hi, int wi, int c, int ho, int wo, int dtype,
+                                          void* stream) {
+  if (n <= 0 || hi <= 0 || wi <= 0 || c <= 0 || ho <= 0 || wo <= 0) return RTSDS_ERR_SHAPE;
+  DISPATCH_T(dtype, hipLaunchKernelGGL(adaptive_avgpool_bwd_kernel<T>, dim3(ew_blocks((long)n * hi * wi * c)), dim3(256), 0,
+                                       (hipStream_t)stream, (const T*)dy, (T*)dx, n, hi, wi, c, ho, wo));
+  RET_LAUNCH();
+}
+
 // ------------------------------------------------------------------ bilinear (align_corners=False)
 // bil_src (ATen source index, align_corners=False): common.h
 // Forward: one thread per (output pixel, channel chunk of CH); the 4 taps and weights are

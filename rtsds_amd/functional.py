@@ -620,6 +620,36 @@ def cross_entropy(x, target, ignore_index=-100):
     return CrossEntropyFn.apply(x, target, ignore_index)
 
 
+class AdaptiveAvgPoolFn(torch.autograd.Function):
+    """F.adaptive_avg_pool2d(x, (ho, wo)) (train.py:410,438,445), NHWC."""
+
+    @staticmethod
+    def forward(ctx, x, ho, wo):
+        require_hip(x)
+        x = nhwc(x)
+        n, c, hi, wi = x.shape
+        y = empty_nhwc(n, c, ho, wo, x.dtype, x.device)
+        lib.rtsds_adaptive_avgpool_fwd(_P(x), _P(y), n, hi, wi, c, ho, wo, dcode(x), stream())
+        ctx.geo = (n, c, hi, wi, ho, wo)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        n, c, hi, wi, ho, wo = ctx.geo
+        dy = nhwc(dy)
+        dx = empty_nhwc(n, c, hi, wi, dy.dtype, dy.device)
+        lib.rtsds_adaptive_avgpool_bwd(_P(dy), _P(dx), n, hi, wi, c, ho, wo, dcode(dy), stream())
+        return dx, None, None
+
+
+def adaptive_avg_pool2d(x, output_size):
+    """Identity (same tensor, as ATen's values) when the size already matches."""
+    ho, wo = (output_size, output_size) if isinstance(output_size, int) else output_size
+    if tuple(x.shape[-2:]) == (int(ho), int(wo)):
+        return x
+    return AdaptiveAvgPoolFn.apply(x, int(ho), int(wo))
+
+
 class UpsampleCrossEntropyFn(torch.autograd.Function):
     """sum_h CrossEntropy(interpolate_bilinear(head_h, (H, W)), target) without materialising
     the full-resolution logits (rtsds_upce_*; the chain it replaces is cited in the header).

@@ -122,10 +122,11 @@ class BiSeNet(torch.nn.Module):
                 nn.init.constant_(m.weight, 1)
                 nn.init.constant_(m.bias, 0)
 
-    def _heads(self, input):
+    def _heads(self, input, main_only=False):
         """Everything up to the final resizes: [(low-res logits, resize geometry), ...] --
         the main head (conv before up8, see below) then, in training, the two supervision
-        heads (build_bisenet.py:151-166)."""
+        heads (build_bisenet.py:151-166).  main_only: skip the supervision heads (1x1 convs
+        with no state; for callers that discard them, e.g. the DA target branch)."""
         x = to_input(input)
         sx = self.saptial_path(x)
         f3, f4, tail = self.context_path(x)
@@ -135,7 +136,8 @@ class BiSeNet(torch.nn.Module):
         cx1 = F.interpolate_bilinear(cx1, size=hw)
         cx2 = F.interpolate_bilinear(cx2, size=hw)
         heads = []
-        if self.training:
+        aux_on = self.training and not main_only
+        if aux_on:
             full = input.shape[-2:]
             s1, s2 = self.supervision1(cx1), self.supervision2(cx2)
             aux = [(s1, F.upsample_geometry(s1, size=full)), (s2, F.upsample_geometry(s2, size=full))]
@@ -149,15 +151,15 @@ class BiSeNet(torch.nn.Module):
             heads.append((main, F.upsample_geometry(main, scale_factor=8)))
         else:
             heads.append((result, None))
-        if self.training:
+        if aux_on:
             heads += aux
         return heads
 
-    def forward_lowres(self, input):
+    def forward_lowres(self, input, main_only=False):
         """Training-loop entry used by rtsds_amd.train: the heads before their final bilinear
         resize, so the resize can be fused into the loss (functional.upsample_cross_entropy).
         forward() is exactly these heads, resized."""
-        return self._heads(input)
+        return self._heads(input, main_only)
 
     def forward(self, input):
         outs = [t if geo is None else F.interpolate_geometry(t, geo) for t, geo in self._heads(input)]

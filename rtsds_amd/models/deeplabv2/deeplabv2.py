@@ -99,7 +99,7 @@ class ResNetMulti(nn.Module):
             layers.append(block(self.inplanes, planes, dilation=dilation))
         return nn.Sequential(*layers)
 
-    def forward_lowres(self, x):
+    def forward_lowres(self, x, main_only=False):
         """[(stride-8 logits, resize geometry)] -- forward() before its final bilinear resize
         (deeplabv2.py:126), so the training loop can fuse the resize into the loss."""
         _, _, H, W = x.size()

@@ -106,31 +106,64 @@ def train(epoch: int, model: torch.nn.Module, train_loader, criterion: torch.nn.
     return model
 
 
+def _main_output(model, x):
+    """The model's main (first) output at full resolution; auxiliary heads that the caller
+    would discard are not computed when the model exposes forward_lowres (they hold no state)."""
+    if hasattr(model, "forward_lowres"):
+        (t, geo), = model.forward_lowres(x, main_only=True)
+        return F.interpolate_geometry(t, geo) if geo is not None else t
+    out = model(x)
+    return out[0] if isinstance(out, tuple) else out
+
+
+def _seg_loss(model, criterion, x, label, correct):
+    """Sum over the model's heads of criterion(head, label) (train.py:86-92, 196-204, 392-399)
+    plus head 0's pixel matches added to ``correct``.  Returns (loss, low-res main head and its
+    resize geometry, or the full-resolution main output with geometry None)."""
+    fused = _fused_heads(model, criterion, x)
+    if fused is not None and fused[1] is not None:
+        heads, geo = fused
+        loss = F.upsample_cross_entropy(heads, label, geo, criterion.ignore_index, correct)
+        return loss, heads[0], geo
+    if fused is not None:
+        outs = fused[0]
+    else:
+        out = model(x)
+        outs = list(out) if isinstance(out, tuple) else [out]
+    loss = None
+    for o in outs:
+        if o is None:  # DeepLab returns (x, None, None) (deeplabv2.py:128-129)
+            continue
+        l = criterion(o, label)
+        loss = l if loss is None else loss + l
+    F.argmax_channels(outs[0].detach(), label, correct, want_map=False)
+    return loss, outs[0], None
+
+
+def _full(t, geo):
+    return F.interpolate_geometry(t, geo) if geo is not None else t
+
+
 def da_step(generator, discriminator, generator_optimizer, discriminator_optimizer,
             generator_loss, discriminator_loss, source_image, source_label, target_image,
             lambda_, iterations):
     """One adversarial_train iteration body (train.py:174-275, LR scheduling excluded).
-    Returns device tensors (l_seg, l_adv, l_dsrc, l_dtgt, correct)."""
+    Returns device tensors (l_seg, l_adv, l_dsrc, l_dtgt, correct).  The source heads' resizes
+    run fused into their cross-entropy; the discriminator consumes the detached main output,
+    so it is resized without a gradient graph."""
     generator_optimizer.zero_grad()
     discriminator_optimizer.zero_grad()
     # the discriminator is frozen while the generator trains (train.py:192-193)
     for p in discriminator.parameters():
         p.requires_grad = False
-    out = generator(source_image)
-    if isinstance(out, tuple):
-        loss_seg = generator_loss(out[0], source_label)
-        for aux in out[1:]:
-            if aux is not None:  # DeepLab returns (x, None, None) (deeplabv2.py:128-129)
-                loss_seg = loss_seg + generator_loss(aux, source_label)
-        source_features = out[0]
-    else:
-        loss_seg = generator_loss(out, source_label)
-        source_features = out
+    correct = torch.zeros(1, dtype=torch.int64, device=source_image.device)
+    loss_seg, main, geo = _seg_loss(generator, generator_loss, source_image, source_label, correct)
     loss_seg = loss_seg / iterations
     loss_seg.backward()
+    with torch.no_grad():
+        source_features = _full(main.detach(), geo)
 
-    tout = generator(target_image)
-    target_feature = tout[0] if isinstance(tout, tuple) else tout
+    target_feature = _main_output(generator, target_image)
     pred_t = discriminator(F.softmax(target_feature, dim=1))
     ones = torch.ones(pred_t.size(), device=pred_t.device)
     loss_adv = lambda_ * discriminator_loss(pred_t, ones) / iterations
@@ -138,7 +171,6 @@ def da_step(generator, discriminator, generator_optimizer, discriminator_optimiz
 
     for p in discriminator.parameters():
         p.requires_grad = True
-    source_features = source_features.detach()
     target_feature = target_feature.detach()
     pred_s = discriminator(F.softmax(source_features, dim=1))
     loss_dsrc = discriminator_loss(pred_s, torch.ones(pred_s.size(), device=pred_s.device)) / iterations
@@ -149,9 +181,52 @@ def da_step(generator, discriminator, generator_optimizer, discriminator_optimiz
 
     generator_optimizer.step()
     discriminator_optimizer.step()
-    correct = torch.zeros(1, dtype=torch.int64, device=source_features.device)
-    F.argmax_channels(source_features, source_label, correct, want_map=False)
     return loss_seg.detach(), loss_adv.detach(), loss_dsrc.detach(), loss_dtgt.detach(), correct
+
+
+def da2_step(generator, discriminator, generator_optimizer, discriminator_optimizer,
+             generator_loss, discriminator_loss, source_image, source_label, target_image,
+             lambda_adv):
+    """One adversarial_train_2 iteration body (train.py:373-466, LR scheduling excluded):
+    G step on L_seg(source) + lambda_adv * BCE(D(softmax(pool(G(target)))), 0), then a D step
+    on BCE(D(softmax(pool(G(target)))), 1) + BCE(D(softmax(pool(G(source)))), 0) with both
+    generator outputs recomputed under no_grad (train mode).  pool = adaptive_avg_pool2d to
+    the target size.  D's parameter gradients of the G step are discarded by the reference
+    (zero_grad before the D step), so D is frozen there.  Returns device tensors (l_seg,
+    l_adv, g_total, d_real, d_fake, d_total, correct)."""
+    th, tw = int(target_image.shape[2]), int(target_image.shape[3])
+    b = int(target_image.shape[0])
+    dev = target_image.device
+    real_labels = torch.ones(b, 1, 1, 1, device=dev)
+    fake_labels = torch.zeros(b, 1, 1, 1, device=dev)
+
+    generator_optimizer.zero_grad()
+    for p in discriminator.parameters():
+        p.requires_grad = False
+    correct = torch.zeros(1, dtype=torch.int64, device=dev)
+    g_loss_seg, _, _ = _seg_loss(generator, generator_loss, source_image, source_label, correct)
+    real_seg = F.adaptive_avg_pool2d(_main_output(generator, target_image), (th, tw))
+    d_real_output = discriminator(F.softmax(real_seg, dim=1))
+    loss_adv = discriminator_loss(d_real_output, fake_labels)
+    g_loss = g_loss_seg + lambda_adv * loss_adv
+    g_loss.backward()
+    generator_optimizer.step()
+    for p in discriminator.parameters():
+        p.requires_grad = True
+
+    discriminator_optimizer.zero_grad()
+    with torch.no_grad():
+        fake_seg = F.adaptive_avg_pool2d(_main_output(generator, source_image), (th, tw))
+        real_seg = F.adaptive_avg_pool2d(_main_output(generator, target_image), (th, tw))
+    d_real_output = discriminator(F.softmax(real_seg, dim=1))
+    d_fake_output = discriminator(F.softmax(fake_seg, dim=1))
+    d_real_loss = discriminator_loss(d_real_output, real_labels)
+    d_fake_loss = discriminator_loss(d_fake_output, fake_labels)
+    d_loss = d_real_loss + d_fake_loss
+    d_loss.backward()
+    discriminator_optimizer.step()
+    return (g_loss_seg.detach(), loss_adv.detach(), g_loss.detach(), d_real_loss.detach(),
+            d_fake_loss.detach(), d_loss.detach(), correct)
 
 
 def adversarial_train(iterations: int, epochs: int, generator: torch.nn.Module,
@@ -219,4 +294,76 @@ def adversarial_train(iterations: int, epochs: int, generator: torch.nn.Module,
         cb.on_train_end()
 
 
-__all__ = ["train", "adversarial_train", "seg_step", "da_step", "Callback"]
+def adversarial_train_2(iterations: int, epochs: int, generator: torch.nn.Module,
+                        discriminator: torch.nn.Module, generator_optimizer, discriminator_optimizer,
+                        source_dataloader, target_dataloader, generator_loss: torch.nn.Module,
+                        discriminator_loss: torch.nn.Module, lambda_: float, gen_init_lr: float,
+                        gen_power: float, dis_power: float, dis_init_lr: float,
+                        lr_decay_iter: float, num_classes: int, class_names: list, val_loader,
+                        do_validation: int = 1, device: str = "cuda", when_print: int = 10,
+                        callbacks: list = []):
+    """Second adversarial loop (train.py:322-500): D trained on real (target) vs fake (source)
+    segmentations pooled to the target size, inverted adversarial label, lambda schedule
+    max(lambda, 10 lambda - 0.001 epoch).  Reference behaviour kept: both learning rates use
+    ``dis_power`` (train.py:385-386), best-mIoU is reset every epoch, validation skips
+    epoch 0."""
+    dis_lr = gen_lr = None
+    for epoch in range(epochs):
+        generator.train()
+        discriminator.train()
+        run = {"loss_gen_source": 0.0, "loss_adversarial": 0.0, "loss_gen_total": 0.0,
+               "loss_disc_target": 0.0, "loss_disc_source": 0.0, "loss_disc_total": 0.0}
+        g_correct, g_total = 0, 0
+        best_mIoU = 0.0
+        max_iter = epochs * iterations
+        lambda_adv = max(lambda_, (lambda_ * 10) - 0.001 * epoch)
+        for i in tqdm(range(iterations), total=iterations, desc=f"Epoch {epoch}"):
+            source_image, source_label = next(iter(source_dataloader))
+            target_image, _ = next(iter(target_dataloader))
+            source_image, source_label = source_image.to(device), source_label.to(device)
+            source_label = source_label.squeeze(1)
+            target_image = target_image.to(device)
+            current_iter = epoch * iterations + i
+            if current_iter % lr_decay_iter == 0 and current_iter <= max_iter:
+                dis_lr = utils.poly_lr_scheduler(discriminator_optimizer, dis_init_lr, current_iter,
+                                                 lr_decay_iter, max_iter, dis_power)
+                gen_lr = utils.poly_lr_scheduler(generator_optimizer, gen_init_lr, current_iter,
+                                                 lr_decay_iter, max_iter, dis_power)
+            *losses, corr = da2_step(generator, discriminator, generator_optimizer,
+                                     discriminator_optimizer, generator_loss, discriminator_loss,
+                                     source_image, source_label, target_image, lambda_adv)
+            vals = torch.stack([l.double() for l in losses] + [corr[0].double()]).tolist()
+            for k, v in zip(("loss_gen_source", "loss_adversarial", "loss_gen_total",
+                             "loss_disc_target", "loss_disc_source", "loss_disc_total"), vals):
+                run[k] += v
+            g_correct += int(vals[6])
+            g_total += source_label.size(0) * source_label.size(1) * source_label.size(2)
+        print(f"Epoch Results {epoch}")
+        utils.tabular_print({"Genrator Accuracy": (100.0 * g_correct / g_total),
+                             "dis_lr": dis_lr if dis_lr else -1, "gen_lr": gen_lr if gen_lr else -1})
+        for cb in callbacks:
+            cb.on_epoch_end(epoch, {
+                "dis_lr": dis_lr if dis_lr else -1, "gen_lr": gen_lr if gen_lr else -1,
+                "loss_gen_source": run["loss_gen_source"] / iterations,
+                "loss_adversarial": run["loss_adversarial"] / iterations,
+                "loss_disc_source": run["loss_disc_source"] / iterations,
+                "loss_disc_target": run["loss_disc_target"] / iterations,
+                "loss_disc_total": run["loss_disc_total"] / iterations,
+                "loss_gen_total": run["loss_gen_total"] / iterations,
+                "Genrator Accuracy": 100.0 * g_correct / g_total})
+        if do_validation != -1 and epoch % do_validation == 0 and epoch != 0:
+            print("-" * 50, "Validation", "-" * 50)
+            validation_mIou, _ = val_GTA5(epoch, generator, val_loader, num_classes, class_names,
+                                          callbacks, device=device)
+            print("-" * 100)
+            if validation_mIou > best_mIoU:
+                best_mIoU = validation_mIou
+                torch.save(generator.state_dict(), "best_generator.pth")
+                torch.save(discriminator.state_dict(), "best_discriminator.pth")
+                print(f"Best Model Saved at Epoch {epoch}")
+    for cb in callbacks:
+        cb.on_train_end()
+
+
+__all__ = ["train", "adversarial_train", "adversarial_train_2", "seg_step", "da_step", "da2_step",
+           "Callback"]

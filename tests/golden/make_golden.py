@@ -95,7 +95,9 @@ def save(name, arrays, meta):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
+    ap.add_argument("--only", default="", help="comma-separated fixture groups (default: all)")
     args = ap.parse_args()
+    only = set(filter(None, args.only.split(",")))
     sys.dont_write_bytecode = True
     install_stubs()
     sys.path.insert(0, args.ref)
@@ -106,6 +108,11 @@ def main():
     from models.deeplabv2.deeplabv2 import get_deeplab_v2
     from models.domain_shift.adversarial.model import DomainDiscriminator, TinyDomainDiscriminator
     import train as ref_train
+
+    if only:
+        if "da2" in only:
+            make_da2(ref_train, BiSeNet, TinyDomainDiscriminator)
+        return
 
     keys = {}
     # ---------------- BiSeNet-R18: config 1 shape (2x3x128x256), train + eval
@@ -206,9 +213,46 @@ def main():
                                   if k.endswith("running_mean")}
     save("da_iter_c1", arrays, meta)
 
+    make_da2(ref_train, BiSeNet, TinyDomainDiscriminator)
+
     with open(os.path.join(HERE, "state_dict_keys.json"), "w") as f:
         json.dump(keys, f)
     print("wrote state_dict_keys.json")
+
+
+def make_da2(ref_train, BiSeNet, TinyDomainDiscriminator):
+    """adversarial_train_2 (train.py:322-500): 2 epochs x 1 iteration, source images larger
+    than the target (exercises adaptive_avg_pool2d), validation at epoch 1."""
+    torch.manual_seed(42)
+    g = apply_recipe(BiSeNet(19, "resnet18"), seed=1)
+    d = apply_recipe(TinyDomainDiscriminator(19), seed=2)
+    og = torch.optim.Adam(g.parameters(), lr=1e-4)
+    od = torch.optim.Adam(d.parameters(), lr=1e-4, weight_decay=1e-4)
+    xs = synthetic_images(2, 160, 320, seed=47)
+    ys = synthetic_labels(2, 160, 320, seed=48)
+    xt = synthetic_images(2, 128, 256, seed=46)
+    yt = synthetic_labels(2, 128, 256, seed=43)
+    cap = Capture()
+    cwd = os.getcwd()
+    with tempfile.TemporaryDirectory() as tmp:
+        os.chdir(tmp)
+        try:
+            ref_train.adversarial_train_2(
+                iterations=1, epochs=2, generator=g, discriminator=d, generator_optimizer=og,
+                discriminator_optimizer=od, source_dataloader=[(xs, ys.unsqueeze(1))],
+                target_dataloader=[(xt, yt.unsqueeze(1))], generator_loss=torch.nn.CrossEntropyLoss(ignore_index=19),
+                discriminator_loss=torch.nn.BCEWithLogitsLoss(), lambda_=0.1, gen_init_lr=1e-4,
+                gen_power=0.9, dis_power=0.05, dis_init_lr=1e-4, lr_decay_iter=1,
+                num_classes=19, class_names=[str(i) for i in range(19)],
+                val_loader=[(xt, yt.unsqueeze(1))], do_validation=1, callbacks=[cap])
+        finally:
+            os.chdir(cwd)
+    arrays, meta = {}, {"epochs": cap.epochs, "val_mIoU": float(cap.val["validation_mIoU"])}
+    param_summary(arrays, meta, "gparam", dict(g.named_parameters()))
+    param_summary(arrays, meta, "dparam", dict(d.named_parameters()))
+    meta["g_running_mean_sum"] = {k: float(v.double().sum()) for k, v in g.state_dict().items()
+                                  if k.endswith("running_mean")}
+    save("da2_c1", arrays, meta)
 
 
 if __name__ == "__main__":

@@ -278,3 +278,57 @@ def test_da_iterations_match_reference_adversarial_train(inputs, golden, tmp_pat
     ours = {k: v.detach().cpu() - p0[k] for k, v in list(g.named_parameters()) + list(d.named_parameters())}
     print("DA param-update worst:", _noise_bounded(ours, upd[torch.float32], upd[torch.float64],
                                                    "DA update", floor=1e-2))
+
+
+def test_da2_epochs_match_reference_adversarial_train_2(golden, tmp_path, monkeypatch):
+    """adversarial_train_2 (train.py:322-500): 2 epochs x 1 iteration, source 160x320 pooled to
+    the 128x256 target (adaptive_avg_pool2d), inverted adversarial label, lambda schedule,
+    both LRs on dis_power, validation at epoch 1."""
+    arrays, meta = golden("da2_c1")
+    xs, ys = synthetic_images(2, 160, 320, seed=47), synthetic_labels(2, 160, 320, seed=48)
+    xt, yt = synthetic_images(2, 128, 256, seed=46), synthetic_labels(2, 128, 256, seed=43)
+    g = _load(BiSeNet(19, "resnet18"), 1).to(DEV)
+    d = _load(TinyDomainDiscriminator(19), 2).to(DEV)
+    og = optim.Adam(g.parameters(), lr=1e-4)
+    od = optim.Adam(d.parameters(), lr=1e-4, weight_decay=1e-4)
+    from tests.golden.make_golden import Capture
+    cap = Capture()
+    monkeypatch.chdir(tmp_path)
+    with rtsds_amd.precision(torch.float32):
+        rtrain.adversarial_train_2(
+            iterations=1, epochs=2, generator=g, discriminator=d, generator_optimizer=og,
+            discriminator_optimizer=od, source_dataloader=[(xs, ys.unsqueeze(1))],
+            target_dataloader=[(xt, yt.unsqueeze(1))],
+            generator_loss=losses.CrossEntropyLoss(ignore_index=19),
+            discriminator_loss=losses.BCEWithLogitsLoss(), lambda_=0.1, gen_init_lr=1e-4,
+            gen_power=0.9, dis_power=0.05, dis_init_lr=1e-4, lr_decay_iter=1, num_classes=19,
+            class_names=[str(i) for i in range(19)], val_loader=[(xt, yt.unsqueeze(1))],
+            do_validation=1, callbacks=[cap])
+    assert len(cap.epochs) == 2
+    for got, want in zip(cap.epochs, meta["epochs"]):
+        for k, v in want.items():
+            assert abs(got[k] - v) <= 2e-4 * abs(v) + 1e-6, (k, got[k], v)
+    assert abs(cap.val["validation_mIoU"] - meta["val_mIoU"]) < 2e-3
+    assert (tmp_path / "best_generator.pth").exists()
+    from oracle import steps as osteps
+    upd = {}
+    for dt in (torch.float64, torch.float32):
+        g_ = _load(om.BiSeNet(19, "resnet18"), 1).to(dt).train()
+        d_ = _load(om.TinyDomainDiscriminator(19), 2).to(dt).train()
+        p0 = {k: v.detach().clone() for k, v in list(g_.named_parameters()) + list(d_.named_parameters())}
+        o1 = torch.optim.Adam(g_.parameters(), lr=1e-4)
+        o2 = torch.optim.Adam(d_.parameters(), lr=1e-4, weight_decay=1e-4)
+        for epoch in range(2):
+            g_.train()
+            osteps.poly_lr(o2, 1e-4, epoch, 2, 0.05)
+            osteps.poly_lr(o1, 1e-4, epoch, 2, 0.05)
+            osteps.da2_step(g_, d_, o1, o2, torch.nn.CrossEntropyLoss(ignore_index=19),
+                            torch.nn.BCEWithLogitsLoss(), xs.to(dt), ys, xt.to(dt),
+                            max(0.1, 1.0 - 0.001 * epoch))
+        upd[dt] = {k: v.detach() - p0[k] for k, v in list(g_.named_parameters()) + list(d_.named_parameters())}
+    g0 = _load(BiSeNet(19, "resnet18"), 1)
+    d0 = _load(TinyDomainDiscriminator(19), 2)
+    p0 = {k: v.detach() for k, v in list(g0.named_parameters()) + list(d0.named_parameters())}
+    ours = {k: v.detach().cpu() - p0[k] for k, v in list(g.named_parameters()) + list(d.named_parameters())}
+    print("DA2 param-update worst:", _noise_bounded(ours, upd[torch.float32], upd[torch.float64],
+                                                    "DA2 update", floor=1e-2))

@@ -285,6 +285,27 @@ def test_softmax_ce_argmax(dt):
     assert int(correct.item()) == int((ref == t).sum())
 
 
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("sizes", [((20, 40), (16, 32)), ((23, 37), (10, 13)), ((9, 9), (4, 7)),
+                                   ((16, 32), (16, 32))])
+def test_adaptive_avg_pool(sizes, dt):
+    """F.adaptive_avg_pool2d (train.py:410,438,445) forward/backward vs ATen fp64."""
+    (hi, wi), (ho, wo) = sizes
+    g = torch.Generator().manual_seed(31)
+    x = torch.randn(2, 19, hi, wi, generator=g, dtype=torch.float64)
+    if dt == torch.bfloat16:
+        x = x.bfloat16().double()
+    xr = x.clone().requires_grad_()
+    yr = TF.adaptive_avg_pool2d(xr, (ho, wo))
+    gy = torch.randn(yr.shape, generator=g, dtype=torch.float64)
+    yr.backward(gy)
+    xd = _dev(x, dt).requires_grad_()
+    y = F.adaptive_avg_pool2d(xd, (ho, wo))
+    y.backward(_dev(gy, dt))
+    _close(y, yr, dt, "y", 1e-5 if dt == torch.float32 else None)
+    _close(xd.grad, xr.grad, dt, "dx", 1e-5 if dt == torch.float32 else None)
+
+
 def _upce_reference(heads, t, geo_args, ignore):
     """fp64 torch: sum_h CE(interpolate(head_h)), grads, and head-0 argmax matches."""
     hr = [h.clone().requires_grad_() for h in heads]
