@@ -171,6 +171,9 @@ int rtsds_softmax_bwd(const void* dy, const void* y, int ld, void* dx, long sn, 
 /* nn.CrossEntropyLoss(ignore_index) mean over valid pixels (main.py:124-130).  The forward
  * leaves the valid count at ((float*)ws)[2048]; pass that pointer as `count` to the bwd.  */
 size_t rtsds_ce_workspace(void);
+/* ws + 2048 floats holds (valid count C, loss sum S); rtsds_ce_finish sets loss = S / C after
+ * the caller summed C over data-parallel ranks (the backward reads the same C).           */
+int rtsds_ce_finish(const void* ws, float* loss, void* stream);
 int rtsds_ce_fwd(const void* x, long sn, long sc, long shw, const int64_t* target, float* loss, int n,
                  long hw, int c, int ignore_index, int dtype, void* ws, size_t ws_bytes, void* stream);
 int rtsds_ce_bwd(const void* x, long sn, long sc, long shw, const int64_t* target,
@@ -216,6 +219,12 @@ int rtsds_upce_fwd(int nheads, const void* const* logits, const int64_t* target,
                    int wl, int c, int H, int W, float scale_h, float scale_w, int ignore_index,
                    float* loss, float* loss_sum, unsigned long long* correct, int want_grad,
                    int dtype, void* ws, size_t ws_bytes, void* stream);
+/* Data-parallel global mean: ws starts with float stat[1 + nheads] = (valid-pixel count,
+ * per-head loss sums).  After the caller sums stat[0] over ranks (a 1-element all-reduce),
+ * rtsds_upce_finish recomputes loss / loss_sum = this rank's sums / global count, and
+ * rtsds_upce_bwd scales by the global count: the ranks' losses and gradients sum to the
+ * single-device mean over the gathered batch exactly.                                     */
+int rtsds_upce_finish(int nheads, const void* ws, float* loss, float* loss_sum, void* stream);
 int rtsds_upce_bwd(int nheads, const float* grad_loss, int grad_stride, void* const* dlogits,
                    int n, int hl, int wl, int c, int H, int W, float scale_h, float scale_w,
                    int dtype, const void* ws, size_t ws_bytes, void* stream);

@@ -73,6 +73,8 @@ SIGNATURES = {
     "rtsds_confusion": (c_int, [P, P, P, c_long, c_int, P]),
     "rtsds_adaptive_avgpool_fwd": (c_int, [P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, P]),
     "rtsds_adaptive_avgpool_bwd": (c_int, [P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, P]),
+    "rtsds_upce_finish": (c_int, [c_int, P, P, P, P]),
+    "rtsds_ce_finish": (c_int, [P, P, P]),
     "rtsds_upce_workspace": (c_size_t, [c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_float]),
     "rtsds_upce_fwd": (c_int, [c_int, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_float,
                                c_int, P, P, P, c_int, c_int, P, c_size_t, P]),

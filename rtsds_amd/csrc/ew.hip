@@ -806,8 +806,12 @@ __global__ void ce_fwd_final_kernel(float* __restrict__ part, int nb, float* __r
   if (threadIdx.x == 0) {
     const float S = rs[0] + rs[1] + rs[2] + rs[3], C = rc[0] + rc[1] + rc[2] + rc[3];
     part[2 * kCeRB] = C;
+    part[2 * kCeRB + 1] = S;
     loss[0] = S / C;
   }
+}
+__global__ void ce_finish_kernel(const float* __restrict__ part, float* __restrict__ loss) {
+  if (threadIdx.x == 0) loss[0] = part[2 * kCeRB + 1] / part[2 * kCeRB];
 }
 template <typename T>
 __global__ void ce_bwd_kernel(const T* __restrict__ x, const int64_t* __restrict__ tgt, const float* __restrict__ gout,
@@ -916,6 +920,11 @@ extern "C" int rtsds_ce_fwd(const void* x, long sn, long sc, long shw, const int
       hipLaunchKernelGGL(ce_fwd_part_kernel<T>, dim3(nb), dim3(256), 0, st, (const T*)x, tgt, (float*)ws, n, hw, c, sn, sc, shw, ignore_index);
   });
   hipLaunchKernelGGL(ce_fwd_final_kernel, dim3(1), dim3(256), 0, st, (float*)ws, nb, loss);
+  RET_LAUNCH();
+}
+// loss = S / C with C summed by the caller over data-parallel ranks (ws + 2*1024 floats: C, S).
+extern "C" int rtsds_ce_finish(const void* ws, float* loss, void* stream) {
+  hipLaunchKernelGGL(ce_finish_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, (const float*)ws, loss);
   RET_LAUNCH();
 }
 // count = the valid-pixel count written by rtsds_ce_fwd into its workspace (ws + 2*1024 floats).

@@ -307,8 +307,19 @@ __global__ void __launch_bounds__(256) upce_fwd_kernel(UpceArgs a) {
   }
 }
 
-// loss[h] = sum_b lpart[h][b] / sum_b cpart[b];  *loss_sum = ((loss[0] + loss[1]) + ...) in
-// head order (the reference's left-to-right sum of the head losses);  count -> stat[0].
+// stat[0] = valid-pixel count, stat[1 + h] = head h's loss sum (deterministic block sums);
+// then loss[h] = stat[1 + h] / stat[0], *loss_sum = ((loss[0] + loss[1]) + ...) in head order
+// (the reference's left-to-right sum of the head losses).  rtsds_upce_finish re-runs the
+// second half after the caller has summed the count stat[0] over data-parallel ranks.
+RT_DEV void upce_losses(const float* stat, int nheads, float* loss, float* loss_sum) {
+  float total = 0.f;
+  for (int h = 0; h < nheads; ++h) {
+    const float l = stat[1 + h] / stat[0];
+    total = h == 0 ? l : total + l;
+    if (loss) loss[h] = l;
+  }
+  if (loss_sum) loss_sum[0] = total;
+}
 __global__ void __launch_bounds__(256) upce_final_kernel(const float* __restrict__ lpart, const float* __restrict__ cpart, int nblocks,
                                                          int nheads, float* __restrict__ loss, float* __restrict__ loss_sum,
                                                          float* __restrict__ stat) {
@@ -316,19 +327,18 @@ __global__ void __launch_bounds__(256) upce_final_kernel(const float* __restrict
   float c = 0.f;
   for (int b = threadIdx.x; b < nblocks; b += 256) c += cpart[b];
   c = upce_block_sum(c, red);
-  float total = 0.f;
+  if (threadIdx.x == 0) stat[0] = c;
   for (int h = 0; h < nheads; ++h) {
     float s = 0.f;
     for (int b = threadIdx.x; b < nblocks; b += 256) s += lpart[(long)h * nblocks + b];
     s = upce_block_sum(s, red);
-    const float l = s / c;
-    total = h == 0 ? l : total + l;
-    if (threadIdx.x == 0 && loss) loss[h] = l;
+    if (threadIdx.x == 0) stat[1 + h] = s;
   }
-  if (threadIdx.x == 0) {
-    if (loss_sum) loss_sum[0] = total;
-    stat[0] = c;
-  }
+  if (threadIdx.x == 0) upce_losses(stat, nheads, loss, loss_sum);
+}
+__global__ void upce_finish_kernel(const float* __restrict__ stat, int nheads, float* __restrict__ loss,
+                                   float* __restrict__ loss_sum) {
+  if (threadIdx.x == 0) upce_losses(stat, nheads, loss, loss_sum);
 }
 
 struct UpceBwdArgs {
@@ -397,10 +407,11 @@ static size_t upce_lds(const UpceGeo& g) {
   return (tile_el + 4 * (size_t)(g.tw + 1) * cp + 4 * (size_t)g.wmax * cp + (size_t)(g.tw + 1) * g.wmax + 4 * (size_t)g.wmax + 2 * (size_t)(g.tw + 1)) * 4;
 }
 static size_t upce_tile_el(const UpceGeo& g) { return (size_t)(g.th + 1) * (g.tw + 1) * g.c; }
-// ws: [heads][nblocks][tile_el] gradient partials | [heads][nblocks] loss partials |
-//     [nblocks] counts | stat[64]
+// ws: stat[64] (count, per-head loss sums; offset 0, see the header) | [heads][nblocks][tile_el]
+//     gradient partials | [heads][nblocks] loss partials | [nblocks] counts
+static const size_t kUpceStat = 64;
 static size_t upce_ws_floats(const UpceGeo& g, int heads) {
-  return (size_t)heads * g.nblocks * upce_tile_el(g) + (size_t)heads * g.nblocks + g.nblocks + 64;
+  return kUpceStat + (size_t)heads * g.nblocks * upce_tile_el(g) + (size_t)heads * g.nblocks + g.nblocks;
 }
 
 extern "C" size_t rtsds_upce_workspace(int nheads, int n, int hl, int wl, int c, int H, int W, float scale_h, float scale_w) {
@@ -419,7 +430,8 @@ extern "C" int rtsds_upce_fwd(int nheads, const void* const* logits, const int64
   if (!upce_plan(n, hl, wl, c, H, W, scale_h, scale_w, g)) return RTSDS_ERR_UNSUPPORTED;
   if (ws_bytes < rtsds_upce_workspace(nheads, n, hl, wl, c, H, W, scale_h, scale_w) || !ws) return RTSDS_ERR_WORKSPACE;
   UpceArgs a;
-  float* f = (float*)ws;
+  float* stat = (float*)ws;
+  float* f = stat + kUpceStat;
   const size_t te = upce_tile_el(g);
   for (int h = 0; h < kUpceMaxHeads; ++h) {
     a.x[h] = h < nheads ? logits[h] : nullptr;
@@ -427,7 +439,6 @@ extern "C" int rtsds_upce_fwd(int nheads, const void* const* logits, const int64
   }
   a.lpart = f + (size_t)nheads * g.nblocks * te;
   a.cpart = a.lpart + (size_t)nheads * g.nblocks;
-  float* stat = a.cpart + g.nblocks;
   a.tgt = target;
   a.correct = correct;
   a.g = g;
@@ -458,7 +469,7 @@ extern "C" int rtsds_upce_bwd(int nheads, const float* grad_loss, int grad_strid
   if (!upce_plan(n, hl, wl, c, H, W, scale_h, scale_w, g)) return RTSDS_ERR_UNSUPPORTED;
   if (ws_bytes < rtsds_upce_workspace(nheads, n, hl, wl, c, H, W, scale_h, scale_w) || !ws) return RTSDS_ERR_WORKSPACE;
   UpceBwdArgs a;
-  const float* f = (const float*)ws;
+  const float* f = (const float*)ws + kUpceStat;
   const size_t te = upce_tile_el(g);
   for (int h = 0; h < kUpceMaxHeads; ++h) {
     a.gpart[h] = h < nheads ? f + (size_t)h * g.nblocks * te : nullptr;
@@ -466,7 +477,7 @@ extern "C" int rtsds_upce_bwd(int nheads, const float* grad_loss, int grad_strid
   }
   a.gout = grad_loss;
   a.gstride = grad_stride;
-  a.count = f + (size_t)nheads * g.nblocks * te + (size_t)nheads * g.nblocks + g.nblocks;
+  a.count = (const float*)ws;  // stat[0]
   a.g = g;
   a.nheads = nheads;
   const long total = (long)nheads * n * hl * wl * c;
@@ -475,5 +486,11 @@ extern "C" int rtsds_upce_bwd(int nheads, const float* grad_loss, int grad_strid
   if (dtype == RTSDS_BF16) hipLaunchKernelGGL(upce_bwd_kernel<bf16>, dim3(blocks), dim3(256), 0, st, a);
   else if (dtype == RTSDS_F32) hipLaunchKernelGGL(upce_bwd_kernel<float>, dim3(blocks), dim3(256), 0, st, a);
   else return RTSDS_ERR_UNSUPPORTED;
+  return hipGetLastError() == hipSuccess ? RTSDS_OK : RTSDS_ERR_LAUNCH;
+}
+
+extern "C" int rtsds_upce_finish(int nheads, const void* ws, float* loss, float* loss_sum, void* stream) {
+  if (nheads <= 0 || nheads > kUpceMaxHeads || !ws) return RTSDS_ERR_UNSUPPORTED;
+  hipLaunchKernelGGL(upce_finish_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, (const float*)ws, nheads, loss, loss_sum);
   return hipGetLastError() == hipSuccess ? RTSDS_OK : RTSDS_ERR_LAUNCH;
 }

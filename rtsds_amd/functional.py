@@ -11,7 +11,7 @@ import numpy as np
 import torch
 
 from ._lib import ACT_SIGMOID, ConvDesc, lib
-from .runtime import CL, dcode, empty_nhwc, nhwc, require_hip, stream, workspace
+from .runtime import CL, dcode, dp_world, empty_nhwc, nhwc, require_hip, stream, workspace
 
 _P = lambda t: None if t is None else t.data_ptr()  # noqa: E731
 
@@ -599,6 +599,10 @@ class CrossEntropyFn(torch.autograd.Function):
         ws = workspace(lib.rtsds_ce_workspace(), x.device)
         lib.rtsds_ce_fwd(_P(x), sn, sc, shw, _P(target), _P(loss), n, h * w, c, ignore_index,
                          dcode(x), _P(ws), ws.numel(), stream())
+        if dp_world() > 1:  # global-batch mean: local loss sum over the all-reduced count
+            import torch.distributed as dist
+            dist.all_reduce(ws.view(torch.float32)[2048:2049])
+            lib.rtsds_ce_finish(_P(ws), _P(loss), stream())
         ctx.ignore = ignore_index
         ctx.save_for_backward(x, target, ws)
         return loss
@@ -669,6 +673,13 @@ class UpsampleCrossEntropyFn(torch.autograd.Function):
         want = any(ctx.needs_input_grad[4:])
         lib.rtsds_upce_fwd(k, ptrs, _P(target), n, hl, wl, c, H, W, sh, sw, ignore_index, _P(per_head),
                            _P(total), _P(correct), int(want), dt, _P(ws), ws.numel(), stream())
+        if dp_world() > 1:
+            # global-batch mean: this rank's loss sums over the all-reduced valid-pixel count
+            # (its contribution; the ranks' losses and gradients then SUM to the single-device
+            # values, see runtime.dp_world)
+            import torch.distributed as dist
+            dist.all_reduce(ws.view(torch.float32)[:1])
+            lib.rtsds_upce_finish(k, _P(ws), _P(per_head), _P(total), stream())
         ctx.geo, ctx.k, ctx.dt, ctx.dtype = geo, k, dt, xs[0].dtype
         ctx.ws = ws
         ctx.per_head = per_head

@@ -4,11 +4,13 @@ import torch
 from torch import nn
 
 from . import functional as F
+from .runtime import dp_world
 
 
 class CrossEntropyLoss(nn.Module):
     """Mean over non-ignored pixels of -log softmax(x)[target]; logits [N, C, H, W] (NHWC or
-    NCHW memory), target int64 [N, H, W] (or [N, 1, H, W])."""
+    NCHW memory), target int64 [N, H, W] (or [N, 1, H, W]).  Under data parallelism the mean
+    runs over every rank's pixels (runtime.dp_world)."""
 
     def __init__(self, weight=None, ignore_index=-100, reduction="mean"):
         super().__init__()
@@ -27,4 +29,7 @@ class BCEWithLogitsLoss(nn.Module):
             raise NotImplementedError("rtsds_amd.BCEWithLogitsLoss: mean only (main.py:132)")
 
     def forward(self, input, target):
-        return F.bce_with_logits(input, target)
+        loss = F.bce_with_logits(input, target)
+        w = dp_world()
+        # global-batch mean under data parallelism (see runtime.dp_world)
+        return loss if w == 1 else loss * (1.0 / w)

@@ -26,15 +26,15 @@ from .runtime import stream
 def allreduce_flat(buffers):
     """Sum flat gradient buffers over the data-parallel group (RCCL over xGMI for HIP
     tensors, gloo for CPU tests) -- one collective per buffer, replacing DataParallel's
-    per-module reduce (utils.py:104-105).  Returns the 1/world scale the caller applies
-    (folded into the Adam kernel), 1.0 when not distributed."""
+    per-module reduce (utils.py:104-105).  The rtsds losses are already normalised by the
+    global batch (runtime.dp_world), so the SUM is the single-device gradient; returns the
+    gradient scale the Adam kernel applies (1.0)."""
     if not (dist.is_available() and dist.is_initialized()):
         return 1.0
-    world = dist.get_world_size()
-    if world > 1:
+    if dist.get_world_size() > 1:
         for b in buffers:
             dist.all_reduce(b)
-    return 1.0 / world
+    return 1.0
 
 
 class _Arena:

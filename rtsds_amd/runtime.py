@@ -31,6 +31,20 @@ def precision(dtype):
         _state["dtype"] = old
 
 
+def dp_world():
+    """Size of the data-parallel group (1 when torch.distributed is not initialised).
+
+    Under data parallelism the rtsds losses are normalised by the GLOBAL batch (the
+    reference's DataParallel computes each loss once over the gathered batch): CE divides
+    by the all-reduced valid-pixel count, BCE by world * local batch, and the optimizer
+    SUMS the gradients (optim.allreduce_flat) -- so a sharded step equals the single-device
+    step on the concatenated batch (with per-replica BatchNorm statistics, as DataParallel)."""
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_world_size()
+    return 1
+
+
 def dcode(t):
     """torch dtype -> RTSDS_F32 / RTSDS_BF16."""
     if t.dtype == torch.float32:

@@ -10,6 +10,7 @@ import torch
 
 from . import functional as F
 from . import losses, utils
+from .runtime import dp_world
 from .callbacks import Callback
 from .validation import val_GTA5
 
@@ -18,6 +19,17 @@ try:
 except ImportError:  # pragma: no cover
     def tqdm(it, **_):
         return it
+
+
+def _host_values(tensors):
+    """The iteration's logged scalars in one host sync.  Under data parallelism each rank
+    holds its contribution to the global-batch losses (and its pixel count), so they are
+    summed over ranks first."""
+    t = torch.stack([x.double().reshape(()) for x in tensors])
+    if dp_world() > 1:
+        import torch.distributed as dist
+        dist.all_reduce(t)
+    return t.tolist()
 
 
 def _unpack(outputs):
@@ -91,9 +103,9 @@ def train(epoch: int, model: torch.nn.Module, train_loader, criterion: torch.nn.
         inputs = inputs.to(device)
         targets = targets.to(device).squeeze(1)
         loss, corr = seg_step(model, criterion, optimizer, inputs, targets)
-        vals = torch.stack([loss.double(), corr[0].double()]).tolist()
+        vals = _host_values([loss, corr[0]])
         running_loss += vals[0]
-        total += targets.size(0) * targets.size(1) * targets.size(2)
+        total += targets.size(0) * targets.size(1) * targets.size(2) * dp_world()
         correct += int(vals[1])
         for cb in callbacks:
             cb.on_batch_end(batch_idx, {"train_loss": vals[0],
@@ -262,11 +274,11 @@ def adversarial_train(iterations: int, epochs: int, generator: torch.nn.Module,
             *losses, corr = da_step(generator, discriminator, generator_optimizer,
                                     discriminator_optimizer, generator_loss, discriminator_loss,
                                     source_image, source_label, target_image, lambda_, iterations)
-            vals = torch.stack([l.double() for l in losses] + [corr[0].double()]).tolist()
+            vals = _host_values(list(losses) + [corr[0]])
             for k in range(4):
                 run[k] += vals[k]
             g_correct += int(vals[4])
-            g_total += source_label.size(0) * source_label.size(1) * source_label.size(2)
+            g_total += source_label.size(0) * source_label.size(1) * source_label.size(2) * dp_world()
             for cb in callbacks:
                 cb.on_batch_end(i, {"loss_gen_source": vals[0], "loss_adversarial": vals[1],
                                     "loss_disc_source": vals[2], "loss_disc_target": vals[3]})
@@ -332,12 +344,12 @@ def adversarial_train_2(iterations: int, epochs: int, generator: torch.nn.Module
             *losses, corr = da2_step(generator, discriminator, generator_optimizer,
                                      discriminator_optimizer, generator_loss, discriminator_loss,
                                      source_image, source_label, target_image, lambda_adv)
-            vals = torch.stack([l.double() for l in losses] + [corr[0].double()]).tolist()
+            vals = _host_values(list(losses) + [corr[0]])
             for k, v in zip(("loss_gen_source", "loss_adversarial", "loss_gen_total",
                              "loss_disc_target", "loss_disc_source", "loss_disc_total"), vals):
                 run[k] += v
             g_correct += int(vals[6])
-            g_total += source_label.size(0) * source_label.size(1) * source_label.size(2)
+            g_total += source_label.size(0) * source_label.size(1) * source_label.size(2) * dp_world()
         print(f"Epoch Results {epoch}")
         utils.tabular_print({"Genrator Accuracy": (100.0 * g_correct / g_total),
                              "dis_lr": dis_lr if dis_lr else -1, "gen_lr": gen_lr if gen_lr else -1})
