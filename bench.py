@@ -39,6 +39,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-infer", action="store_true")
     ap.add_argument("--conv-report", action="store_true")
+    ap.add_argument("--no-conv-profile", action="store_true", help="skip the event-timed roofline step")
     return ap.parse_args()
 
 
@@ -77,6 +78,16 @@ def cpu_baseline(seconds=15.0):
     return {"value": round(2 * n / dt, 4), "unit": "images/s", "cores": threads, "kind": "port",
             "sample": f"oracle BiSeNet-R18 train step (fwd+3xCE+bwd+Adam), fp32, 2x3x512x1024, "
                       f"{n} timed steps after 1 warm-up ({dt:.1f} s)"}
+
+
+def conv_traffic(args, dtype):
+    """HBM bytes per step of the conv kernels, from the committed rocprofv3 --pmc passes of this
+    same bench command (tools/pmc_bench.sh + tools/pmc_traffic.py; gfx950 FETCH_SIZE x2)."""
+    path = os.path.join(ROOT, "profiles", "conv_traffic.json")
+    if args.batch != 8 or dtype != torch.bfloat16 or not os.path.exists(path):
+        return None
+    with open(path) as f:
+        return json.load(f)["conv_gemm_kernel_bytes_per_step"]
 
 
 def main():
@@ -127,11 +138,13 @@ def main():
     final_loss = float(loss.item())
 
     # ---- live conv roofline: one more step with HIP events around each implicit-GEMM launch
-    F.CONV_PROFILE = []
-    step(args.warmup + args.steps)
-    torch.cuda.synchronize()
-    recs, F.CONV_PROFILE = F.CONV_PROFILE, None
-    conv_ms = sum(r[0].elapsed_time(r[1]) for r in recs)
+    recs = []
+    if not args.no_conv_profile:
+        F.CONV_PROFILE = []
+        step(args.warmup + args.steps)
+        torch.cuda.synchronize()
+        recs, F.CONV_PROFILE = F.CONV_PROFILE, None
+    conv_ms = sum(r[0].elapsed_time(r[1]) for r in recs) or float("nan")
     conv_flop = sum(r[2] for r in recs)
     if args.conv_report and rank == 0:
         rows = []
@@ -149,21 +162,32 @@ def main():
     achieved = conv_flop / (conv_ms * 1e-3) / 1e12
 
     # ---- inference FPS (eval forward, no grad)
+    # Eval-mode forward (BN folded into the conv epilogues), replayed as one hipGraph per batch
+    # size (runtime.GraphedForward); each replay copies the batch into the captured input.
     infer = {}
     if not args.no_infer:
+        from rtsds_amd.runtime import GraphedForward
         net.eval()
         with torch.no_grad():
             for bs in (args.batch, 1):
                 xb = x[:bs].contiguous()
+                fwd = GraphedForward(net, xb)
                 for _ in range(3):
-                    net(xb)
+                    fwd(xb)
                 torch.cuda.synchronize()
-                k = 20 if bs > 1 else 50
+                k = 50 if bs > 1 else 200
                 t1 = time.perf_counter()
                 for _ in range(k):
-                    net(xb)
+                    fwd(xb)
                 torch.cuda.synchronize()
                 infer[f"inference_fps_bs{bs}"] = round(bs * k * world / (time.perf_counter() - t1), 2)
+                # eager (no graph) for reference
+                t1 = time.perf_counter()
+                for _ in range(k // 5):
+                    net(xb)
+                torch.cuda.synchronize()
+                infer[f"inference_fps_bs{bs}_eager"] = round(bs * (k // 5) * world / (time.perf_counter() - t1), 2)
+                del fwd
         net.train()
 
     out = {
@@ -180,7 +204,8 @@ def main():
                                                 "incl. dgrad repack + wgrad split-reduce launches)",
                      "achieved": round(achieved, 2), "peak": MFMA_BF16_PEAK_TFLOPS if dtype == torch.bfloat16 else 157.3,
                      "unit": "TFLOP/s", "frac": round(achieved / (MFMA_BF16_PEAK_TFLOPS if dtype == torch.bfloat16 else 157.3), 4),
-                     "traffic": None, "launches_per_step": len(recs),
+                     "traffic": conv_traffic(args, dtype), "traffic_unit": "HBM bytes per step, all conv launches",
+                     "launches_per_step": len(recs),
                      "conv_ms_per_step": round(conv_ms, 3),
                      "conv_gflop_per_step": round(conv_flop / 1e9, 1)},
         "whole_step_conv_flop_rate_tflops": round(GFLOP_PER_IMG_TRAIN * args.batch / ms, 2),

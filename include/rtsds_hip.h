@@ -60,6 +60,13 @@ size_t rtsds_conv2d_fwd_workspace(const rtsds_conv_desc* d);
 int rtsds_conv2d_fwd_stats_tiles(const rtsds_conv_desc* d);
 int rtsds_conv2d_fwd(const rtsds_conv_desc* d, const void* x, const void* w, const float* bias,
                      void* y, int act, float* bn_stats, void* ws, size_t ws_bytes, void* stream);
+/* Eval-mode conv + BatchNorm(running stats) (+ residual) (+ act) in one launch (inference
+ * path of build_bisenet.py:16-18 ConvBlock, torchvision BasicBlock / Bottleneck,
+ * deeplabv2.py:32-47): y = act(conv(x, w) * scale[k] + shift[k] + res), res NHWC like y (may
+ * be NULL); scale / shift from rtsds_bn_fold.  Same workspace as rtsds_conv2d_fwd.         */
+int rtsds_conv2d_fwd_bn(const rtsds_conv_desc* d, const void* x, const void* w, const float* scale,
+                        const float* shift, const void* res, void* y, int act, void* ws, size_t ws_bytes,
+                        void* stream);
 /* dx (+)= conv_transpose(dy, w) (accumulate != 0: dx += ...).  Needs ws >=
  * rtsds_conv2d_dgrad_workspace(d).  Strides 1 and 2 only.                               */
 size_t rtsds_conv2d_dgrad_workspace(const rtsds_conv_desc* d);
@@ -90,6 +97,12 @@ int rtsds_bn_fwd(const void* x, const void* res, void* y, long rows, int c, cons
                  float* save_invstd, float momentum, float eps, int training, int act,
                  const float* stats_part, int stats_nrb, int dtype, void* ws, size_t ws_bytes,
                  void* stream);
+/* Eval-mode fold of BatchNorm2d(running stats) into the preceding conv (+ its bias, may be
+ * NULL): scale = gamma / sqrt(running_var + eps), shift = beta + (bias - running_mean) * scale
+ * (fp32 [c]; gamma / beta may be NULL = 1 / 0).                                            */
+int rtsds_bn_fold(const float* gamma, const float* beta, const float* running_mean,
+                  const float* running_var, const float* conv_bias, float eps, int c, float* scale,
+                  float* shift, void* stream);
 /* Backward of the fused BN(+res)(+act) above.  y (post-activation output) gives the
  * activation mask; it may be NULL without a residual for act NONE/RELU/LEAKY, when the mask
  * is recomputed bit-exactly from x, gamma, beta and save_*.  dx, dres (may be NULL),

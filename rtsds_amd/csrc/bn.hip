@@ -618,3 +618,26 @@ extern "C" int rtsds_bn_bwd(const void* dy, const void* x, const void* y, void* 
   } else return RTSDS_ERR_UNSUPPORTED;
   return hipGetLastError() == hipSuccess ? RTSDS_OK : RTSDS_ERR_LAUNCH;
 }
+
+// Eval-mode BatchNorm folded into the producing conv (rtsds_conv2d_fwd_bn):
+// scale = gamma / sqrt(running_var + eps), shift = beta + (bias - running_mean) * scale.
+__global__ void bn_fold_kernel(const float* __restrict__ gamma, const float* __restrict__ beta,
+                               const float* __restrict__ rm, const float* __restrict__ rv,
+                               const float* __restrict__ bias, float eps, int c, float* __restrict__ scale,
+                               float* __restrict__ shift) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= c) return;
+  const float s = (gamma ? gamma[i] : 1.f) / sqrtf(rv[i] + eps);
+  scale[i] = s;
+  shift[i] = fmaf((bias ? bias[i] : 0.f) - rm[i], s, beta ? beta[i] : 0.f);
+}
+
+extern "C" int rtsds_bn_fold(const float* gamma, const float* beta, const float* running_mean,
+                             const float* running_var, const float* conv_bias, float eps, int c, float* scale,
+                             float* shift, void* stream) {
+  if (c <= 0) return RTSDS_ERR_SHAPE;
+  if (!running_mean || !running_var || !scale || !shift) return RTSDS_ERR_UNSUPPORTED;
+  hipLaunchKernelGGL(bn_fold_kernel, dim3(rt_cdiv(c, 256)), dim3(256), 0, (hipStream_t)stream, gamma, beta, running_mean,
+                     running_var, conv_bias, eps, c, scale, shift);
+  return hipGetLastError() == hipSuccess ? RTSDS_OK : RTSDS_ERR_LAUNCH;
+}

@@ -39,6 +39,11 @@ struct ConvArgs {
   int accum;          // FWD/DGRAD: y += result
   float* stats;       // FWD: per-M-tile BatchNorm partials [mtile][N][count, mean, M2] (or null)
   long split_stride;  // elements between WGRAD split slabs
+  // FWD eval-mode BatchNorm fold: y = act(acc * scale[co] + bias[co] (+ res)), scale/bias the
+  // running-statistics BN folded with the conv bias (rtsds_bn_fold); res = residual, same
+  // layout as y (or null).
+  const float* scale;
+  const void* res;
 };
 
 template <typename T> struct Mma;
@@ -179,21 +184,26 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(const ConvArgs P) {
   // XCD-aware remap (cdna_hip_programming.md T1, bijective form): workgroups b and b+8 run on
   // one XCD, so give each XCD a contiguous run of tiles -- M-adjacent tiles share input halo
   // rows and the same weight tile in that XCD's L2.
-  int mt, nt;
+  // WGRAD includes the split index (the tiles of one pixel range read the same dY rows and
+  // overlapping X rows: keep them on one XCD).
+  int mt, nt, kz;
   {
-    const int gx = gridDim.x, nwg = gx * gridDim.y;
-    const int bid = blockIdx.y * gx + blockIdx.x;
+    const int gx = gridDim.x, gxy = gx * gridDim.y;
+    const int nwg = RC ? gxy * (int)gridDim.z : gxy;
+    const int bid = (RC ? (int)blockIdx.z * gxy : 0) + blockIdx.y * gx + blockIdx.x;
     const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
     const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
-    mt = wg % gx;
-    nt = wg / gx;
+    const int t = RC ? wg % gxy : wg;
+    kz = RC ? wg / gxy : blockIdx.z;
+    mt = t % gx;
+    nt = t / gx;
   }
   const int m0 = mt * BM, n0 = nt * BN;
   const T* __restrict__ ga = (const T*)P.a;
   const T* __restrict__ gb = (const T*)P.b;
 
   const int nk_total = (P.K + BK - 1) / BK;
-  const int kt0 = blockIdx.z * P.tiles_per_split;
+  const int kt0 = kz * P.tiles_per_split;
   const int kt1 = min(nk_total, kt0 + P.tiles_per_split);
 
   // ---- per-thread invariant gather state
@@ -718,7 +728,7 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(const ConvArgs P) {
   // ---- epilogue: C[row][col], row = (lane>>4)*4 + e, col = lane&15 within each 16x16 block
   const int er = (lane >> 4) * 4, ec = lane & 15;
   if (MODE == MODE_WGRAD) {
-    float* out = (float*)P.out + (long)blockIdx.z * P.split_stride;
+    float* out = (float*)P.out + (long)kz * P.split_stride;
     if (P.N % 4 == 0) {
       // fp32 slab rows leave as 16-B chunks: the C fragments are staged through LDS one
       // wave-row band (WTM rows) at a time, [WTM][BN + 4] fp32.
@@ -773,6 +783,7 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(const ConvArgs P) {
       }
       return gm;
     };
+    const bool has_res = MODE == MODE_FWD && P.res != nullptr;
     bool stored = false;
     if constexpr (sizeof(T) == 2) {
       if (!P.accum && P.N % V == 0) {
@@ -786,18 +797,32 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(const ConvArgs P) {
 #pragma unroll
         for (int j = 0; j < FN; ++j) {
           const int col = wn0 + j * 16 + ec;
-          const float bv = (P.bias && n0 + col < P.N) ? P.bias[n0 + col] : 0.f;
+          const bool ok = n0 + col < P.N;
+          const float bv = (P.bias && ok) ? P.bias[n0 + col] : 0.f;
+          const float sv = (MODE == MODE_FWD && P.scale && ok) ? P.scale[n0 + col] : 1.f;
 #pragma unroll
           for (int i = 0; i < FM; ++i)
 #pragma unroll
-            for (int e = 0; e < 4; ++e) cs[(wm0 + i * 16 + er + e) * CP + col] = from_f<T>(act_f(acc[i][j][e] + bv));
+            for (int e = 0; e < 4; ++e) {
+              const float v = fmaf(acc[i][j][e], sv, bv);
+              cs[(wm0 + i * 16 + er + e) * CP + col] = from_f<T>(has_res ? v : act_f(v));
+            }
         }
         __syncthreads();
 #pragma unroll
         for (int c = tid; c < BM * CPR; c += 256) {
           const int row = c / CPR, cc = c - row * CPR;
           const int gm = m0 + row, gn = n0 + cc * V;
-          if (gm < P.M && gn < P.N) *(V16*)(out + out_row(gm) * P.N + gn) = *(const V16*)(cs + row * CP + cc * V);
+          if (gm < P.M && gn < P.N) {
+            const long o = out_row(gm) * P.N + gn;
+            V16 v = *(const V16*)(cs + row * CP + cc * V);
+            if (has_res) {
+              const V16 r = *(const V16*)((const T*)P.res + o);
+#pragma unroll
+              for (int q = 0; q < V; ++q) v[q] = from_f<T>(act_f(to_f(v[q]) + to_f(r[q])));
+            }
+            *(V16*)(out + o) = v;
+          }
         }
         stored = true;
       }
@@ -808,6 +833,7 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(const ConvArgs P) {
         const int gn = n0 + wn0 + j * 16 + ec;
         if (gn >= P.N) continue;
         const float bv = P.bias ? P.bias[gn] : 0.f;
+        const float sv = (MODE == MODE_FWD && P.scale) ? P.scale[gn] : 1.f;
 #pragma unroll
         for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -815,7 +841,8 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(const ConvArgs P) {
             const int gm = m0 + wm0 + i * 16 + er + e;
             if (gm >= P.M) continue;
             const long orow = out_row(gm);
-            float v = acc[i][j][e] + bv;
+            float v = fmaf(acc[i][j][e], sv, bv);
+            if (has_res) v += to_f(((const T*)P.res)[orow * P.N + gn]);
             if (P.accum) v += to_f(out[orow * P.N + gn]);
             out[orow * P.N + gn] = from_f<T>(act_f(v));
           }
@@ -1158,6 +1185,39 @@ extern "C" int rtsds_conv2d_fwd(const rtsds_conv_desc* d0, const void* x, const 
   p.accum = (act & RTSDS_ACCUMULATE) ? 1 : 0;
   if (bn_stats && (p.act || p.accum)) return RTSDS_ERR_UNSUPPORTED;
   p.stats = bn_stats;
+  p.M = d.n * d.ho * d.wo;
+  p.N = d.k;
+  p.K = d.kh * d.kw * d.c;
+  if (d.dtype == RTSDS_BF16) dispatch_align<bf16, MODE_FWD>(p, d.c, st);
+  else dispatch_align<float, MODE_FWD>(p, d.c, st);
+  return hipGetLastError() == hipSuccess ? RTSDS_OK : RTSDS_ERR_LAUNCH;
+}
+
+// Eval-mode conv + BatchNorm(running statistics) [+ residual] [+ activation] in one launch:
+// y = act(conv(x, w) * scale + shift + res), scale / shift from rtsds_bn_fold.
+extern "C" int rtsds_conv2d_fwd_bn(const rtsds_conv_desc* d0, const void* x, const void* w, const float* scale,
+                                   const float* shift, const void* res, void* y, int act, void* ws, size_t ws_bytes,
+                                   void* stream) {
+  if (!scale || !shift || (act & RTSDS_ACCUMULATE)) return RTSDS_ERR_UNSUPPORTED;
+  int e = check_desc(d0);
+  if (e) return e;
+  if (ws_bytes < rtsds_conv2d_fwd_workspace(d0)) return RTSDS_ERR_WORKSPACE;
+  hipStream_t st = (hipStream_t)stream;
+  rtsds_conv_desc d = *d0;
+  const int cp = pad_c(d.c, d.dtype);
+  if (cp != d.c) {
+    const size_t es = esize(d.dtype);
+    void* xp = ws;
+    void* wp = (char*)ws + al256((size_t)d.n * d.h * d.w * cp * es);
+    pad_any(d.dtype, x, xp, (long)d.n * d.h * d.w, d.c, cp, st);
+    pad_any(d.dtype, w, wp, (long)d.k * d.kh * d.kw, d.c, cp, st);
+    x = xp;
+    w = wp;
+    d.c = cp;
+  }
+  ConvArgs p = make_args(&d);
+  p.a = x; p.b = w; p.bias = shift; p.scale = scale; p.res = res; p.out = y;
+  p.act = act & 0xff;
   p.M = d.n * d.ho * d.wo;
   p.N = d.k;
   p.K = d.kh * d.kw * d.c;

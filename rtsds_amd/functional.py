@@ -157,6 +157,31 @@ def conv2d(x, weight, bias, wq, stride=(1, 1), padding=(0, 0), dilation=(1, 1), 
     return y
 
 
+def conv_bn_eval(x, weight, bias, wq, stride, padding, dilation, gamma, beta, running_mean, running_var,
+                 eps, act=0, residual=None):
+    """Inference (no autograd) conv -> BatchNorm(running statistics) [-> + residual] [-> act]
+    as ONE implicit-GEMM launch: the BN is folded into a per-channel scale / shift of the conv
+    epilogue (rtsds_bn_fold + rtsds_conv2d_fwd_bn).  Same function as the unfused
+    conv2d -> batch_norm(training=False) chain, with the BN applied to the fp32 accumulators."""
+    require_hip(x, weight)
+    x = nhwc(x)
+    k, _, kh, kw = weight.shape
+    d = _conv_desc(x, k, kh, kw, stride, padding, dilation)
+    ss = torch.empty(2 * k, dtype=torch.float32, device=x.device)
+    lib.rtsds_bn_fold(_P(gamma), _P(beta), _P(running_mean), _P(running_var), _P(bias), float(eps), k,
+                      _P(ss), ss.data_ptr() + 4 * k, stream())
+    if residual is not None:
+        residual = nhwc(residual)
+        if residual.dtype != x.dtype or tuple(residual.shape) != (d.n, k, d.ho, d.wo):
+            raise RuntimeError("rtsds_amd.conv_bn_eval: residual must match the conv output")
+    y = empty_nhwc(d.n, k, d.ho, d.wo, x.dtype, x.device)
+    ws = workspace(lib.rtsds_conv2d_fwd_workspace(ctypes.byref(d)), x.device)
+    with _Timed(d, "fwd"):
+        lib.rtsds_conv2d_fwd_bn(ctypes.byref(d), _P(x), _P(wq), _P(ss), ss.data_ptr() + 4 * k, _P(residual), _P(y),
+                                act, _P(ws), ws.numel(), stream())
+    return y
+
+
 class ConvSumFn(torch.autograd.Function):
     """sum_i conv_i(x) + bias_i over convs sharing x and output shape (ASPP,
     deeplabv2.py:62-66): one output buffer accumulated in the GEMM epilogue; the backward

@@ -118,10 +118,23 @@ class MaxPool2d(nn.Module):
         return F.max_pool2d(x, self.kernel_size, self.stride, self.padding, self.ceil_mode)
 
 
+def _no_grad_needed(conv, bn, x, residual):
+    if not torch.is_grad_enabled():
+        return True
+    ts = [x, residual, conv.weight, conv.bias, bn.weight, bn.bias]
+    return not any(t is not None and t.requires_grad for t in ts)
+
+
 def conv_bn(conv, bn, x, act=None, residual=None):
     """bn(conv(x)) with the BatchNorm's batch statistics produced by the conv epilogue
-    (train mode) instead of a separate pass over the conv output."""
+    (train mode) instead of a separate pass over the conv output.  Eval mode without
+    autograd (inference, validation): the BN (+ residual + act) folds into the conv's
+    epilogue -- one launch per ConvBlock / residual branch."""
     use_batch = bn.training or not bn.track_running_stats
+    if not use_batch and bn.momentum is not None and _no_grad_needed(conv, bn, x, residual):
+        wq = _shadow(conv.weight, x.dtype)
+        return F.conv_bn_eval(x, conv.weight, conv.bias, wq, conv.stride, conv.padding, conv.dilation,
+                              bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.eps, ACT[act], residual)
     return bn(conv(x, bn_stats=use_batch), act=act, residual=residual)
 
 

@@ -85,3 +85,32 @@ def nhwc(t):
 
 def workspace(nbytes, device):
     return torch.empty(max(int(nbytes), 16), dtype=torch.uint8, device=device)
+
+
+class GraphedForward:
+    """hipGraph capture of a fixed-shape inference forward (torch.cuda.CUDAGraph is a hipGraph
+    on ROCm): every rtsds kernel of ``module(x)`` is recorded once on a side stream and the
+    whole launch sequence is replayed with one call, removing the per-kernel host launch cost
+    that dominates small-batch inference.  ``x`` fixes shape / dtype / device; replays copy the
+    new batch into the captured input buffer and return the captured output buffer (valid
+    until the next replay)."""
+
+    def __init__(self, module, x, warmup=2):
+        self.module = module
+        self.static_in = x.detach().clone()
+        side = torch.cuda.Stream(device=x.device)
+        side.wait_stream(torch.cuda.current_stream(x.device))
+        with torch.no_grad(), torch.cuda.stream(side):
+            for _ in range(warmup):  # settle lazy allocations (bf16 shadows, workspaces)
+                module(self.static_in)
+        torch.cuda.current_stream(x.device).wait_stream(side)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.no_grad(), torch.cuda.graph(self.graph):
+            self.static_out = module(self.static_in)
+
+    def __call__(self, x):
+        if x.shape != self.static_in.shape or x.dtype != self.static_in.dtype:
+            raise RuntimeError("GraphedForward: input shape/dtype differs from the captured one")
+        self.static_in.copy_(x)
+        self.graph.replay()
+        return self.static_out

@@ -416,3 +416,75 @@ def test_confusion():
     k = (lab >= 0) & (lab < 19)
     ref = torch.bincount(19 * lab[k] + pred[k], minlength=361)
     assert torch.equal(hist.cpu(), ref)
+
+
+FOLD_CASES = [
+    # n, c, h, w, k, kh, stride, pad, bias, act, residual
+    (2, 3, 32, 48, 64, 7, 2, 3, False, 1, False),    # stem conv + bn1 + relu
+    (2, 64, 16, 24, 64, 3, 1, 1, False, 1, True),    # BasicBlock conv2 + bn2 + identity + relu
+    (2, 64, 16, 16, 128, 1, 2, 0, False, 0, False),  # downsample 1x1 s2 + bn
+    (8, 256, 1, 1, 256, 1, 1, 0, True, 3, False),    # ARM 1x1(bias) + bn + sigmoid
+    (2, 1024, 8, 16, 19, 3, 1, 1, False, 1, False),  # FFM ConvBlock (N=19: scalar epilogue)
+    (8, 128, 64, 64, 128, 3, 1, 1, False, 1, True),  # 128x128 LDS-DMA tile + residual
+]
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("case", FOLD_CASES)
+def test_conv_bn_eval_fold(case, dt):
+    """Inference conv -> BN(running stats) [+res] [-> act] as one launch vs ATen fp64."""
+    n, c, h, w, k, kh, s, p, has_bias, act, has_res = case
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn(n, c, h, w, generator=g, dtype=torch.float64)
+    wt = torch.randn(k, c, kh, kh, generator=g, dtype=torch.float64) / (c * kh * kh) ** 0.5
+    b = torch.randn(k, generator=g, dtype=torch.float64) if has_bias else None
+    rm, rv = torch.randn(k, generator=g, dtype=torch.float64), 0.5 + torch.rand(k, generator=g, dtype=torch.float64)
+    gam, bet = torch.randn(k, generator=g, dtype=torch.float64), torch.randn(k, generator=g, dtype=torch.float64)
+    if dt == torch.bfloat16:
+        x, wt = x.bfloat16().double(), wt.bfloat16().double()
+    y0 = TF.batch_norm(TF.conv2d(x, wt, b, s, p), rm, rv, gam, bet, False, 0.1, 1e-5)
+    res = torch.randn(y0.shape, generator=g, dtype=torch.float64) if has_res else None
+    if res is not None:
+        if dt == torch.bfloat16:
+            res = res.bfloat16().double()
+        y0 = y0 + res
+    yr = {0: y0, 1: TF.relu(y0), 3: torch.sigmoid(y0)}[act]
+    wd = wt.float().to(DEV).contiguous(memory_format=CL)
+    dv = lambda t: None if t is None else t.float().to(DEV)  # noqa: E731
+    with torch.no_grad():
+        y = F.conv_bn_eval(_dev(x, dt), wd, dv(b), _shadow(wd, dt), (s, s), (p, p), (1, 1), dv(gam), dv(bet),
+                           dv(rm), dv(rv), 1e-5, act, None if res is None else _dev(res, dt))
+    _close(y, yr, dt, "y", 2e-4 if dt == torch.float32 else 3e-2)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_bisenet_eval_fold_and_graph(dt):
+    """BiSeNet eval forward: folded conv+BN path == unfused path (autograd-enabled eval), and a
+    hipGraph replay (runtime.GraphedForward) == eager."""
+    import rtsds_amd
+    from rtsds_amd.models.bisenet.build_bisenet import BiSeNet
+    from rtsds_amd.runtime import GraphedForward
+    torch.manual_seed(0)
+    with rtsds_amd.precision(dt):
+        net = BiSeNet(19, "resnet18").to(DEV)
+        # non-trivial running statistics: a few train-mode forwards
+        xs = torch.randn(2, 3, 64, 128, device=DEV)
+        with torch.no_grad():
+            for _ in range(2):
+                net(xs)
+        net.eval()
+        x = torch.randn(2, 3, 64, 128, device=DEV)
+        ref = net(x.requires_grad_()).detach()  # autograd on: unfused conv -> BN chain
+        x = x.detach()
+        with torch.no_grad():
+            fused = net(x)
+        gf = GraphedForward(net, x)
+        x2 = torch.randn_like(x)
+        with torch.no_grad():
+            eager2 = net(x2)
+        rep2 = gf(x2).clone()
+        rep1 = gf(x).clone()
+    tol = 1e-3 if dt == torch.float32 else 5e-2
+    scale = ref.abs().max().item()
+    assert (fused.float() - ref.float()).abs().max().item() <= tol * scale
+    assert torch.equal(rep1, fused) and torch.equal(rep2, eager2)
