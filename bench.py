@@ -7,6 +7,13 @@ forward (3 heads), 3x cross-entropy(ignore 19), backward, Adam step, pixel-accur
 (torchrun), each with its own batch of 8 (weak scaling); gradients all-reduced over RCCL
 inside the optimizer step.  Prints ONE JSON line on rank 0.
 
+``--workload`` selects the other BASELINE.json configs as separate bench lines (the default is
+configs[1]): ``bisenet-da`` (configs[3] per GPU: adversarial_train iteration, 8 source + 8
+target 1024x512 images, TinyDomainDiscriminator), ``deeplab-seg`` (configs[2]: DeepLabV2
+ResNet-101 + ASPP seg step, bs 4, 1024x512), ``deeplab-da`` (configs[4] per GPU: DeepLabV2 DA
+iteration, 2 + 2 images at 1280x720).  Unit: source images/s (one DA unit = a source image
+with its paired target image).
+
 Extra fields: inference FPS (eval forward, bs 8 and bs 1), the live conv roofline
 (HIP events around every implicit-GEMM launch over one extra step after the timed
 region), and the CPU baseline (the oracle's restatement of the reference step on the host
@@ -25,8 +32,18 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 MFMA_BF16_PEAK_TFLOPS = 2500.0   # MI355X dense bf16 (MI355X_MICROARCH.md)
-GFLOP_PER_IMG_TRAIN = 151.6      # conv GFLOP fwd+bwd per image, 1024x512
-H, W, NC = 512, 1024, 19
+NC = 19
+# workload -> (model, DA?, default per-GPU batch, H, W, conv GFLOP per unit, BASELINE config)
+WORKLOADS = {
+    "bisenet-seg": ("bisenet", False, 8, 512, 1024, 151.6, "configs[1]: BiSeNet-R18 seg-only train step (train.py:65-113)"),
+    "bisenet-da": ("bisenet", True, 8, 512, 1024, 333.8,
+                   "configs[3] per GPU: BiSeNet-R18 + TinyD adversarial_train iteration (train.py:172-284)"),
+    "deeplab-seg": ("deeplab", False, 4, 512, 1024, 2239.5,
+                    "configs[2]: DeepLabV2-R101 + ASPP seg-only train step (train.py:65-113)"),
+    "deeplab-da": ("deeplab", True, 2, 720, 1280, 7881.3,
+                   "configs[4] per GPU: DeepLabV2-R101 + TinyD adversarial_train iteration (train.py:172-284)"),
+}
+H, W = 512, 1024
 
 
 def parse():
@@ -34,7 +51,10 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=8)
+    ap.add_argument("--workload", default="bisenet-seg", choices=sorted(WORKLOADS))
+    ap.add_argument("--batch", type=int, default=None, help="per-GPU batch (default: the workload's)")
+    ap.add_argument("--allreduce-dtype", default="fp32", choices=["fp32", "fp16", "bf16"],
+                    help="gradient all-reduce wire dtype (N>1)")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-infer", action="store_true")
@@ -43,8 +63,9 @@ def parse():
     return ap.parse_args()
 
 
-def synthetic_batch(n, seed, device):
+def synthetic_batch(n, seed, device, h=H, w=W):
     """ImageNet-normalised 0-255 images + labels in [0, 19] (19 = ignore), SURVEY 8(d)."""
+    H, W = h, w
     g = torch.Generator().manual_seed(seed)
     x = torch.randint(0, 256, (n, 3, H, W), generator=g).float()
     mean = torch.tensor([0.485, 0.456, 0.406]).view(1, 3, 1, 1)
@@ -84,36 +105,64 @@ def conv_traffic(args, dtype):
     """HBM bytes per step of the conv kernels, from the committed rocprofv3 --pmc passes of this
     same bench command (tools/pmc_bench.sh + tools/pmc_traffic.py; gfx950 FETCH_SIZE x2)."""
     path = os.path.join(ROOT, "profiles", "conv_traffic.json")
-    if args.batch != 8 or dtype != torch.bfloat16 or not os.path.exists(path):
+    if args.workload != "bisenet-seg" or args.batch != 8 or dtype != torch.bfloat16 or not os.path.exists(path):
         return None
     with open(path) as f:
         return json.load(f)["conv_gemm_kernel_bytes_per_step"]
 
 
+def build(args, dev, rank):
+    """Model(s), optimizer(s), synthetic resident inputs and the step closure of the workload."""
+    from rtsds_amd import losses, optim
+    from rtsds_amd.train import da_step, seg_step
+    from rtsds_amd.utils import poly_lr_scheduler
+    model, da, _, h, w, _, _ = WORKLOADS[args.workload]
+    if model == "bisenet":
+        from rtsds_amd.models.bisenet.build_bisenet import BiSeNet
+        net = BiSeNet(NC, "resnet18").to(dev).train()
+    else:
+        from rtsds_amd.models.deeplabv2.deeplabv2 import get_deeplab_v2
+        net = get_deeplab_v2(NC, pretrain=False).to(dev).train()
+    opt = optim.Adam(net.parameters(), lr=1e-4)
+    crit = losses.CrossEntropyLoss(ignore_index=NC)
+    x, y = synthetic_batch(args.batch, 42 + 2 * rank, dev, h, w)
+    max_iter = 1000
+    if not da:
+        def step(i):
+            poly_lr_scheduler(opt, 1e-4, i, 1, max_iter, 0.9)
+            return seg_step(net, crit, opt, x, y)
+        return net, x, step
+    from rtsds_amd.models.domain_shift.adversarial.model import TinyDomainDiscriminator
+    disc = TinyDomainDiscriminator(NC).to(dev).train()
+    dopt = optim.Adam(disc.parameters(), lr=1e-4, weight_decay=1e-4)
+    bce = losses.BCEWithLogitsLoss()
+    xt, _ = synthetic_batch(args.batch, 43 + 2 * rank, dev, h, w)
+    poly_lr_scheduler(dopt, 1e-4, 0, 1, 10, 0.05)  # per epoch (train.py:167)
+
+    def step(i):
+        poly_lr_scheduler(opt, 1e-4, i, 1, max_iter, 0.9)
+        out = da_step(net, disc, opt, dopt, crit, bce, x, y, xt, 0.1, 100)  # lambda, iterations: config.yaml
+        return out[0], out[-1]
+    return net, x, step
+
+
 def main():
     args = parse()
     from rtsds_amd import functional as F
-    from rtsds_amd import losses, optim, set_compute_dtype
-    from rtsds_amd.models.bisenet.build_bisenet import BiSeNet
-    from rtsds_amd.train import seg_step
-    from rtsds_amd.utils import init_distributed, poly_lr_scheduler
+    from rtsds_amd import optim, set_compute_dtype
+    from rtsds_amd.utils import init_distributed
 
+    wl = WORKLOADS[args.workload]
+    if args.batch is None:
+        args.batch = wl[2]
     rank, local, world = init_distributed()
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
     set_compute_dtype(dtype)
+    optim.set_allreduce_dtype({"fp32": torch.float32, "fp16": torch.float16, "bf16": torch.bfloat16}[args.allreduce_dtype])
     torch.manual_seed(42)
-
-    net = BiSeNet(NC, "resnet18").to(dev).train()
-    opt = optim.Adam(net.parameters(), lr=1e-4)
-    crit = losses.CrossEntropyLoss(ignore_index=NC)
-    x, y = synthetic_batch(args.batch, 42 + 2 * rank, dev)
-    max_iter = 1000
-
-    def step(i):
-        poly_lr_scheduler(opt, 1e-4, i, 1, max_iter, 0.9)
-        return seg_step(net, crit, opt, x, y)
+    net, x, step = build(args, dev, rank)
 
     for i in range(args.warmup):
         step(i)
@@ -165,7 +214,7 @@ def main():
     # Eval-mode forward (BN folded into the conv epilogues), replayed as one hipGraph per batch
     # size (runtime.GraphedForward); each replay copies the batch into the captured input.
     infer = {}
-    if not args.no_infer:
+    if not args.no_infer and args.workload == "bisenet-seg":
         from rtsds_amd.runtime import GraphedForward
         net.eval()
         with torch.no_grad():
@@ -196,9 +245,11 @@ def main():
         "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
         "data": "synthetic (ImageNet-normalised 0-255 images, labels 0..19, 19=ignore; random-init weights)",
-        "config": {"workload": "BiSeNet-R18 seg-only train step (train.py:65-113)", "model": "BiSeNet-ResNet18",
+        "config": {"workload": wl[6], "model": "BiSeNet-ResNet18" if wl[0] == "bisenet" else "DeepLabV2-ResNet101",
                    "global_batch": args.batch * world, "per_gpu_batch": args.batch,
-                   "image": "3x512x1024", "num_classes": NC, "parallelism": f"dp{world}"},
+                   "image": f"3x{wl[3]}x{wl[4]}", "num_classes": NC, "parallelism": f"dp{world}",
+                   **({"discriminator": "TinyDomainDiscriminator", "target_batch_per_gpu": args.batch} if wl[1] else {}),
+                   **({"grad_allreduce_dtype": args.allreduce_dtype} if world > 1 else {})},
         **infer,
         "roofline": {"bound": "mfma", "kernel": "conv_gemm_kernel (implicit-GEMM conv fwd/dgrad/wgrad, "
                                                 "incl. dgrad repack + wgrad split-reduce launches)",
@@ -208,10 +259,10 @@ def main():
                      "launches_per_step": len(recs),
                      "conv_ms_per_step": round(conv_ms, 3),
                      "conv_gflop_per_step": round(conv_flop / 1e9, 1)},
-        "whole_step_conv_flop_rate_tflops": round(GFLOP_PER_IMG_TRAIN * args.batch / ms, 2),
+        "whole_step_conv_flop_rate_tflops": round(wl[5] * args.batch / ms, 2),
         "final_loss": round(final_loss, 4),
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.workload == "bisenet-seg":
         out["cpu_baseline"] = cpu_baseline()
     if rank == 0:
         print(json.dumps(out), flush=True)

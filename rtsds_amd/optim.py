@@ -23,6 +23,18 @@ from ._lib import lib
 from .runtime import stream
 
 
+_ALLREDUCE = {"dtype": torch.float32}
+
+
+def set_allreduce_dtype(dtype):
+    """Wire dtype of the gradient all-reduce: float32 (exact, default) or float16 / bfloat16
+    (half the xGMI bytes; BASELINE configs[4] runs fp16).  The fp32 arena is cast down, summed
+    and cast back before the Adam step."""
+    if dtype not in (torch.float32, torch.float16, torch.bfloat16):
+        raise ValueError("all-reduce dtype must be float32, float16 or bfloat16")
+    _ALLREDUCE["dtype"] = dtype
+
+
 def allreduce_flat(buffers):
     """Sum flat gradient buffers over the data-parallel group (RCCL over xGMI for HIP
     tensors, gloo for CPU tests) -- one collective per buffer, replacing DataParallel's
@@ -32,8 +44,14 @@ def allreduce_flat(buffers):
     if not (dist.is_available() and dist.is_initialized()):
         return 1.0
     if dist.get_world_size() > 1:
+        wire = _ALLREDUCE["dtype"]
         for b in buffers:
-            dist.all_reduce(b)
+            if wire == torch.float32:
+                dist.all_reduce(b)
+            else:
+                t = b.to(wire)
+                dist.all_reduce(t)
+                b.copy_(t)
     return 1.0
 
 

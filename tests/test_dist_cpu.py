@@ -20,12 +20,14 @@ def _port():
     return p
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, wire="fp32"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
     from rtsds_amd.utils import init_distributed
     r, local, w = init_distributed("gloo")
     assert (r, w) == (rank, world)
+    from rtsds_amd.optim import set_allreduce_dtype
+    set_allreduce_dtype({"fp32": torch.float32, "fp16": torch.float16, "bf16": torch.bfloat16}[wire])
     g = torch.arange(10, dtype=torch.float32) * (rank + 1)
     scale = allreduce_flat([g])
     q.put((rank, g.tolist(), scale))
@@ -33,12 +35,14 @@ def _worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("wire", ["fp32", "fp16"])
 @pytest.mark.parametrize("world", [2])
-def test_gloo_flat_allreduce(world):
+def test_gloo_flat_allreduce(world, wire):
+    """Exact for small integers in every wire dtype (fp16 represents 0..27 exactly)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, wire)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=120) for _ in range(world)]
