@@ -44,6 +44,7 @@ struct ConvArgs {
   // layout as y (or null).
   const float* scale;
   const void* res;
+  int gbuf;           // operand tensors < 2 GiB: buffer-resource DMA with 32-bit offsets allowed
 };
 
 template <typename T> struct Mma;
@@ -131,6 +132,23 @@ RT_DEV bf16x8 rc_gl_frag(s16x4 t0, s16x4 t1) {
   s16x8 r = {t0[0], t0[1], t0[2], t0[3], t1[0], t1[1], t1[2], t1[3]};
   return __builtin_bit_cast(bf16x8, r);
 }
+// Buffer-resource LDS-DMA (buffer_load_dwordx4 ... offen lds): 32-bit byte offsets, and an
+// offset past num_records zero-fills the LDS destination.  The host compilation pass of the
+// kernel templates only needs the signatures.
+#if defined(__HIP_DEVICE_COMPILE__)
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+RT_DEV rsrc_t make_rsrc(const void* p, int bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)p, 0, bytes, 0x00020000);
+}
+RT_DEV void buf_lds16(rsrc_t r, void* lds, int voff, int soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, voff, soff, 0, 0);
+}
+#else
+struct rsrc_t { int w[4]; };
+RT_DEV rsrc_t make_rsrc(const void*, int) { return rsrc_t{}; }
+RT_DEV void buf_lds16(rsrc_t, void*, int, int) {}
+#endif
+
 // 16 zero bytes: the DMA source of padding / out-of-range gathers.
 __device__ __attribute__((aligned(16))) bf16 g_conv_zero[8];
 template <int N> RT_DEV void wait_vmcnt() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
@@ -250,6 +268,40 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(const ConvArgs P) {
     }
   }
 
+  // GL + ALA 2 (one filter tap per K-tile): LDS-DMA through buffer resources with 32-bit
+  // offsets.  Each staged A row keeps its element offset at tap (0, 0) (negative in the
+  // padding band is fine), the per-K-tile tap adds a wave-uniform offset, and an invalid
+  // gather (padding, M edge) gets an out-of-range offset, which the DMA zero-fills (probed:
+  // tools/probe/buf_lds_oob.hip).  B rows keep their byte offset; K-tiles add k0 as soffset.
+  // DGRAD: stride 1, or the stride-2 parity phases (every reaching tap has matching parity, so
+  // (a_h - r*dh) / 2 = (a_h >> 1) - ((r*dh) >> 1)).
+  constexpr bool GB = G && !RC && ALA == 2;
+  int gba_base[GB ? NA : 1], gbb_off[GB ? NB : 1];
+  rsrc_t rs_a, rs_b;
+  const int gsh = (MODE == MODE_DGRAD && P.sh == 2) ? 1 : 0;
+  if constexpr (GB) {
+    const int a_bytes = (MODE == MODE_FWD ? P.n * P.h * P.w * P.c : P.n * P.ho * P.wo * P.k) * 2;
+    rs_a = make_rsrc(ga, a_bytes);
+    rs_b = make_rsrc(gb, P.N * P.K * 2);
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+      const int row = i * 32 + wave * 8 + (lane >> 3);
+      const int ch = gl_swz(row, lane & 7) * V;
+      gba_base[i] = MODE == MODE_FWD ? (int)a_off[i] + (a_h[i] * P.w + a_w[i]) * P.c + ch
+                                     : (int)a_off[i] + ((a_h[i] >> gsh) * P.wo + (a_w[i] >> gsh)) * P.k + ch;
+      gba_base[i] *= 2;
+      // opaque to the optimiser: otherwise it re-derives the offset from (hh, ww) with two
+      // quarter-rate multiplies per gather inside the K loop
+      asm volatile("" : "+v"(gba_base[i]));
+    }
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const int row = i * 32 + wave * 8 + (lane >> 3);
+      const int nrow = n0 + row;
+      gbb_off[i] = nrow < P.N ? (nrow * P.K + gl_swz(row, lane & 7) * V) * 2 : (int)0x80000000;
+    }
+  }
+
   // GL WGRAD: the (tap, ci) column of each B chunk this lane stages is fixed for the whole
   // reduction (the swizzled chunk depends only on the tile row).
   int gb_r[G && RC ? NB : 1], gb_s[G && RC ? NB : 1], gb_ci[G && RC ? NB : 1];
@@ -268,6 +320,30 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(const ConvArgs P) {
       gb_ci[i] = (gb_ok[i] ? nn : 0) - tap * P.c;
       gb_r[i] = fdiv(tap, P.f_kw);
       gb_s[i] = tap - gb_r[i] * P.kw;
+    }
+  }
+  // GL WGRAD on whole-row K-tiles with buffer-resource DMA: per-chunk constant parts of the
+  // gather offsets; per K-tile only the tile origin (uniform) is added.  dY rows past the last
+  // pixel fall past num_records and are zero-filled.
+  int wga_off[G && RC ? NA : 1], wgb_ch[G && RC ? NB : 1], wgb_cw[G && RC ? NB : 1], wgb_cb[G && RC ? NB : 1];
+  if constexpr (G && RC) {
+    if (P.gbuf && P.wg_rows) {
+      rs_a = make_rsrc(ga, P.K * P.k * 2);
+      rs_b = make_rsrc(gb, P.n * P.h * P.w * P.c * 2);
+      constexpr int CPA = BM / V, RPA = 64 / CPA, CPB = BN / V, RPB = 64 / CPB;
+#pragma unroll
+      for (int i = 0; i < NA; ++i) {
+        const int row = (i * 4 + wave) * RPA + lane / CPA;
+        const int co = m0 + ((lane % CPA) ^ rc_swz<BM>(row)) * V;
+        wga_off[i] = co < P.M ? (row * P.k + co) * 2 : (int)0x80000000;
+      }
+#pragma unroll
+      for (int i = 0; i < NB; ++i) {
+        wgb_ch[i] = gb_ok[i] ? gb_dh[i] * P.sh - P.ph + gb_r[i] * P.dh : -(1 << 30);
+        wgb_cw[i] = gb_dw[i] * P.sw - P.pw + gb_s[i] * P.dw;
+        wgb_cb[i] = ((wgb_ch[i] * P.w + wgb_cw[i]) * P.c + gb_ci[i]) * 2;
+        asm volatile("" : "+v"(wgb_cb[i]));
+      }
     }
   }
 
@@ -437,6 +513,20 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(const ConvArgs P) {
       T* sb = sa + A_EL;
       constexpr int CPA = BM / V, RPA = 64 / CPA;  // chunks per row, rows per wave-instruction
       constexpr int CPB = BN / V, RPB = 64 / CPB;
+      if (P.gbuf && P.wg_rows) {
+#pragma unroll
+        for (int i = 0; i < NA; ++i) buf_lds16(rs_a, sa + (i * 4 + wave) * RPA * BM, wga_off[i], k0 * P.k * 2);
+        const int t_img = fdiv(k0, P.f_howo), t_rem = k0 - t_img * P.ho * P.wo;
+        const int t_oh = fdiv(t_rem, P.f_wo), t_ow = t_rem - t_oh * P.wo;
+        const int uh = t_oh * P.sh, uw = t_ow * P.sw;
+        const int ub = (((t_img * P.h + uh) * P.w + uw) * P.c) * 2;
+#pragma unroll
+        for (int i = 0; i < NB; ++i) {
+          const bool ok = (unsigned)(uh + wgb_ch[i]) < (unsigned)P.h && (unsigned)(uw + wgb_cw[i]) < (unsigned)P.w;
+          buf_lds16(rs_b, sb + (i * 4 + wave) * RPB * BN, ok ? ub + wgb_cb[i] : (int)0x80000000, 0);
+        }
+        return;
+      }
 #pragma unroll
       for (int i = 0; i < NA; ++i) {  // dY rows (pixels) x Cout columns
         const int rb = (i * 4 + wave) * RPA, row = rb + lane / CPA;
@@ -468,6 +558,36 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(const ConvArgs P) {
         }
         __builtin_amdgcn_global_load_lds((glb_t)src, (lds_t)(sb + rb * BN), 16, 0, 0);
       }
+    } else if constexpr (GB) {
+      const int k0 = kt * BK;
+      T* sa = smem + buf * (A_EL + B_EL);
+      T* sb = sa + A_EL;
+      const int Cr = (MODE == MODE_FWD) ? P.c : P.k;
+      const int tap = k0 / Cr, ci = k0 - tap * Cr;
+      int r, sx;
+      if (MODE == MODE_FWD) {
+        r = tap / P.kw;
+        sx = tap - r * P.kw;
+      } else {
+        const int rr = tap / P.tkw;
+        r = P.r0h + rr * P.rstep;
+        sx = P.r0w + (tap - rr * P.tkw) * P.rstep;
+      }
+      const int dhh = (r * P.dh) >> gsh, dww = (sx * P.dw) >> gsh;
+      const int toff = MODE == MODE_FWD ? (dhh * P.w + dww) * P.c + ci : ci - (dhh * P.wo + dww) * P.k;
+      const unsigned lim_h = MODE == MODE_FWD ? P.h : P.ho, lim_w = MODE == MODE_FWD ? P.w : P.wo;
+      const int toff2 = toff * 2;
+#pragma unroll
+      for (int i = 0; i < NA; ++i) {
+        const int hh = MODE == MODE_FWD ? a_h[i] + dhh : (a_h[i] >> gsh) - dhh;
+        const int ww = MODE == MODE_FWD ? a_w[i] + dww : (a_w[i] >> gsh) - dww;
+        const bool ok = a_ok[i] && (unsigned)hh < lim_h && (unsigned)ww < lim_w;
+        const int voff = ok ? gba_base[i] + toff2 : (int)0x80000000;
+        buf_lds16(rs_a, sa + (i * 32 + wave * 8) * BK, voff, 0);
+      }
+#pragma unroll
+      for (int i = 0; i < NB; ++i)
+        buf_lds16(rs_b, sb + (i * 32 + wave * 8) * BK, gbb_off[i], k0 * 2);
     } else if constexpr (G) {
       typedef __attribute__((address_space(3))) void* lds_t;
       typedef const __attribute__((address_space(1))) void* glb_t;
@@ -1019,6 +1139,7 @@ __global__ void colsum_final_kernel(const float* __restrict__ part, float* __res
 static const int kColsumRB = 1024;
 
 // ---- host side ---------------------------------------------------------------------------
+static size_t esize(int dtype) { return dtype == RTSDS_BF16 ? 2 : 4; }
 static ConvArgs make_args(const rtsds_conv_desc* d) {
   ConvArgs p = {};
   p.n = d->n; p.h = d->h; p.w = d->w; p.c = d->c; p.ho = d->ho; p.wo = d->wo; p.k = d->k;
@@ -1037,6 +1158,8 @@ static ConvArgs make_args(const rtsds_conv_desc* d) {
   p.tiles_per_split = 1 << 30;
   const int hw = d->ho * d->wo;
   p.wg_rows = (hw % 64 == 0) && (d->wo % 64 == 0 || 64 % d->wo == 0);
+  const long big = std::max((long)d->n * d->h * d->w * d->c, (long)d->n * d->ho * d->wo * d->k) * (long)esize(d->dtype);
+  p.gbuf = big < (1L << 31) && (long)d->k * d->kh * d->kw * d->c * (long)esize(d->dtype) < (1L << 31);
   return p;
 }
 
@@ -1066,7 +1189,6 @@ static int pad_c(int c, int dtype) {
   return (c + V - 1) / V * V;
 }
 static size_t al256(size_t b) { return (b + 255) & ~(size_t)255; }
-static size_t esize(int dtype) { return dtype == RTSDS_BF16 ? 2 : 4; }
 
 template <typename T>
 static void pad_launch(const void* src, void* dst, long rows, int c, int cp, hipStream_t st) {
@@ -1102,7 +1224,11 @@ static bool glds_enabled() {
 static void pick_tile(long M, int N, bool b16, int& bm, int& bn) {
   auto blocks = [&](int a, int b) { return ((M + a - 1) / a) * (long)((N + b - 1) / b); };
   if (b16) {
+#ifdef RTSDS_N32_BM128
+    if (N <= 32) { bn = 32; bm = 128; }
+#else
     if (N <= 32) { bn = 32; bm = blocks(256, 32) >= 256 ? 256 : 128; }
+#endif
     else if (N <= 64) { bn = 64; bm = blocks(128, 64) >= 256 ? 128 : 64; }
     else if (blocks(128, 128) >= 256) { bm = 128; bn = 128; }
     else { bm = 64; bn = 64; }
@@ -1120,8 +1246,13 @@ static void launch_al(const ConvArgs& p, int cr, hipStream_t st) {
     // (not for 3-channel images padded to 8: eight taps per K-tile gathered per chunk lose
     // to the register path there)
     if (glds_enabled() && cr % 32 == 0 && p.K % 8 == 0) {
-      if (cr % 64 == 0) launch<T, MODE, BM, BN, 64, WM, WN, 2, 1, 2>(p, 1, st);
-      else launch<T, MODE, BM, BN, 64, WM, WN, 1, 1, 2>(p, 1, st);
+#ifndef RTSDS_GLN
+#define RTSDS_GLN 2
+#endif
+      // ALA 2 (buffer-offset DMA): DGRAD only at stride 1 or in the stride-2 parity phases
+      const bool gb_ok = p.gbuf && (MODE != MODE_DGRAD || (p.sh == p.sw && (p.sh == 1 || (p.sh == 2 && p.psh == 2))));
+      if (cr % 64 == 0 && gb_ok) launch<T, MODE, BM, BN, 64, WM, WN, 2, 1, RTSDS_GLN>(p, 1, st);
+      else launch<T, MODE, BM, BN, 64, WM, WN, 1, 1, RTSDS_GLN>(p, 1, st);
       return;
     }
   }
