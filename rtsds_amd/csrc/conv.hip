@@ -1276,8 +1276,195 @@ static void dispatch_align(const ConvArgs& p, int cr, hipStream_t st) {
   }
 }
 
+// ---- pooled-vector 1x1 convs (ARM / FFM attention on [N, C, 1, 1], build_bisenet.py:41,
+// 67-69): M = N <= 32 rows, a GEMV-sized problem.  One launch per pass, no channel padding,
+// fp32 accumulation, BatchNorm partial statistics (one "tile" of M rows) from the exact values.
+static const int kPooledMaxRows = 32;
+static bool pooled_1x1(const rtsds_conv_desc* d) {
+  return d->h == 1 && d->w == 1 && d->kh == 1 && d->kw == 1 && d->sh == 1 && d->sw == 1 && d->ph == 0 &&
+         d->pw == 0 && d->n <= kPooledMaxRows;
+}
+
+// y[m][k] = act(sum_c x[m][c] w[k][c] + bias[k]); one wave per output channel k.
+template <typename T, int MR>
+__global__ void __launch_bounds__(256) pooled_fwd_kernel(const T* __restrict__ x, const T* __restrict__ w,
+                                                        const float* __restrict__ bias, T* __restrict__ y, int m_n, int c,
+                                                        int k_n, int act, int accum, float* __restrict__ stats) {
+  const int k = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (k >= k_n) return;
+  float acc[MR];
+#pragma unroll
+  for (int m = 0; m < MR; ++m) acc[m] = 0.f;
+  for (int ci = lane; ci < c; ci += 64) {
+    const float wv = to_f(w[(long)k * c + ci]);
+#pragma unroll
+    for (int m = 0; m < MR; ++m)
+      if (m < m_n) acc[m] = fmaf(to_f(x[(long)m * c + ci]), wv, acc[m]);
+  }
+#pragma unroll
+  for (int m = 0; m < MR; ++m)
+    if (m < m_n) acc[m] = wave_sum(acc[m]);
+  if (lane != 0) return;
+  const float bv = bias ? bias[k] : 0.f;
+  float mean = 0.f;
+#pragma unroll
+  for (int m = 0; m < MR; ++m)
+    if (m < m_n) {
+      float v = acc[m] + bv;
+      acc[m] = v;
+      mean += v;
+      if (accum) v += to_f(y[(long)m * k_n + k]);
+      if (act == RTSDS_ACT_RELU) v = fmaxf(v, 0.f);
+      else if (act == RTSDS_ACT_LEAKY) v = v > 0.f ? v : 0.2f * v;
+      else if (act == RTSDS_ACT_SIGMOID) v = 1.f / (1.f + expf(-v));
+      y[(long)m * k_n + k] = from_f<T>(v);
+    }
+  if (stats) {
+    mean /= (float)m_n;
+    float m2 = 0.f;
+#pragma unroll
+    for (int m = 0; m < MR; ++m)
+      if (m < m_n) m2 += (acc[m] - mean) * (acc[m] - mean);
+    stats[k * 3 + 0] = (float)m_n;
+    stats[k * 3 + 1] = mean;
+    stats[k * 3 + 2] = m2;
+  }
+}
+
+// dx[m][c] (+)= sum_k dy[m][k] w[k][c]; one wave per input channel c, lanes over k.
+template <typename T, int MR>
+__global__ void __launch_bounds__(256) pooled_dgrad_kernel(const T* __restrict__ dy, const T* __restrict__ w, T* __restrict__ dx,
+                                                          int m_n, int c, int k_n, int accum) {
+  const int ci = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (ci >= c) return;
+  float acc[MR];
+#pragma unroll
+  for (int m = 0; m < MR; ++m) acc[m] = 0.f;
+  for (int k = lane; k < k_n; k += 64) {
+    const float wv = to_f(w[(long)k * c + ci]);
+#pragma unroll
+    for (int m = 0; m < MR; ++m)
+      if (m < m_n) acc[m] = fmaf(to_f(dy[(long)m * k_n + k]), wv, acc[m]);
+  }
+#pragma unroll
+  for (int m = 0; m < MR; ++m)
+    if (m < m_n) acc[m] = wave_sum(acc[m]);
+  if (lane != 0) return;
+#pragma unroll
+  for (int m = 0; m < MR; ++m)
+    if (m < m_n) {
+      const long o = (long)m * c + ci;
+      dx[o] = from_f<T>(accum ? acc[m] + to_f(dx[o]) : acc[m]);
+    }
+}
+
+// dw[k][c] (+)= sum_m dy[m][k] x[m][c] (fp32), dbias[k] (+)= sum_m dy[m][k]; one thread per (k, c).
+template <typename T>
+__global__ void __launch_bounds__(256) pooled_wgrad_kernel(const T* __restrict__ x, const T* __restrict__ dy, float* __restrict__ dw,
+                                                          float* __restrict__ dbias, int m_n, int c, int k_n, int accum) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= k_n * c) return;
+  const int k = i / c, ci = i - k * c;
+  float acc = 0.f, bsum = 0.f;
+  for (int m = 0; m < m_n; ++m) {
+    const float g = to_f(dy[(long)m * k_n + k]);
+    acc = fmaf(g, to_f(x[(long)m * c + ci]), acc);
+    bsum += g;
+  }
+  dw[i] = accum ? dw[i] + acc : acc;
+  if (dbias && ci == 0) dbias[k] = accum ? dbias[k] + bsum : bsum;
+}
+
+template <typename T>
+static void pooled_fwd_launch(const rtsds_conv_desc* d, const void* x, const void* w, const float* bias, void* y, int act,
+                              int accum, float* stats, hipStream_t st) {
+  if (d->n <= 8)
+    hipLaunchKernelGGL((pooled_fwd_kernel<T, 8>), dim3(rt_cdiv(d->k, 4)), dim3(256), 0, st, (const T*)x, (const T*)w, bias,
+                       (T*)y, d->n, d->c, d->k, act, accum, stats);
+  else
+    hipLaunchKernelGGL((pooled_fwd_kernel<T, kPooledMaxRows>), dim3(rt_cdiv(d->k, 4)), dim3(256), 0, st, (const T*)x,
+                       (const T*)w, bias, (T*)y, d->n, d->c, d->k, act, accum, stats);
+}
+template <typename T>
+static void pooled_dgrad_launch(const rtsds_conv_desc* d, const void* dy, const void* w, void* dx, int accum, hipStream_t st) {
+  if (d->n <= 8)
+    hipLaunchKernelGGL((pooled_dgrad_kernel<T, 8>), dim3(rt_cdiv(d->c, 4)), dim3(256), 0, st, (const T*)dy, (const T*)w,
+                       (T*)dx, d->n, d->c, d->k, accum);
+  else
+    hipLaunchKernelGGL((pooled_dgrad_kernel<T, kPooledMaxRows>), dim3(rt_cdiv(d->c, 4)), dim3(256), 0, st, (const T*)dy,
+                       (const T*)w, (T*)dx, d->n, d->c, d->k, accum);
+}
+template <typename T>
+static void pooled_wgrad_launch(const rtsds_conv_desc* d, const void* x, const void* dy, float* dw, float* dbias, int accum,
+                                hipStream_t st) {
+  hipLaunchKernelGGL(pooled_wgrad_kernel<T>, dim3(rt_cdiv((long)d->k * d->c, 256)), dim3(256), 0, st, (const T*)x,
+                     (const T*)dy, dw, dbias, d->n, d->c, d->k, accum);
+}
+
+// ---- 3-channel stride-2 convs on the image (ResNet stem 7x7 s2 p3, build_contextpath.py via
+// torchvision conv1; spatial-path ConvBlock 3x3 s2 p1, build_bisenet.py:9-14).  Gathering one
+// 16-B chunk per tap would carry 3 useful channels of 8 (and 8/3 of the MFMA K): instead the
+// image is padded to 4 channels and viewed as "superpixels" of two horizontally adjacent
+// pixels (8 bf16 = one 16-B chunk).  With odd padding pw, taps s = 2p - 1 + q (q = 0, 1) of
+// output column ow read superpixel ow - (pw + 1) / 2 + p, so the conv becomes an ordinary
+// implicit GEMM over (row tap, tap pair, 8 elements) with stride (2, 1): K = kh * (kw + 1) / 2 * 8
+// (stem: 224 instead of 392), every chunk 16-B aligned and fully in or out of the padding.
+static bool sp_path(const rtsds_conv_desc* d) {
+  return d->dtype == RTSDS_BF16 && d->c == 3 && d->sh == 2 && d->sw == 2 && d->dh == 1 && d->dw == 1 &&
+         (d->pw & 1) == 1 && (d->kw & 1) == 1 && (d->w & 1) == 0;
+}
+static rtsds_conv_desc sp_desc(const rtsds_conv_desc* d) {
+  rtsds_conv_desc v = *d;
+  v.w = d->w / 2;
+  v.c = 8;
+  v.kw = (d->kw + 1) / 2;
+  v.sw = 1;
+  v.pw = (d->pw + 1) / 2;
+  return v;
+}
+__global__ void __launch_bounds__(256) sp_pad4_kernel(const bf16* __restrict__ x, bf16* __restrict__ x4, long pixels) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= pixels) return;
+  bf16x4 v;
+  v[0] = x[i * 3];
+  v[1] = x[i * 3 + 1];
+  v[2] = x[i * 3 + 2];
+  v[3] = (bf16)0.f;
+  *(bf16x4*)(x4 + i * 4) = v;
+}
+// w[k][r][s][3] -> w'[k][r][p][q*4 + ch], s = 2p - 1 + q (zero outside [0, kw), ch == 3).
+__global__ void __launch_bounds__(256) sp_repack_w_kernel(const bf16* __restrict__ w, bf16* __restrict__ wp, int k, int kh,
+                                                          int kw, int kwp) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= k * kh * kwp * 8) return;
+  const int e = i & 7, t = i >> 3;
+  const int p = t % kwp, kr = t / kwp;  // kr = co * kh + r
+  const int s = 2 * p - 1 + (e >> 2), ch = e & 3;
+  wp[i] = (s >= 0 && s < kw && ch < 3) ? w[((long)kr * kw + s) * 3 + ch] : (bf16)0.f;
+}
+// dW'[k][r][p][8] (fp32) -> dw[k][r][s][3] (+=).
+__global__ void __launch_bounds__(256) sp_unpack_dw_kernel(const float* __restrict__ dwp, float* __restrict__ dw, int k, int kh,
+                                                           int kw, int kwp, int accumulate) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= k * kh * kw * 3) return;
+  const int ch = i % 3, t = i / 3;
+  const int s = t % kw, kr = t / kw;
+  const int p = (s + 1) >> 1, q = (s + 1) & 1;
+  const float v = dwp[((long)kr * kwp + p) * 8 + q * 4 + ch];
+  dw[i] = accumulate ? dw[i] + v : v;
+}
+static size_t sp_x4_bytes(const rtsds_conv_desc* d) { return ((size_t)d->n * d->h * d->w * 8 + 255) & ~(size_t)255; }
+static size_t sp_w_bytes(const rtsds_conv_desc* d) {
+  return ((size_t)d->k * d->kh * ((d->kw + 1) / 2) * 16 + 255) & ~(size_t)255;
+}
+static void sp_pad4(const rtsds_conv_desc* d, const void* x, void* x4, hipStream_t st) {
+  const long px = (long)d->n * d->h * d->w;
+  hipLaunchKernelGGL(sp_pad4_kernel, dim3((unsigned)((px + 255) / 256)), dim3(256), 0, st, (const bf16*)x, (bf16*)x4, px);
+}
+
 // Number of M tiles (= BatchNorm partial-statistics rows) the forward launch of d uses.
 extern "C" int rtsds_conv2d_fwd_stats_tiles(const rtsds_conv_desc* d) {
+  if (pooled_1x1(d)) return 1;
   int bm, bn;
   const long M = (long)d->n * d->ho * d->wo;
   pick_tile(M, d->k, d->dtype == RTSDS_BF16, bm, bn);
@@ -1286,19 +1473,31 @@ extern "C" int rtsds_conv2d_fwd_stats_tiles(const rtsds_conv_desc* d) {
 
 // FWD workspace: channel-padded copies of x and w when Cin is not a vector multiple.
 extern "C" size_t rtsds_conv2d_fwd_workspace(const rtsds_conv_desc* d) {
+  if (pooled_1x1(d)) return 0;
+  if (sp_path(d)) return sp_x4_bytes(d) + sp_w_bytes(d);
   const int cp = pad_c(d->c, d->dtype);
   if (cp == d->c) return 0;
   const size_t es = esize(d->dtype);
   return al256((size_t)d->n * d->h * d->w * cp * es) + al256((size_t)d->k * d->kh * d->kw * cp * es);
 }
 
-extern "C" int rtsds_conv2d_fwd(const rtsds_conv_desc* d0, const void* x, const void* w, const float* bias,
-                                void* y, int act, float* bn_stats, void* ws, size_t ws_bytes, void* stream) {
-  int e = check_desc(d0);
-  if (e) return e;
-  if (ws_bytes < rtsds_conv2d_fwd_workspace(d0)) return RTSDS_ERR_WORKSPACE;
-  hipStream_t st = (hipStream_t)stream;
-  rtsds_conv_desc d = *d0;
+// Operands of the forward GEMM: the superpixel view of 3-channel stride-2 convs, or
+// channel-padded copies when Cin is not a vector multiple (workspace), else x / w as given.
+static void fwd_prepare(const rtsds_conv_desc* d0, const void*& x, const void*& w, void* ws, rtsds_conv_desc& d,
+                        hipStream_t st) {
+  d = *d0;
+  if (sp_path(d0)) {
+    void* x4 = ws;
+    void* wp = (char*)ws + sp_x4_bytes(d0);
+    sp_pad4(d0, x, x4, st);
+    const int n = d0->k * d0->kh * ((d0->kw + 1) / 2) * 8;
+    hipLaunchKernelGGL(sp_repack_w_kernel, dim3(rt_cdiv(n, 256)), dim3(256), 0, st, (const bf16*)w, (bf16*)wp, d0->k,
+                       d0->kh, d0->kw, (d0->kw + 1) / 2);
+    d = sp_desc(d0);
+    x = x4;
+    w = wp;
+    return;
+  }
   const int cp = pad_c(d.c, d.dtype);
   if (cp != d.c) {
     const size_t es = esize(d.dtype);
@@ -1310,6 +1509,23 @@ extern "C" int rtsds_conv2d_fwd(const rtsds_conv_desc* d0, const void* x, const 
     w = wp;
     d.c = cp;
   }
+}
+
+extern "C" int rtsds_conv2d_fwd(const rtsds_conv_desc* d0, const void* x, const void* w, const float* bias,
+                                void* y, int act, float* bn_stats, void* ws, size_t ws_bytes, void* stream) {
+  int e = check_desc(d0);
+  if (e) return e;
+  if (ws_bytes < rtsds_conv2d_fwd_workspace(d0)) return RTSDS_ERR_WORKSPACE;
+  hipStream_t st = (hipStream_t)stream;
+  if (pooled_1x1(d0)) {
+    const int accum = (act & RTSDS_ACCUMULATE) ? 1 : 0;
+    if (bn_stats && ((act & 0xff) || accum)) return RTSDS_ERR_UNSUPPORTED;
+    if (d0->dtype == RTSDS_BF16) pooled_fwd_launch<bf16>(d0, x, w, bias, y, act & 0xff, accum, bn_stats, st);
+    else pooled_fwd_launch<float>(d0, x, w, bias, y, act & 0xff, accum, bn_stats, st);
+    return hipGetLastError() == hipSuccess ? RTSDS_OK : RTSDS_ERR_LAUNCH;
+  }
+  rtsds_conv_desc d;
+  fwd_prepare(d0, x, w, ws, d, st);
   ConvArgs p = make_args(&d);
   p.a = x; p.b = w; p.bias = bias; p.out = y;
   p.act = act & 0xff;
@@ -1334,18 +1550,8 @@ extern "C" int rtsds_conv2d_fwd_bn(const rtsds_conv_desc* d0, const void* x, con
   if (e) return e;
   if (ws_bytes < rtsds_conv2d_fwd_workspace(d0)) return RTSDS_ERR_WORKSPACE;
   hipStream_t st = (hipStream_t)stream;
-  rtsds_conv_desc d = *d0;
-  const int cp = pad_c(d.c, d.dtype);
-  if (cp != d.c) {
-    const size_t es = esize(d.dtype);
-    void* xp = ws;
-    void* wp = (char*)ws + al256((size_t)d.n * d.h * d.w * cp * es);
-    pad_any(d.dtype, x, xp, (long)d.n * d.h * d.w, d.c, cp, st);
-    pad_any(d.dtype, w, wp, (long)d.k * d.kh * d.kw, d.c, cp, st);
-    x = xp;
-    w = wp;
-    d.c = cp;
-  }
+  rtsds_conv_desc d;
+  fwd_prepare(d0, x, w, ws, d, st);
   ConvArgs p = make_args(&d);
   p.a = x; p.b = w; p.bias = shift; p.scale = scale; p.res = res; p.out = y;
   p.act = act & 0xff;
@@ -1359,6 +1565,7 @@ extern "C" int rtsds_conv2d_fwd_bn(const rtsds_conv_desc* d0, const void* x, con
 
 // DGRAD workspace: repacked (and Cout-padded) weights + a Cout-padded copy of dy if needed.
 extern "C" size_t rtsds_conv2d_dgrad_workspace(const rtsds_conv_desc* d) {
+  if (pooled_1x1(d)) return 0;
   const int kp = pad_c(d->k, d->dtype);
   const size_t es = esize(d->dtype);
   size_t b = al256((size_t)kp * d->kh * d->kw * d->c * es);
@@ -1395,6 +1602,11 @@ extern "C" int rtsds_conv2d_dgrad(const rtsds_conv_desc* d0, const void* dy, con
   if (d0->sh > 2 || d0->sw > 2) return RTSDS_ERR_UNSUPPORTED;
   if (ws_bytes < rtsds_conv2d_dgrad_workspace(d0)) return RTSDS_ERR_WORKSPACE;
   hipStream_t st = (hipStream_t)stream;
+  if (pooled_1x1(d0)) {
+    if (d0->dtype == RTSDS_BF16) pooled_dgrad_launch<bf16>(d0, dy, w, dx, accumulate ? 1 : 0, st);
+    else pooled_dgrad_launch<float>(d0, dy, w, dx, accumulate ? 1 : 0, st);
+    return hipGetLastError() == hipSuccess ? RTSDS_OK : RTSDS_ERR_LAUNCH;
+  }
   rtsds_conv_desc d = *d0;
   const int kp = pad_c(d.k, d.dtype);
   const size_t es = esize(d.dtype);
@@ -1477,6 +1689,12 @@ static WgradPlan wgrad_plan(const rtsds_conv_desc* d) {
 }
 
 extern "C" size_t rtsds_conv2d_wgrad_workspace(const rtsds_conv_desc* d) {
+  if (pooled_1x1(d)) return 0;
+  if (sp_path(d)) {
+    const rtsds_conv_desc v = sp_desc(d);
+    const WgradPlan w = wgrad_plan(&v);
+    return w.slab_bytes + w.colsum_bytes + sp_x4_bytes(d) + al256((size_t)v.k * v.kh * v.kw * 8 * 4);
+  }
   const WgradPlan w = wgrad_plan(d);
   return w.slab_bytes + w.dyp_bytes + w.xp_bytes + w.colsum_bytes;
 }
@@ -1505,20 +1723,34 @@ extern "C" int rtsds_conv2d_wgrad(const rtsds_conv_desc* d0, const void* x, cons
   if (e) return e;
   if (ws_bytes < rtsds_conv2d_wgrad_workspace(d0)) return RTSDS_ERR_WORKSPACE;
   hipStream_t st = (hipStream_t)stream;
-  const WgradPlan pl = wgrad_plan(d0);
+  if (pooled_1x1(d0)) {
+    if (d0->dtype == RTSDS_BF16) pooled_wgrad_launch<bf16>(d0, x, dy, dw, dbias, accumulate ? 1 : 0, st);
+    else pooled_wgrad_launch<float>(d0, x, dy, dw, dbias, accumulate ? 1 : 0, st);
+    return hipGetLastError() == hipSuccess ? RTSDS_OK : RTSDS_ERR_LAUNCH;
+  }
+  const bool sp = sp_path(d0);
+  const rtsds_conv_desc dv = sp ? sp_desc(d0) : *d0;
+  const WgradPlan pl = wgrad_plan(&dv);
   char* slab = (char*)ws;
   char* dyp = slab + pl.slab_bytes;
   char* xp = dyp + pl.dyp_bytes;
   float* part = (float*)(xp + pl.xp_bytes);
   const long R = (long)d0->n * d0->ho * d0->wo;
-  rtsds_conv_desc d = *d0;
+  rtsds_conv_desc d = dv;
   const void* dyk = dy;
+  float* dws = nullptr;  // superpixel path: dW' [k][kh][kwp][8] before the unpack
+  if (sp) {
+    void* x4 = (char*)part + pl.colsum_bytes;
+    dws = (float*)((char*)x4 + sp_x4_bytes(d0));
+    sp_pad4(d0, x, x4, st);
+    x = x4;
+  }
   if (pl.kp != d.k) {
     pad_any(d.dtype, dy, dyp, R, d.k, pl.kp, st);
     dyk = dyp;
     d.k = pl.kp;
   }
-  if (pl.cp != d.c) {
+  if (!sp && pl.cp != d.c) {
     pad_any(d.dtype, x, xp, (long)d.n * d.h * d.w, d.c, pl.cp, st);
     x = xp;
     d.c = pl.cp;
@@ -1533,7 +1765,14 @@ extern "C" int rtsds_conv2d_wgrad(const rtsds_conv_desc* d0, const void* x, cons
   p.out = slab;
   if (d.dtype == RTSDS_BF16) wgrad_launch<bf16>(p, pl.bm, pl.bn, pl.splits, st);
   else wgrad_launch<float>(p, pl.bm, pl.bn, pl.splits, st);
-  {
+  if (sp) {
+    const int nv = dv.k * dv.kh * dv.kw * 2;
+    hipLaunchKernelGGL(split_reduce_kernel<4>, dim3(std::min(8192, (nv + 255) / 256)), dim3(256), 0, st, (const float*)slab, dws,
+                       nv, 2, fastdiv_make(2), 8, p.split_stride, pl.splits, 0);
+    const int n = d0->k * d0->kh * d0->kw * 3;
+    hipLaunchKernelGGL(sp_unpack_dw_kernel, dim3(rt_cdiv(n, 256)), dim3(256), 0, st, (const float*)dws, dw, d0->k, d0->kh,
+                       d0->kw, dv.kw, accumulate);
+  } else {
     const int V = d0->c % 4 == 0 ? 4 : 1, cv = d0->c / V;
     const int nv = d0->k * d0->kh * d0->kw * cv;
     const int blocks = std::min(8192, (nv + 255) / 256);
