@@ -173,6 +173,7 @@ def main():
     t0 = time.perf_counter()
     for i in range(args.steps):
         loss, corr = step(args.warmup + i)
+    t_enqueue = time.perf_counter() - t0
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -261,6 +262,7 @@ def main():
                      "conv_gflop_per_step": round(conv_flop / 1e9, 1)},
         "whole_step_conv_flop_rate_tflops": round(wl[5] * args.batch / ms, 2),
         "final_loss": round(final_loss, 4),
+        "host_enqueue_ms_per_step": round(1000.0 * t_enqueue / args.steps, 3),
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.workload == "bisenet-seg":
         out["cpu_baseline"] = cpu_baseline()

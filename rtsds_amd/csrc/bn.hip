@@ -9,7 +9,13 @@
 #include "common.h"
 #include <algorithm>
 
-static const int kBnMaxRB = 2048;  // row blocks of the partial-statistics pass
+#ifndef RTSDS_BN_MAXRB
+#define RTSDS_BN_MAXRB 2048
+#endif
+#ifndef RTSDS_BN_RPT
+#define RTSDS_BN_RPT 8
+#endif
+static const int kBnMaxRB = RTSDS_BN_MAXRB;  // row blocks of the partial-statistics pass
 
 // Threads of a 256-block are laid out [row group][channel vector]; TPR = threads per row.
 template <int VEC> struct BnLayout {
@@ -380,6 +386,36 @@ __global__ void __launch_bounds__(256) bn_bwd_stats_kernel(const T* __restrict__
       }
     }
   }
+  if ((L.tpr & (L.tpr - 1)) == 0 && L.tpr <= 64) {
+    // power-of-two row width: sum the wave's rows with xor shuffles (lanes l and l ^ (tpr << i)
+    // hold the same channel vector), then the four wave sums through LDS -- a per-block tail of
+    // a few hundred cycles instead of a serial LDS loop over all rpi rows.
+    const int lane = tid & 63, wave = tid >> 6;
+    for (int o = L.tpr; o < 64; o <<= 1) {
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) {
+        sg[j] += __shfl_xor(sg[j], o, 64);
+        sgx[j] += __shfl_xor(sgx[j], o, 64);
+      }
+    }
+    if (lane < L.tpr) {
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) { red[0][wave * 64 + lane][j] = sg[j]; red[1][wave * 64 + lane][j] = sgx[j]; }
+    }
+    __syncthreads();
+    if (tid < L.tpr && tid * VEC < cl) {
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) {
+        const float a = (red[0][tid][j] + red[0][64 + tid][j]) + (red[0][128 + tid][j] + red[0][192 + tid][j]);
+        const float b = (red[1][tid][j] + red[1][64 + tid][j]) + (red[1][128 + tid][j] + red[1][192 + tid][j]);
+        if (ch0 + j < c) {
+          float* o = part + ((long)blockIdx.x * c + ch0 + j) * 2;
+          o[0] = a; o[1] = b;
+        }
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int j = 0; j < VEC; ++j) { red[0][tid][j] = sg[j]; red[1][tid][j] = sgx[j]; }
   __syncthreads();
@@ -495,7 +531,7 @@ static long bn_need(long rows, int c, int vec) {
 static int bn_rb(long rows, int c, int vec) {
   const long need = bn_need(rows, c, vec);
   long rb = std::min<long>(need, kBnMaxRB);
-  rb = std::max<long>(1, std::min<long>(rb, (need + 3) / 4));
+  rb = std::max<long>(1, std::min<long>(rb, (need + RTSDS_BN_RPT - 1) / RTSDS_BN_RPT));
   return (int)rb;
 }
 // Row blocks of the elementwise passes: ~2 rows per thread.

@@ -559,11 +559,17 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(const ConvArgs P) {
         __builtin_amdgcn_global_load_lds((glb_t)src, (lds_t)(sb + rb * BN), 16, 0, 0);
       }
     } else if constexpr (GB) {
-      const int k0 = kt * BK;
       T* sa = smem + buf * (A_EL + B_EL);
       T* sb = sa + A_EL;
+      // K-tiles run channel-chunk-major, tap-minor: the taps of one 64-channel chunk follow
+      // each other, so the tile's input rows (+ halo) for that chunk stay in L2 across the
+      // taps instead of being re-fetched from MALL/HBM once per tap (the channel-major order
+      // streams the whole Cin between two taps: 16 MB per XCD for the 1024-channel FFM conv).
       const int Cr = (MODE == MODE_FWD) ? P.c : P.k;
-      const int tap = k0 / Cr, ci = k0 - tap * Cr;
+      const unsigned ntap = (unsigned)(P.K / Cr);
+      const unsigned q = (unsigned)kt / ntap;
+      const int tap = (int)((unsigned)kt - q * ntap), ci = (int)q * BK;
+      const int kb = tap * Cr + ci;  // B column of this K-tile
       int r, sx;
       if (MODE == MODE_FWD) {
         r = tap / P.kw;
@@ -587,7 +593,7 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(const ConvArgs P) {
       }
 #pragma unroll
       for (int i = 0; i < NB; ++i)
-        buf_lds16(rs_b, sb + (i * 32 + wave * 8) * BK, gbb_off[i], k0 * 2);
+        buf_lds16(rs_b, sb + (i * 32 + wave * 8) * BK, gbb_off[i], kb * 2);
     } else if constexpr (G) {
       typedef __attribute__((address_space(3))) void* lds_t;
       typedef const __attribute__((address_space(1))) void* glb_t;
