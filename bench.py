@@ -60,6 +60,8 @@ def parse():
     ap.add_argument("--no-infer", action="store_true")
     ap.add_argument("--conv-report", action="store_true")
     ap.add_argument("--no-conv-profile", action="store_true", help="skip the event-timed roofline step")
+    ap.add_argument("--graph", default="auto", choices=["auto", "on", "off"],
+                    help="replay the iteration as a hipGraph (auto: single process)")
     return ap.parse_args()
 
 
@@ -128,10 +130,12 @@ def build(args, dev, rank):
     x, y = synthetic_batch(args.batch, 42 + 2 * rank, dev, h, w)
     max_iter = 1000
     if not da:
-        def step(i):
+        def set_lr(i):
             poly_lr_scheduler(opt, 1e-4, i, 1, max_iter, 0.9)
+
+        def core():
             return seg_step(net, crit, opt, x, y)
-        return net, x, step
+        return net, x, set_lr, core, [opt]
     from rtsds_amd.models.domain_shift.adversarial.model import TinyDomainDiscriminator
     disc = TinyDomainDiscriminator(NC).to(dev).train()
     dopt = optim.Adam(disc.parameters(), lr=1e-4, weight_decay=1e-4)
@@ -139,11 +143,13 @@ def build(args, dev, rank):
     xt, _ = synthetic_batch(args.batch, 43 + 2 * rank, dev, h, w)
     poly_lr_scheduler(dopt, 1e-4, 0, 1, 10, 0.05)  # per epoch (train.py:167)
 
-    def step(i):
+    def set_lr(i):
         poly_lr_scheduler(opt, 1e-4, i, 1, max_iter, 0.9)
+
+    def core():
         out = da_step(net, disc, opt, dopt, crit, bce, x, y, xt, 0.1, 100)  # lambda, iterations: config.yaml
         return out[0], out[-1]
-    return net, x, step
+    return net, x, set_lr, core, [opt, dopt]
 
 
 def main():
@@ -162,10 +168,25 @@ def main():
     set_compute_dtype(dtype)
     optim.set_allreduce_dtype({"fp32": torch.float32, "fp16": torch.float16, "bf16": torch.bfloat16}[args.allreduce_dtype])
     torch.manual_seed(42)
-    net, x, step = build(args, dev, rank)
+    net, x, set_lr, core, opts = build(args, dev, rank)
+    use_graph = args.graph == "on" or (args.graph == "auto" and world == 1)
+
+    def step(i):
+        set_lr(i)
+        return core()
 
     for i in range(args.warmup):
         step(i)
+    if use_graph:
+        # the whole iteration as one hipGraph replay (runtime.GraphedStep): same kernels, no
+        # per-kernel host launches; lr / Adam step advance through a device buffer
+        from rtsds_amd.runtime import GraphedStep
+        graphed = GraphedStep(core, opts, warmup=1)
+
+        def step(i):
+            set_lr(i)
+            return graphed()
+        step(args.warmup)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -191,7 +212,8 @@ def main():
     recs = []
     if not args.no_conv_profile:
         F.CONV_PROFILE = []
-        step(args.warmup + args.steps)
+        set_lr(args.warmup + args.steps)
+        core()  # eager: HIP events around each conv launch
         torch.cuda.synchronize()
         recs, F.CONV_PROFILE = F.CONV_PROFILE, None
     conv_ms = sum(r[0].elapsed_time(r[1]) for r in recs) or float("nan")
@@ -263,6 +285,7 @@ def main():
         "whole_step_conv_flop_rate_tflops": round(wl[5] * args.batch / ms, 2),
         "final_loss": round(final_loss, 4),
         "host_enqueue_ms_per_step": round(1000.0 * t_enqueue / args.steps, 3),
+        "hip_graph": use_graph,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.workload == "bisenet-seg":
         out["cpu_baseline"] = cpu_baseline()

@@ -204,6 +204,13 @@ int rtsds_adam_step(float* param, const float* grad, float* exp_avg, float* exp_
                     void* bf16_shadow, long n, float lr, float beta1, float beta2, float eps,
                     float weight_decay, int step, float grad_scale, void* stream);
 
+/* The same update with hyper = {lr, 1 - beta1^step, sqrt(1 - beta2^step)} (fp32, device
+ * memory) read by the kernel: a captured hipGraph of the training step replays correct
+ * updates while the host advances lr and step between replays.                            */
+int rtsds_adam_step_dev(float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
+                        void* bf16_shadow, long n, const float* hyper, float beta1, float beta2,
+                        float eps, float weight_decay, float grad_scale, void* stream);
+
 /* ---------------------------------------------------------------- metrics
  * argmax over channels, first maximum wins (train.py:102-106,272-275; validation.py:51).
  * out (int64 [n*hw]) may be NULL; if target and correct are given, *correct += #matches.

@@ -997,6 +997,38 @@ __global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, 
     if (shadow) shadow[i] = (bf16)pi;
   }
 }
+// Same update with (lr, bias_correction1, sqrt(bias_correction2)) read from device memory, so
+// a captured hipGraph replays correct steps as the host advances lr / step counts between
+// replays (runtime.GraphedStep).
+__global__ void adam_dev_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m, float* __restrict__ v,
+                                bf16* __restrict__ shadow, long n, const float* __restrict__ hyper, float b1, float b2, float eps,
+                                float wd, float gscale) {
+  const float lr = hyper[0], bc1 = hyper[1], bc2_sqrt = hyper[2];
+  const float step = lr / bc1;
+  GRID_STRIDE(i, n) {
+    float gi = g[i] * gscale;
+    float pi = p[i];
+    if (wd != 0.f) gi = fmaf(wd, pi, gi);
+    float mi = m[i], vi = v[i];
+    mi = fmaf(1.f - b1, gi - mi, mi);
+    vi = fmaf(b2, vi, (1.f - b2) * gi * gi);
+    const float den = sqrtf(vi) / bc2_sqrt + eps;
+    pi -= step * (mi / den);
+    m[i] = mi;
+    v[i] = vi;
+    p[i] = pi;
+    if (shadow) shadow[i] = (bf16)pi;
+  }
+}
+extern "C" int rtsds_adam_step_dev(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, void* bf16_shadow,
+                                   long n, const float* hyper, float beta1, float beta2, float eps, float weight_decay,
+                                   float grad_scale, void* stream) {
+  if (n <= 0 || !hyper) return RTSDS_ERR_SHAPE;
+  hipLaunchKernelGGL(adam_dev_kernel, dim3(ew_blocks(n, 256, 4096)), dim3(256), 0, (hipStream_t)stream, param, grad, exp_avg,
+                     exp_avg_sq, (bf16*)bf16_shadow, n, hyper, beta1, beta2, eps, weight_decay, grad_scale);
+  RET_LAUNCH();
+}
+
 extern "C" int rtsds_adam_step(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, void* bf16_shadow, long n, float lr,
                                float beta1, float beta2, float eps, float weight_decay, int step, float grad_scale, void* stream) {
   if (n <= 0 || step <= 0) return RTSDS_ERR_SHAPE;

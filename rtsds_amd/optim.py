@@ -127,6 +127,11 @@ class Adam(torch.optim.Optimizer):
         super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
         self._arenas = None
         self._warned = False
+        # hipGraph mode (runtime.GraphedStep): lr and bias corrections come from a device buffer
+        self._graph = False      # launch rtsds_adam_step_dev
+        self._capturing = False  # inside stream capture: the hyper values are staged outside
+        self._runs = None        # [(group, i, j)] of the last step
+        self._hyper = None       # device fp32 [runs][lr, bc1, sqrt(bc2)]
 
     # ------------------------------------------------------------------ arena
     def _ensure(self):
@@ -159,26 +164,69 @@ class Adam(torch.optim.Optimizer):
                         self._warned = True
                     a.rebind_grad(i)
         gscale = allreduce_flat([a.gflat for a in arenas])
-        for g, a in zip(self.param_groups, arenas):
-            b1, b2 = g["betas"]
-            # contiguous runs of touched parameters with equal step counts -> one launch each
+        # contiguous runs of touched parameters with equal step counts -> one launch each
+        runs = []
+        for gi, a in enumerate(arenas):
             i, n = 0, len(a.params)
             while i < n:
                 if not a.touched[i]:
                     i += 1
                     continue
                 j = i
-                step = a.steps[i] + 1
-                while j + 1 < n and a.touched[j + 1] and a.steps[j + 1] + 1 == step:
+                while j + 1 < n and a.touched[j + 1] and a.steps[j + 1] == a.steps[i]:
                     j += 1
-                lo = a.offsets[i]
-                hi = a.offsets[j] + a.params[j].numel()
-                lib.rtsds_adam_step(a.flat.data_ptr() + 4 * lo, a.gflat.data_ptr() + 4 * lo,
-                                    a.m.data_ptr() + 4 * lo, a.v.data_ptr() + 4 * lo,
-                                    a.shadow.data_ptr() + 2 * lo, hi - lo, float(g["lr"]), float(b1),
-                                    float(b2), float(g["eps"]), float(g["weight_decay"]), step,
-                                    gscale, stream())
-                for k in range(i, j + 1):
-                    a.steps[k] = step
+                runs.append((gi, i, j))
                 i = j + 1
+        if self._capturing:
+            if runs != self._runs or self._hyper is None:
+                raise RuntimeError("rtsds_amd.Adam: step structure changed under graph capture")
+        else:
+            self._runs = runs
+            if self._graph:
+                self.stage_hyper()
+        for r, (gi, i, j) in enumerate(runs):
+            g, a = self.param_groups[gi], arenas[gi]
+            b1, b2 = g["betas"]
+            lo = a.offsets[i]
+            hi = a.offsets[j] + a.params[j].numel()
+            ptrs = (a.flat.data_ptr() + 4 * lo, a.gflat.data_ptr() + 4 * lo, a.m.data_ptr() + 4 * lo,
+                    a.v.data_ptr() + 4 * lo, a.shadow.data_ptr() + 2 * lo, hi - lo)
+            if self._graph:
+                lib.rtsds_adam_step_dev(*ptrs, self._hyper.data_ptr() + 12 * r, float(b1), float(b2),
+                                        float(g["eps"]), float(g["weight_decay"]), gscale, stream())
+            else:
+                lib.rtsds_adam_step(*ptrs, float(g["lr"]), float(b1), float(b2), float(g["eps"]),
+                                    float(g["weight_decay"]), a.steps[i] + 1, gscale, stream())
+            for k in range(i, j + 1):
+                a.steps[k] += 1
         return loss
+
+    # ------------------------------------------------------------------ hipGraph support
+    def set_graph_mode(self, on=True):
+        self._graph = bool(on)
+
+    def stage_hyper(self):
+        """Write (lr, 1 - beta1^t, sqrt(1 - beta2^t)) of the NEXT step of every run of the last
+        step into the device hyper buffer (stream-ordered H2D copy from pinned memory)."""
+        runs = self._runs or []
+        arenas = self._ensure()
+        vals = torch.empty(max(1, 3 * len(runs)), dtype=torch.float32, pin_memory=True)
+        for r, (gi, i, _) in enumerate(runs):
+            g = self.param_groups[gi]
+            # betas rounded to fp32 first, exactly as rtsds_adam_step receives them (eager and
+            # replayed steps then update bit-identically)
+            b1, b2 = (float(torch.tensor(b, dtype=torch.float32)) for b in g["betas"])
+            t = arenas[gi].steps[i] + 1
+            vals[3 * r] = float(g["lr"])
+            vals[3 * r + 1] = 1.0 - b1 ** t
+            vals[3 * r + 2] = (1.0 - b2 ** t) ** 0.5
+        if self._hyper is None or self._hyper.numel() < vals.numel():
+            self._hyper = torch.empty(vals.numel(), dtype=torch.float32, device=arenas[0].flat.device)
+        self._hyper[:vals.numel()].copy_(vals, non_blocking=True)
+
+    def advance_steps(self, by=1):
+        """Host step counters after a replayed step (the graph does not run Python)."""
+        arenas = self._ensure()
+        for gi, i, j in self._runs or []:
+            for k in range(i, j + 1):
+                arenas[gi].steps[k] += by

@@ -114,3 +114,52 @@ class GraphedForward:
         self.static_in.copy_(x)
         self.graph.replay()
         return self.static_out
+
+
+class GraphedStep:
+    """hipGraph of a whole training iteration (zero_grad, forward, losses, backward, optimizer
+    step).  ``fn()`` runs one iteration on fixed input buffers and returns device tensors; the
+    rtsds optimizers in ``optimizers`` switch to device-side hyperparameters
+    (optim.Adam.set_graph_mode) so that every replay applies the current learning rate
+    (``param_groups[..]["lr"]``, e.g. set by utils.poly_lr_scheduler before the call) and the
+    advancing Adam step count, staged by a stream-ordered H2D copy before the replay.  The
+    iteration must keep its launch structure (same shapes, same parameters receiving
+    gradients); no host synchronisation may happen inside ``fn``.  Single process: collectives
+    are not captured (data-parallel runs stay eager)."""
+
+    def __init__(self, fn, optimizers, warmup=2):
+        self.fn = fn
+        self.optimizers = list(optimizers)
+        for o in self.optimizers:
+            o.set_graph_mode(True)
+        cur = torch.cuda.current_stream()
+        side = torch.cuda.Stream(device=cur.device)
+        side.wait_stream(cur)
+        with torch.cuda.stream(side):
+            for _ in range(warmup):
+                fn()
+        cur.wait_stream(side)
+        for o in self.optimizers:
+            if o._runs is None:
+                raise RuntimeError("GraphedStep: run one eager iteration before capturing")
+            o.stage_hyper()  # allocates the device hyper buffer outside the capture
+        torch.cuda.synchronize()
+        self.graph = torch.cuda.CUDAGraph()
+        for o in self.optimizers:
+            o._capturing = True
+        try:
+            with torch.cuda.graph(self.graph):
+                self.outputs = fn()
+        finally:
+            for o in self.optimizers:
+                o._capturing = False
+        # the capture ran the optimizers' Python bookkeeping once without executing a step
+        for o in self.optimizers:
+            o.advance_steps(-1)
+
+    def __call__(self):
+        for o in self.optimizers:
+            o.stage_hyper()
+            o.advance_steps()
+        self.graph.replay()
+        return self.outputs

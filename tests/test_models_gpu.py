@@ -332,3 +332,52 @@ def test_da2_epochs_match_reference_adversarial_train_2(golden, tmp_path, monkey
     ours = {k: v.detach().cpu() - p0[k] for k, v in list(g.named_parameters()) + list(d.named_parameters())}
     print("DA2 param-update worst:", _noise_bounded(ours, upd[torch.float32], upd[torch.float64],
                                                     "DA2 update", floor=1e-2))
+
+
+@pytest.mark.parametrize("da", [False, True])
+def test_graphed_step_equals_eager(da):
+    """runtime.GraphedStep: N replays of the captured iteration (poly-LR changing every step,
+    Adam step counts advancing through the device hyper buffer) leave parameters, optimizer
+    state and BN buffers bit-identical to N eager iterations (seg step and DA iteration)."""
+    from rtsds_amd.runtime import GraphedStep
+    from rtsds_amd.utils import poly_lr_scheduler
+
+    def setup():
+        torch.manual_seed(3)
+        net = BiSeNet(19, "resnet18").to(DEV).train()
+        disc = TinyDomainDiscriminator(19).to(DEV).train()
+        opt = optim.Adam(net.parameters(), lr=1e-3)
+        dopt = optim.Adam(disc.parameters(), lr=1e-3, weight_decay=1e-4)
+        return net, disc, opt, dopt
+
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(2, 3, 64, 128, generator=g).to(DEV)
+    xt = torch.randn(2, 3, 64, 128, generator=g).to(DEV)
+    y = torch.randint(0, 20, (2, 64, 128), generator=g).to(DEV)
+    ce, bce = losses.CrossEntropyLoss(ignore_index=19), losses.BCEWithLogitsLoss()
+    states = []
+    with rtsds_amd.precision(torch.bfloat16):
+        for graphed in (False, True):
+            net, disc, opt, dopt = setup()
+
+            def core():
+                if da:
+                    out = rtrain.da_step(net, disc, opt, dopt, ce, bce, x, y, xt, 0.1, 100)
+                    return out[0], out[-1]
+                return rtrain.seg_step(net, ce, opt, x, y)
+
+            run = core
+            for i in range(5):
+                poly_lr_scheduler(opt, 1e-3, i, 1, 10, 0.9)
+                if graphed and i == 1:  # step 0 is GraphedStep's eager warm-up
+                    run = GraphedStep(core, [opt, dopt] if da else [opt], warmup=0)
+                if graphed and i == 0:
+                    core_out = core()
+                else:
+                    core_out = run()
+            torch.cuda.synchronize()
+            states.append({k: v.detach().float().cpu().clone() for k, v in
+                           list(net.state_dict().items()) + list(disc.state_dict().items())})
+            states[-1]["_loss"] = core_out[0].float().cpu().clone()
+    for k in states[0]:
+        assert torch.equal(states[0][k], states[1][k]), k
