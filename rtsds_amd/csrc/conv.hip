@@ -45,6 +45,14 @@ struct ConvArgs {
   const float* scale;
   const void* res;
   int gbuf;           // operand tensors < 2 GiB: buffer-resource DMA with 32-bit offsets allowed
+  // DGRAD stride-2: the parity phases of one conv in ONE launch (blockIdx.z = phase); each
+  // phase patches the phase-dependent fields below over the shared ones.
+  int nph;
+  struct Phase {
+    int hp, wp, offh, offw, r0h, r0w, tkw, M, K;
+    FastDiv f_tkw, f_hw, f_w;
+    long boff;  // element offset of the phase's repacked weights
+  } phs[4];
 };
 
 template <typename T> struct Mma;
@@ -174,7 +182,14 @@ template <typename T> RT_DEV typename VecT<T>::v16 vzero() {
 //       swizzled unpadded image above, the next K-tile's DMA in flight across the barrier
 //       (counted vmcnt, raw s_barrier); 0 = register-staged double buffer.
 template <typename T, int MODE, int BM, int BN, int BK, int WM, int WN, int ALA, int ALB, int GL>
-__global__ void __launch_bounds__(256) conv_gemm_kernel(const ConvArgs P) {
+__global__ void __launch_bounds__(256) conv_gemm_kernel(const ConvArgs P0) {
+  ConvArgs P = P0;
+  if (MODE == MODE_DGRAD && P0.nph > 1) {
+    const ConvArgs::Phase& q = P0.phs[blockIdx.z];
+    P.hp = q.hp; P.wp = q.wp; P.offh = q.offh; P.offw = q.offw; P.r0h = q.r0h; P.r0w = q.r0w;
+    P.tkw = q.tkw; P.M = q.M; P.K = q.K; P.f_tkw = q.f_tkw; P.f_hw = q.f_hw; P.f_w = q.f_w;
+    P.b = (const T*)P0.b + q.boff;
+  }
   typedef typename VecT<T>::v16 V16;
   constexpr int V = VecT<T>::N;
   constexpr bool RC = (MODE == MODE_WGRAD);
@@ -212,11 +227,12 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(const ConvArgs P) {
     const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
     const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
     const int t = RC ? wg % gxy : wg;
-    kz = RC ? wg / gxy : blockIdx.z;
+    kz = RC ? wg / gxy : (P.nph > 1 ? 0 : (int)blockIdx.z);
     mt = t % gx;
     nt = t / gx;
   }
   const int m0 = mt * BM, n0 = nt * BN;
+  if (MODE == MODE_DGRAD && P.nph > 1 && mt * BM >= P.M) return;  // phase with fewer M tiles
   const T* __restrict__ ga = (const T*)P.a;
   const T* __restrict__ gb = (const T*)P.b;
 
@@ -1043,6 +1059,27 @@ __global__ void repack_wt_kernel(const T* __restrict__ w, T* __restrict__ wt, in
   }
 }
 
+// All stride-2 DGRAD phases in one launch (blockIdx.y = phase): Wt_phase[ci][tap][co_p] at
+// element offset boff[phase] (32-bit indexing: a conv's weights are far below 2^31 elements).
+struct RepackPhases {
+  int tkh[4], tkw[4], r0h[4], r0w[4];
+  long boff[4];
+};
+template <typename T>
+__global__ void __launch_bounds__(256) repack_phases_kernel(const T* __restrict__ w, T* __restrict__ wt, int co_n, int co_p, int kh,
+                                                            int kw, int ci_n, int rstep, RepackPhases rp) {
+  const int ph = blockIdx.y;
+  const int tkw = rp.tkw[ph], taps = rp.tkh[ph] * tkw;
+  const int total = co_p * taps * ci_n;
+  T* out = wt + rp.boff[ph];
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int co = i % co_p, rest = i / co_p;
+    const int tap = rest % taps, ci = rest / taps;
+    const int r = rp.r0h[ph] + (tap / tkw) * rstep, sc = rp.r0w[ph] + (tap % tkw) * rstep;
+    out[i] = co < co_n ? w[((co * kh + r) * kw + sc) * ci_n + ci] : (T)0.0f;
+  }
+}
+
 // dst[r][j] = j < c ? src[r][j] : 0   (channel padding of an NHWC tensor or of [co][tap][ci] weights)
 // One thread per 16-byte output vector: dst[r][j0..j0+V) = src[r][j] (j < c) or 0.
 template <typename T>
@@ -1211,7 +1248,7 @@ static void pad_any(int dtype, const void* src, void* dst, long rows, int c, int
 
 template <typename T, int MODE, int BM, int BN, int BK, int WM, int WN, int ALA, int ALB, int GL = 0>
 static void launch(const ConvArgs& p, int splits, hipStream_t st) {
-  dim3 grid(rt_cdiv(p.M, BM), rt_cdiv(p.N, BN), splits);
+  dim3 grid(rt_cdiv(p.M, BM), rt_cdiv(p.N, BN), MODE == MODE_DGRAD && p.nph > 1 ? p.nph : splits);
   hipLaunchKernelGGL((conv_gemm_kernel<T, MODE, BM, BN, BK, WM, WN, ALA, ALB, GL>), grid, dim3(256), 0, st, p);
 }
 
@@ -1625,29 +1662,57 @@ extern "C" int rtsds_conv2d_dgrad(const rtsds_conv_desc* d0, const void* dy, con
   const int k_real = d.k;
   d.k = kp;
   if (d.sh == 2 && d.sw == 2) {
-    // stride-2: four parity phases, each a dense GEMM over only the taps that reach it
+    // stride-2: the four parity phases, each a dense GEMM over only the taps that reach it,
+    // repacked by one launch and computed by one launch (blockIdx.z = phase)
+    ConvArgs p = make_args(&d);
+    p.a = dy; p.b = wt; p.bias = nullptr; p.out = dx; p.act = 0;
+    p.accum = accumulate ? 1 : 0;
+    p.psh = 2;
+    p.N = d.c;
+    RepackPhases rp = {};
+    int nph = 0, rstep = 1, max_m = 0, max_w = 0;
+    long boff = 0;
     for (int a = 0; a < 2; ++a)
       for (int b = 0; b < 2; ++b) {
         int offh, hp, r0h, rsh, tkh, offw, wp, r0w, rsw, tkw;
         phase_taps(a, d.ph, d.dh, d.kh, d.h, offh, hp, r0h, rsh, tkh);
         phase_taps(b, d.pw, d.dw, d.kw, d.w, offw, wp, r0w, rsw, tkw);
         if (hp == 0 || wp == 0) continue;
-        repack_launch(d.dtype, w, wt, k_real, kp, d.kh, d.kw, d.c, tkh, tkw, r0h, r0w, rsh, st);
-        ConvArgs p = make_args(&d);
-        p.a = dy; p.b = wt; p.bias = nullptr; p.out = dx; p.act = 0;
-        p.accum = accumulate ? 1 : 0;
-        p.hp = hp; p.wp = wp; p.psh = 2; p.offh = offh; p.offw = offw;
-        p.r0h = r0h; p.r0w = r0w; p.rstep = rsh;
-        p.tkw = tkw > 0 ? tkw : 1;
-        p.f_tkw = fastdiv_make(p.tkw);
-        p.f_hw = fastdiv_make(hp * wp);
-        p.f_w = fastdiv_make(wp);
-        p.M = d.n * hp * wp;
-        p.N = d.c;
-        p.K = tkh * tkw * kp;
-        if (d.dtype == RTSDS_BF16) dispatch_align<bf16, MODE_DGRAD>(p, kp, st);
-        else dispatch_align<float, MODE_DGRAD>(p, kp, st);
+        rstep = rsh;
+        ConvArgs::Phase& q = p.phs[nph];
+        q.hp = hp; q.wp = wp; q.offh = offh; q.offw = offw; q.r0h = r0h; q.r0w = r0w;
+        q.tkw = tkw > 0 ? tkw : 1;
+        q.f_tkw = fastdiv_make(q.tkw);
+        q.f_hw = fastdiv_make(hp * wp);
+        q.f_w = fastdiv_make(wp);
+        q.M = d.n * hp * wp;
+        q.K = tkh * tkw * kp;
+        q.boff = boff;
+        rp.tkh[nph] = tkh; rp.tkw[nph] = tkw; rp.r0h[nph] = r0h; rp.r0w[nph] = r0w; rp.boff[nph] = boff;
+        boff += (long)q.K * d.c;
+        max_m = std::max(max_m, q.M);
+        max_w = std::max(max_w, q.K * d.c);
+        ++nph;
       }
+    if (nph == 0) return RTSDS_OK;
+    if (max_w > 0) {
+      const dim3 g(std::min(4096, (max_w + 255) / 256), nph);
+      if (d.dtype == RTSDS_BF16)
+        hipLaunchKernelGGL(repack_phases_kernel<bf16>, g, dim3(256), 0, st, (const bf16*)w, (bf16*)wt, k_real, kp, d.kh, d.kw,
+                           d.c, rstep, rp);
+      else
+        hipLaunchKernelGGL(repack_phases_kernel<float>, g, dim3(256), 0, st, (const float*)w, (float*)wt, k_real, kp, d.kh, d.kw,
+                           d.c, rstep, rp);
+    }
+    // shared fields: the first phase's (tile choice and alignment class depend only on M, N, kp)
+    p.nph = nph;
+    p.hp = p.phs[0].hp; p.wp = p.phs[0].wp; p.offh = p.phs[0].offh; p.offw = p.phs[0].offw;
+    p.r0h = p.phs[0].r0h; p.r0w = p.phs[0].r0w; p.rstep = rstep; p.tkw = p.phs[0].tkw;
+    p.f_tkw = p.phs[0].f_tkw; p.f_hw = p.phs[0].f_hw; p.f_w = p.phs[0].f_w;
+    p.M = max_m;
+    p.K = p.phs[0].K;
+    if (d.dtype == RTSDS_BF16) dispatch_align<bf16, MODE_DGRAD>(p, kp, st);
+    else dispatch_align<float, MODE_DGRAD>(p, kp, st);
   } else {
     repack_launch(d.dtype, w, wt, k_real, kp, d.kh, d.kw, d.c, d.kh, d.kw, 0, 0, 1, st);
     ConvArgs p = make_args(&d);
