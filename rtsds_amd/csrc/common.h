@@ -70,13 +70,14 @@ RT_DEV void bil_src(int o, float scale, int in, int& i0, int& i1, float& l0, flo
   l0 = 1.f - l1;
 }
 
-// Blend of the 4 taps (p00 = (h0,w0), p01 = (h0,w1), p10 = (h1,w0), p11 = (h1,w1)): vertical
-// first, explicit fma order -- the fused upsample+CE computes the identical expression from
-// per-row vertical blends, so both paths produce the same logits bit for bit.
+// Blend of the 4 taps (p00 = (h0,w0), p01 = (h0,w1), p10 = (h1,w0), p11 = (h1,w1)): width
+// inner, height outer (the association of ATen's separable upsample_bilinear2d), explicit fma
+// order -- the fused upsample+CE computes the identical expression from per-column
+// horizontal blends, so both paths produce the same logits bit for bit.
 RT_DEV float bil_mix(float p00, float p01, float p10, float p11, float lh0, float lh1, float lw0, float lw1) {
-  const float v0 = fmaf(lh1, p10, lh0 * p00);
-  const float v1 = fmaf(lh1, p11, lh0 * p01);
-  return fmaf(lw1, v1, lw0 * v0);
+  const float t0 = fmaf(lw1, p01, lw0 * p00);
+  const float t1 = fmaf(lw1, p11, lw0 * p10);
+  return fmaf(lh1, t1, lh0 * t0);
 }
 
 #define RT_CHECK_LAUNCH()                                      \

@@ -29,12 +29,15 @@
 #include <cmath>
 
 static const int kUpceCMax = 32;
+#ifndef UPCE_ROWS
+#define UPCE_ROWS 32.f  // full-res rows per tile (one wave walks them)
+#endif
 static const int kUpceMaxHeads = 4;
 
 struct UpceGeo {
   int n, hl, wl, c, H, W;
   float sh, sw;
-  int th, tw, ntr, ntc, wmax, nblocks;
+  int th, tw, ntr, ntc, wmax, hmax, nblocks;
 };
 
 struct UpceArgs {
@@ -79,12 +82,23 @@ RT_DEV float upce_block_sum(float v, float* red) {
 
 // CP: channel count padded to a multiple of 4 (compile time, so every per-class loop is
 // fully unrolled without guards); padding classes hold -1e30 logits (softmax weight 0).
+//
+// One wave per (tile, head): lane l owns the full-res column x = x_lo + xb + l of the tile
+// (xb = 0, then 64 for the rare tiles wider than 64 columns) and walks down the tile's rows.
+// Per row the logits are z = l0*H0 + l1*H1, H0 / H1 the horizontal blends of the two
+// low-res rows at this column (width inner, as ATen's separable upsample_bilinear2d; the
+// same expression as bil_mix, so rtsds_bilinear_fwd gives identical logits), recomputed only
+// when the low-res row pair advances.  g = softmax - onehot is folded vertically in registers
+// into the two low-res rows the pixel feeds (Rlo, Rhi); when the pair advances, the finished
+// low-res row goes through the x-fold once (wave-private LDS row x the tile's weight table),
+// i.e. once per scale-factor rows instead of once per row, and no workgroup barrier runs
+// inside the row loop.
 template <typename T, int CP>
-__global__ void __launch_bounds__(256) upce_fwd_kernel(UpceArgs a) {
+__global__ void __launch_bounds__(256, 3) upce_fwd_kernel(UpceArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  __shared__ float red[4];
   const UpceGeo& q = a.g;
-  const int TH = q.th, TW = q.tw, C = q.c, TW1 = TW + 1, tid = threadIdx.x;
+  const int TH = q.th, TW = q.tw, C = q.c, TW1 = TW + 1, tid = threadIdx.x, nthr = blockDim.x;
+  const int lane = tid & 63, h = tid >> 6;  // wave = head
   const int tiles = q.ntr * q.ntc;
   const int img = blockIdx.x / tiles, tt = blockIdx.x - img * tiles;
   const int tr = tt / q.ntc, tc = tt - tr * q.ntc;
@@ -96,21 +110,30 @@ __global__ void __launch_bounds__(256) upce_fwd_kernel(UpceArgs a) {
   const int Wt = min(x_hi - x_lo, q.wmax);
   const int tile_el = (TH + 1) * TW1 * C;  // gradient-partial layout (compact classes)
   const int rowp = TW1 * CP, ltile = (TH + 1) * rowp;
+  const int npair = TW1 * C;
 
-  // LDS (class stride CP): lt[TH+1][TW1] | vb[4][TW1] | gb[4][wmax] | wcol[TW1][wmax] |
-  //                        xj0 | xj1 | xm0 | xm1 | xs | xe
-  float* lt = smem;
-  float* vb = lt + ltile;
-  float* gb = vb + 4 * rowp;
-  float* wcol = gb + 4 * q.wmax * CP;
+  // LDS: wcol[TW1][wmax] | xj0 | xj1 | xm0 | xm1 [wmax] | xs | xe [TW1] |
+  //      per head: lt[TH+1][TW1][CP] (low-res tile) | xrow[64][CP] (x-fold staging)
+  float* wcol = smem;
   int* xj0 = (int*)(wcol + TW1 * q.wmax);
   int* xj1 = xj0 + q.wmax;
   float* xm0 = (float*)(xj1 + q.wmax);
   float* xm1 = xm0 + q.wmax;
   int* xs = (int*)(xm1 + q.wmax);
   int* xe = xs + TW1;
+  float* hbase = (float*)(xe + TW1);
+  const int per_head = ltile + 64 * CP;
+  // labels of the tile's pixels as bytes (class, 254 = ignore_index, 253 = out of range),
+  // staged once for all heads: the row loop then never waits on a global load
+  unsigned char* lab = (unsigned char*)(hbase + a.nheads * per_head);
+  const int Ht = min(y_hi - y_lo, q.hmax);
+  for (int e = tid; e < Ht * Wt; e += nthr) {
+    const int yy = e / Wt, xx = e - yy * Wt;
+    const long t = a.tgt[((long)img * q.H + y_lo + yy) * q.W + x_lo + xx];
+    lab[e] = t == a.ignore ? 254 : ((t >= 0 && t < C) ? (unsigned char)t : 253);
+  }
 
-  for (int xx = tid; xx < Wt; xx += 256) {
+  for (int xx = tid; xx < Wt; xx += nthr) {
     int j0, j1;
     float m0, m1;
     bil_src(x_lo + xx, q.sw, q.wl, j0, j1, m0, m1);
@@ -121,189 +144,190 @@ __global__ void __launch_bounds__(256) upce_fwd_kernel(UpceArgs a) {
   }
   __syncthreads();
   // x-adjoint weights: wcol[jl][xx] = weight of full-res column xx on low-res column jl
-  for (int e = tid; e < TW1 * Wt; e += 256) {
+  for (int e = tid; e < TW1 * Wt; e += nthr) {
     const int jl = e / Wt, xx = e - jl * Wt;
     wcol[jl * q.wmax + xx] = (xj0[xx] == jl ? xm0[xx] : 0.f) + (xj1[xx] == jl ? xm1[xx] : 0.f);
   }
   // contiguous full-res column range feeding low-res column jl (taps are monotone in x)
-  for (int jl = tid; jl < TW1; jl += 256) {
+  for (int jl = tid; jl < TW1; jl += nthr) {
     int lo = Wt, hi = -1;
     for (int xx = 0; xx < Wt; ++xx)
       if (xj0[xx] == jl || xj1[xx] == jl) { lo = min(lo, xx); hi = xx; }
     xs[jl] = lo;
     xe[jl] = hi;
   }
-
-  float cnt = 0.f;
-  unsigned long long corr = 0;
-  const int ry = tid >> 6, rx = tid & 63;
-  const int npair = TW1 * C;  // <= 512: each thread owns pairs tid and tid + 256
-  int pj[2], pc[2];
-#pragma unroll
-  for (int q2 = 0; q2 < 2; ++q2) {
-    const int p = tid + q2 * 256;
-    pj[q2] = p / C;
-    pc[q2] = p - pj[q2] * C;
-  }
-  // labels of this thread's pixel(s) in a 4-row chunk (column groups 0 / 64; Wt <= 128)
-  auto tload = [&](int yb, int xb) -> long {
-    const int y = yb + ry, xx = xb + rx;
-    return (y < y_hi && xx < Wt) ? a.tgt[((long)img * q.H + y) * q.W + x_lo + xx] : -1;
-  };
-  for (int h = 0; h < a.nheads; ++h) {
-    const T* X = (const T*)a.x[h] + (long)img * q.hl * q.wl * C;
-    __syncthreads();
-    for (int e = tid; e < ltile; e += 256) {
+  for (int hh = 0; hh < a.nheads; ++hh) {
+    const T* X = (const T*)a.x[hh] + (long)img * q.hl * q.wl * C;
+    float* lt = hbase + hh * per_head;
+    for (int e = tid; e < ltile; e += nthr) {
       const int cc = e % CP, cell = e / CP;
       const int il = cell / TW1, jl = cell - il * TW1;
       float v = cc < C ? 0.f : -1e30f;
       if (cc < C && il < rows_l && jl < cols_l) v = to_f(X[((long)(r0 + il) * q.wl + (c0 + jl)) * C + cc]);
       lt[e] = v;
     }
-    __syncthreads();
-    float lsum = 0.f;
-    // y-fold accumulators of the owned (jl, c) pairs for low-res rows cur and cur + 1;
-    // rows are finalised (written to gpart) as the full-res rows advance past them.
-    float Aa[2] = {0.f, 0.f}, Ab[2] = {0.f, 0.f};
-    int cur = 0;
-    float* gdst = a.want_grad ? a.gpart[h] + (long)blockIdx.x * tile_el : nullptr;
-    long tn0 = tload(y_lo, 0), tn1 = Wt > 64 ? tload(y_lo, 64) : -1;
-    for (int yb = y_lo; yb < y_hi; yb += 4) {
-      const long tc0 = tn0, tc1 = tn1;
-      if (yb + 4 < y_hi) {  // prefetch the next chunk's labels
-        tn0 = tload(yb + 4, 0);
-        if (Wt > 64) tn1 = tload(yb + 4, 64);
+  }
+  __syncthreads();
+  if (h >= a.nheads) return;
+
+  const float* lt = hbase + h * per_head;
+  float* xrow = hbase + h * per_head + ltile;
+  float* gdst = a.want_grad ? a.gpart[h] + (long)blockIdx.x * tile_el : nullptr;
+  const float kL2E = 1.4426950408889634f, kLN2 = 0.6931471805599453f;
+  float lsum = 0.f, cnt = 0.f;
+  unsigned long long corr = 0;
+
+  for (int xb = 0; xb < Wt; xb += 64) {
+    const int xx = xb + lane;
+    const bool xv = xx < Wt;
+    const int xc = xv ? xx : Wt - 1;
+    const int j0 = xj0[xc], j1 = xj1[xc];
+    const float m0 = xm0[xc], m1 = xm1[xc];
+    const int xend = min(xb + 63, Wt - 1);
+    const bool add = xb > 0;  // later column chunks add into the rows the first one wrote
+    float H0[CP], H1[CP], Rlo[CP], Rhi[CP];
+#pragma unroll
+    for (int k = 0; k < CP; ++k) { Rlo[k] = 0.f; Rhi[k] = 0.f; }
+    int pj[3], pc[3], plo[3], phi[3];  // this lane's x-fold pairs (low-res column, class)
+#pragma unroll
+    for (int u = 0; u < 3; ++u) {
+      const int p = min(lane + 64 * u, npair - 1);
+      pj[u] = p / C;
+      pc[u] = p - pj[u] * C;
+      plo[u] = max(xs[pj[u]], xb);
+      phi[u] = min(xe[pj[u]], xend);
+    }
+    auto hblend = [&](int li, float* H) {
+      const float* L = lt + li * rowp;
+#pragma unroll
+      for (int k = 0; k < CP; ++k) H[k] = fmaf(m1, L[j1 * CP + k], m0 * L[j0 * CP + k]);
+    };
+    // x-fold of finished low-res row il (all lanes of the wave take part)
+    auto emit = [&](int il, const float* R) {
+      if (xv) {
+#pragma unroll
+        for (int k = 0; k < CP; ++k) xrow[lane * CP + k] = R[k];
       }
-      const int y = yb + ry;
-      // vertical interpolation of this wave's full-res row on the tile's low-res columns
-      // (vrow[jl][c]); each pixel then only blends its two columns:
-      //   z = m1 * vrow[j1] + m0 * vrow[j0],  vrow[j] = l1 * L[i1][j] + l0 * L[i0][j]
-      // (the same fma order as rtsds_bilinear_fwd, so both give identical logits).
-      float* vrow = vb + ry * rowp;
-      if (y < y_hi) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // LDS only: the row's global stores stay in flight
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int u = 0; u < 3; ++u) {  // pairs p = lane + 64u (npair <= 3 * 64: see upce_plan)
+        const int p = lane + 64 * u;
+        if (p >= npair) break;
+        const float* wr = wcol + pj[u] * q.wmax;
+        const float* xr = xrow + pc[u] - xb * CP;
+        float s = 0.f;
+        for (int x2 = plo[u]; x2 <= phi[u]; ++x2) s = fmaf(wr[x2], xr[x2 * CP], s);
+        float* o = gdst + il * npair + p;
+        *o = add ? *o + s : s;
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // LDS only: the row's global stores stay in flight
+      __builtin_amdgcn_wave_barrier();
+    };
+    // rows grouped by their top low-res row gi = r0 + li: H0 / H1 are fixed over a group, and
+    // low-res row li is complete when its group ends (earlier rows fed it through Rhi)
+    int li = 0;
+    for (int ya = y_lo; ya < y_lo + Ht; ++li) {
+      const int gi = r0 + li;
+      const int yb = min(upce_first_ge(gi + 1, q.sh, q.hl, q.H), y_lo + Ht);
+      const bool same = gi + 1 >= q.hl;  // bottom clamp: i1 == i0, both taps on row li
+      hblend(li, H0);
+      hblend(same ? li : li + 1, H1);
+      const float* L0 = lt + li * rowp;
+      const float* L1 = lt + (same ? li : li + 1) * rowp;
+      int tb_next = xv ? lab[(ya - y_lo) * Wt + xx] : 254;
+      for (int y = ya; y < yb; ++y) {
+        const int tb = tb_next;
+        if (xv && y + 1 < yb) tb_next = lab[(y + 1 - y_lo) * Wt + xx];
         int i0, i1;
         float l0, l1;
         bil_src(y, q.sh, q.hl, i0, i1, l0, l1);
-        const float* L0 = lt + (i0 - r0) * rowp;
-        const float* L1 = lt + (i1 - r0) * rowp;
-        for (int e = rx; e < rowp; e += 64) vrow[e] = fmaf(l1, L1[e], l0 * L0[e]);
-      }
-      __syncthreads();
-      for (int xb = 0; xb < Wt; xb += 64) {
-        const int xx = xb + rx;
-        if (y >= y_hi || xx >= Wt) continue;
-        const long t = xb == 0 ? tc0 : tc1;
-        const float m0 = xm0[xx], m1 = xm1[xx];
-        const float* v0 = vrow + xj0[xx] * CP;
-        const float* v1 = vrow + xj1[xx] * CP;
+        if (!xv) continue;
         float z[CP];
-        float mx = -INFINITY;
 #pragma unroll
-        for (int k = 0; k < CP; ++k) {
-          z[k] = fmaf(m1, v1[k], m0 * v0[k]);
-          mx = fmaxf(mx, z[k]);
-        }
-        const bool in_range = t >= 0 && t < C;
-        const float zt = in_range ? fmaf(m1, v1[t], m0 * v0[t]) : NAN;
-        if (h == 0 && a.correct) {  // first maximum wins (torch argmax)
-          float best = z[0];
-          int bi = 0;
+        for (int k = 0; k < CP; ++k) z[k] = fmaf(l1, H1[k], l0 * H0[k]);
+        // max as a 4-way interleaved tree (dependent-chain depth CP/4 + 2 instead of CP)
+        float mq[4] = {z[0], z[1], z[2], z[3]};
 #pragma unroll
-          for (int k = 1; k < CP; ++k)
-            if (z[k] > best || (z[k] != z[k] && best == best)) { best = z[k]; bi = k; }
-          corr += (t == bi) ? 1ull : 0ull;
-        }
-        const bool valid = t != a.ignore;
+        for (int k = 4; k < CP; ++k) mq[k & 3] = fmaxf(mq[k & 3], z[k]);
+        const float mx = fmaxf(fmaxf(mq[0], mq[1]), fmaxf(mq[2], mq[3]));
+        const bool in_range = tb < 253;
+        const int t = in_range ? tb : (tb == 254 ? a.ignore : -1);
+        // z[t] recomputed from the LDS tile with the same expression (no register indexing)
+        const int tq = in_range ? tb : 0;
+        const float h0 = fmaf(m1, L0[j1 * CP + tq], m0 * L0[j0 * CP + tq]);
+        const float h1 = fmaf(m1, L1[j1 * CP + tq], m0 * L1[j0 * CP + tq]);
+        const float zt = in_range ? fmaf(l1, h1, l0 * h0) : NAN;
+        const bool valid = tb != 254;
         // softmax with the hardware exp2 / log2 / rcp (v_exp_f32, v_log_f32, v_rcp_f32)
-        const float kL2E = 1.4426950408889634f, kLN2 = 0.6931471805599453f;
         const float mxs = mx * kL2E;
-        float se = 0.f;
+        int bi = 0;  // argmax before z is overwritten
+        if (h == 0 && a.correct) {
 #pragma unroll
-        for (int k = 0; k < CP; ++k) {
+          for (int k = CP - 1; k >= 0; --k) bi = z[k] == mx ? k : bi;
+        }
+        float sq[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int k = 0; k < CP; ++k) {  // z -> exp(z - max) in place
           z[k] = __builtin_amdgcn_exp2f(fmaf(z[k], kL2E, -mxs));
-          se += z[k];
+          sq[k & 3] += z[k];
         }
-        if (valid) {
-          lsum += fmaf(__builtin_amdgcn_logf(se), kLN2, mx) - zt;
-          if (h == 0) cnt += 1.f;
+        const float se = (sq[0] + sq[1]) + (sq[2] + sq[3]);
+        if (h == 0 && a.correct) {  // first maximum wins (torch argmax; a NaN logit wins)
+          if (__builtin_amdgcn_ballot_w64(se != se)) {  // wave-uniform: only with NaN logits
+            float best = fmaf(l1, H1[0], l0 * H0[0]);
+            int bn = 0;
+            for (int k = 1; k < CP; ++k) {
+              const float zk = fmaf(l1, H1[k], l0 * H0[k]);
+              if (zk > best || (zk != zk && best == best)) { best = zk; bn = k; }
+            }
+            bi = se != se ? bn : bi;
+          }
+          corr += (t == bi) ? 1ull : 0ull;  // t = ignore_index (or -1): never a class index < C
         }
+        lsum += valid ? fmaf(__builtin_amdgcn_logf(se), kLN2, mx) - zt : 0.f;
+        if (h == 0) cnt += valid ? 1.f : 0.f;
         if (a.want_grad) {
-          float* gp = gb + (ry * q.wmax + xx) * CP;
           const float is = valid ? __builtin_amdgcn_rcpf(se) : 0.f;
+          const int th1 = (valid && in_range) ? tb : -1;
 #pragma unroll
-          for (int k = 0; k < CP; ++k) gp[k] = z[k] * is;
-          if (valid && in_range) gp[t] -= 1.f;
-        }
-      }
-      if (!a.want_grad) continue;
-      __syncthreads();
-      // adjoint, x-fold: R[r][jl][c] = sum_x wcol[jl][x] g[r][x][c] for the 4 chunk rows at once
-      float R[2][4];
+          for (int k = 0; k < CP; ++k) z[k] = fmaf(z[k], is, th1 == k ? -1.f : 0.f);  // g in place
+          if (same) {  // group-uniform
 #pragma unroll
-      for (int q2 = 0; q2 < 2; ++q2) {
-        R[q2][0] = R[q2][1] = R[q2][2] = R[q2][3] = 0.f;
-        const int p = tid + q2 * 256;
-        if (p < npair) {
-          const int jl = pj[q2];
-          const float* wr = wcol + jl * q.wmax;
-          const float* gq = gb + pc[q2];
-          const int rs = q.wmax * CP;
-          const int xhi = xe[jl];
-          for (int xx = xs[jl]; xx <= xhi; ++xx) {
-            const float w = wr[xx];
-            const float* g0 = gq + xx * CP;
-            R[q2][0] = fmaf(w, g0[0], R[q2][0]);
-            R[q2][1] = fmaf(w, g0[rs], R[q2][1]);
-            R[q2][2] = fmaf(w, g0[2 * rs], R[q2][2]);
-            R[q2][3] = fmaf(w, g0[3 * rs], R[q2][3]);
+            for (int k = 0; k < CP; ++k) Rlo[k] = fmaf(l1, z[k], fmaf(l0, z[k], Rlo[k]));
+          } else {
+#pragma unroll
+            for (int k = 0; k < CP; ++k) {
+              Rlo[k] = fmaf(l0, z[k], Rlo[k]);
+              Rhi[k] = fmaf(l1, z[k], Rhi[k]);
+            }
           }
         }
       }
-      // y-fold into the running row accumulators
+      if (a.want_grad) {  // row li is complete
+        emit(li, Rlo);
 #pragma unroll
-      for (int r2 = 0; r2 < 4; ++r2) {
-        const int y2 = yb + r2;
-        if (y2 >= y_hi) break;
-        int k0, k1;
-        float h0, h1;
-        bil_src(y2, q.sh, q.hl, k0, k1, h0, h1);
-        k0 -= r0;
-        k1 -= r0;
-        while (k0 > cur) {
-#pragma unroll
-          for (int q2 = 0; q2 < 2; ++q2) {
-            const int p = tid + q2 * 256;
-            if (p < npair) gdst[cur * npair + p] = Aa[q2];
-            Aa[q2] = Ab[q2];
-            Ab[q2] = 0.f;
-          }
-          ++cur;
-        }
-#pragma unroll
-        for (int q2 = 0; q2 < 2; ++q2) {
-          Aa[q2] = fmaf(h0, R[q2][r2], Aa[q2]);
-          if (k1 == k0) Aa[q2] = fmaf(h1, R[q2][r2], Aa[q2]);
-          else Ab[q2] = fmaf(h1, R[q2][r2], Ab[q2]);
-        }
+        for (int k = 0; k < CP; ++k) { Rlo[k] = Rhi[k]; Rhi[k] = 0.f; }
       }
-      __syncthreads();
+      ya = yb;
     }
-    if (a.want_grad) {  // flush rows cur, cur + 1; rows never reached are zero
-#pragma unroll
-      for (int q2 = 0; q2 < 2; ++q2) {
-        const int p = tid + q2 * 256;
-        if (p >= npair) continue;
-        for (int il = cur; il <= TH; ++il) gdst[il * npair + p] = il == cur ? Aa[q2] : (il == cur + 1 ? Ab[q2] : 0.f);
-      }
+    const int cur = li;  // first low-res row not yet emitted (Rlo holds its contributions)
+    if (a.want_grad) {  // flush row cur; rows never reached are zero
+      if (cur <= TH) emit(cur, Rlo);
+      if (!add)
+        for (int il = cur + 1; il <= TH; ++il)
+          for (int p = lane; p < npair; p += 64) gdst[il * npair + p] = 0.f;
     }
-    const float s = upce_block_sum(lsum, red);
-    if (tid == 0) a.lpart[(long)h * q.nblocks + blockIdx.x] = s;
   }
-  const float cs = upce_block_sum(cnt, red);
-  if (tid == 0) a.cpart[blockIdx.x] = cs;
-  if (a.correct) {
-    for (int o = 32; o > 0; o >>= 1) corr += __shfl_xor(corr, o, 64);
-    if ((tid & 63) == 0 && corr) atomicAdd(a.correct, corr);
+  lsum = wave_sum(lsum);
+  if (lane == 0) a.lpart[(long)h * q.nblocks + blockIdx.x] = lsum;
+  if (h == 0) {
+    cnt = wave_sum(cnt);
+    if (lane == 0) a.cpart[blockIdx.x] = cnt;
+    if (a.correct) {
+      for (int o = 32; o > 0; o >>= 1) corr += __shfl_xor(corr, o, 64);
+      if (lane == 0 && corr) atomicAdd(a.correct, corr);
+    }
   }
 }
 
@@ -388,23 +412,27 @@ static bool upce_plan(int n, int hl, int wl, int c, int H, int W, float sh, floa
   const float fy = 1.f / sh, fx = 1.f / sw;
   g.n = n; g.hl = hl; g.wl = wl; g.c = c; g.H = H; g.W = W; g.sh = sh; g.sw = sw;
   g.tw = std::max(1, std::min(32, (int)(64.f / std::ceil(fx))));
-  g.th = std::max(1, std::min(32, (int)(64.f / std::ceil(fy))));
+  // 32 full-res rows per tile: one wave per (tile, head) walks them, so shorter tiles mean more
+  // waves in flight (the row loop is latency-bound at ~3 waves per SIMD)
+  g.th = std::max(1, std::min(32, (int)(UPCE_ROWS / std::ceil(fy))));
   g.ntr = (hl + g.th - 1) / g.th;
   g.ntc = (wl + g.tw - 1) / g.tw;
   g.wmax = (int)std::ceil((g.tw + 1) * fx) + 4;
+  g.hmax = (int)std::ceil((g.th + 1) * fy) + 4;
   // kernel limits: two 64-column groups per row, <= 512 owned (column, class) pairs
-  while (g.tw > 1 && (g.wmax > 128 || (g.tw + 1) * c > 512)) {
+  while (g.tw > 1 && (g.wmax > 128 || (g.tw + 1) * c > 192)) {
     --g.tw;
     g.wmax = (int)std::ceil((g.tw + 1) * fx) + 4;
   }
-  if (g.wmax > 128 || (g.tw + 1) * c > 512) return false;
+  if (g.wmax > 128 || (g.tw + 1) * c > 192) return false;  // <= 3 x-fold pairs per lane
   g.nblocks = n * g.ntr * g.ntc;
   return (long)g.nblocks * g.ntr < (1L << 31);
 }
 static int upce_cp(int c) { return (c + 3) / 4 * 4; }
-static size_t upce_lds(const UpceGeo& g) {
+static size_t upce_lds(const UpceGeo& g, int nheads) {
   const size_t cp = upce_cp(g.c), tile_el = (size_t)(g.th + 1) * (g.tw + 1) * cp;
-  return (tile_el + 4 * (size_t)(g.tw + 1) * cp + 4 * (size_t)g.wmax * cp + (size_t)(g.tw + 1) * g.wmax + 4 * (size_t)g.wmax + 2 * (size_t)(g.tw + 1)) * 4;
+  return ((size_t)(g.tw + 1) * g.wmax + 4 * (size_t)g.wmax + 2 * (size_t)(g.tw + 1) + nheads * (tile_el + 64 * cp)) * 4 +
+         (size_t)g.hmax * g.wmax;
 }
 static size_t upce_tile_el(const UpceGeo& g) { return (size_t)(g.th + 1) * (g.tw + 1) * g.c; }
 // ws: stat[64] (count, per-head loss sums; offset 0, see the header) | [heads][nblocks][tile_el]
@@ -417,7 +445,7 @@ static size_t upce_ws_floats(const UpceGeo& g, int heads) {
 extern "C" size_t rtsds_upce_workspace(int nheads, int n, int hl, int wl, int c, int H, int W, float scale_h, float scale_w) {
   UpceGeo g;
   if (nheads <= 0 || nheads > kUpceMaxHeads || !upce_plan(n, hl, wl, c, H, W, scale_h, scale_w, g)) return 0;
-  if (upce_lds(g) > 64 * 1024) return 0;
+  if (upce_lds(g, nheads) > 64 * 1024) return 0;
   return upce_ws_floats(g, nheads) * 4 + 256;
 }
 
@@ -446,13 +474,14 @@ extern "C" int rtsds_upce_fwd(int nheads, const void* const* logits, const int64
   a.ignore = ignore_index;
   a.want_grad = want_grad;
   hipStream_t st = (hipStream_t)stream;
-  const size_t lds = upce_lds(g);
+  const size_t lds = upce_lds(g, nheads);
+  const dim3 blk(64 * nheads);
   if (dtype != RTSDS_BF16 && dtype != RTSDS_F32) return RTSDS_ERR_UNSUPPORTED;
   switch (upce_cp(c)) {
 #define UPCE_CASE(CPV)                                                                                      \
   case CPV:                                                                                                 \
-    if (dtype == RTSDS_BF16) hipLaunchKernelGGL((upce_fwd_kernel<bf16, CPV>), dim3(g.nblocks), dim3(256), lds, st, a); \
-    else hipLaunchKernelGGL((upce_fwd_kernel<float, CPV>), dim3(g.nblocks), dim3(256), lds, st, a);          \
+    if (dtype == RTSDS_BF16) hipLaunchKernelGGL((upce_fwd_kernel<bf16, CPV>), dim3(g.nblocks), blk, lds, st, a); \
+    else hipLaunchKernelGGL((upce_fwd_kernel<float, CPV>), dim3(g.nblocks), blk, lds, st, a);          \
     break;
     UPCE_CASE(4) UPCE_CASE(8) UPCE_CASE(12) UPCE_CASE(16) UPCE_CASE(20) UPCE_CASE(24) UPCE_CASE(28) UPCE_CASE(32)
 #undef UPCE_CASE
