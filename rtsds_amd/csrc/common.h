@@ -80,6 +80,23 @@ RT_DEV float bil_mix(float p00, float p01, float p10, float p11, float lh0, floa
   return fmaf(lh1, t1, lh0 * t0);
 }
 
+// Buffer-resource LDS-DMA (buffer_load_dwordx4 ... offen lds): 32-bit byte offsets, and an
+// offset past num_records zero-fills the LDS destination.  The host compilation pass of the
+// kernel templates only needs the signatures.
+#if defined(__HIP_DEVICE_COMPILE__)
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+RT_DEV rsrc_t make_rsrc(const void* p, int bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)p, 0, bytes, 0x00020000);
+}
+RT_DEV void buf_lds16(rsrc_t r, void* lds, int voff, int soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, voff, soff, 0, 0);
+}
+#else
+struct rsrc_t { int w[4]; };
+RT_DEV rsrc_t make_rsrc(const void*, int) { return rsrc_t{}; }
+RT_DEV void buf_lds16(rsrc_t, void*, int, int) {}
+#endif
+
 #define RT_CHECK_LAUNCH()                                      \
   do {                                                          \
     if (hipPeekAtLastError() != hipSuccess) return RTSDS_ERR_LAUNCH; \

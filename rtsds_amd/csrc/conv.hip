@@ -140,23 +140,6 @@ RT_DEV bf16x8 rc_gl_frag(s16x4 t0, s16x4 t1) {
   s16x8 r = {t0[0], t0[1], t0[2], t0[3], t1[0], t1[1], t1[2], t1[3]};
   return __builtin_bit_cast(bf16x8, r);
 }
-// Buffer-resource LDS-DMA (buffer_load_dwordx4 ... offen lds): 32-bit byte offsets, and an
-// offset past num_records zero-fills the LDS destination.  The host compilation pass of the
-// kernel templates only needs the signatures.
-#if defined(__HIP_DEVICE_COMPILE__)
-typedef __amdgpu_buffer_rsrc_t rsrc_t;
-RT_DEV rsrc_t make_rsrc(const void* p, int bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc((void*)p, 0, bytes, 0x00020000);
-}
-RT_DEV void buf_lds16(rsrc_t r, void* lds, int voff, int soff) {
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, voff, soff, 0, 0);
-}
-#else
-struct rsrc_t { int w[4]; };
-RT_DEV rsrc_t make_rsrc(const void*, int) { return rsrc_t{}; }
-RT_DEV void buf_lds16(rsrc_t, void*, int, int) {}
-#endif
-
 // 16 zero bytes: the DMA source of padding / out-of-range gathers.
 __device__ __attribute__((aligned(16))) bf16 g_conv_zero[8];
 template <int N> RT_DEV void wait_vmcnt() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
@@ -1505,9 +1488,18 @@ static void sp_pad4(const rtsds_conv_desc* d, const void* x, void* x4, hipStream
   hipLaunchKernelGGL(sp_pad4_kernel, dim3((unsigned)((px + 255) / 256)), dim3(256), 0, st, (const bf16*)x, (bf16*)x4, px);
 }
 
+// Halo-resident direct conv for narrow 3x3 outputs (hconv.hip).
+bool hconv_ok(const rtsds_conv_desc* d);
+int hconv_tiles(const rtsds_conv_desc* d);
+void hconv_fwd(const rtsds_conv_desc* d, const void* x, const void* w, const float* bias, const float* scale, void* y,
+               int act, float* stats, hipStream_t st);
+bool hconv_dgrad_ok(const rtsds_conv_desc* d);
+void hconv_dgrad(const rtsds_conv_desc* d, const void* dyp, int kp, const void* wt, void* dx, int accumulate, hipStream_t st);
+
 // Number of M tiles (= BatchNorm partial-statistics rows) the forward launch of d uses.
 extern "C" int rtsds_conv2d_fwd_stats_tiles(const rtsds_conv_desc* d) {
   if (pooled_1x1(d)) return 1;
+  if (hconv_ok(d)) return hconv_tiles(d);
   int bm, bn;
   const long M = (long)d->n * d->ho * d->wo;
   pick_tile(M, d->k, d->dtype == RTSDS_BF16, bm, bn);
@@ -1516,7 +1508,7 @@ extern "C" int rtsds_conv2d_fwd_stats_tiles(const rtsds_conv_desc* d) {
 
 // FWD workspace: channel-padded copies of x and w when Cin is not a vector multiple.
 extern "C" size_t rtsds_conv2d_fwd_workspace(const rtsds_conv_desc* d) {
-  if (pooled_1x1(d)) return 0;
+  if (pooled_1x1(d) || hconv_ok(d)) return 0;
   if (sp_path(d)) return sp_x4_bytes(d) + sp_w_bytes(d);
   const int cp = pad_c(d->c, d->dtype);
   if (cp == d->c) return 0;
@@ -1567,6 +1559,11 @@ extern "C" int rtsds_conv2d_fwd(const rtsds_conv_desc* d0, const void* x, const 
     else pooled_fwd_launch<float>(d0, x, w, bias, y, act & 0xff, accum, bn_stats, st);
     return hipGetLastError() == hipSuccess ? RTSDS_OK : RTSDS_ERR_LAUNCH;
   }
+  if (hconv_ok(d0) && !(act & RTSDS_ACCUMULATE)) {
+    if (bn_stats && (act & 0xff)) return RTSDS_ERR_UNSUPPORTED;
+    hconv_fwd(d0, x, w, bias, nullptr, y, act & 0xff, bn_stats, st);
+    return hipGetLastError() == hipSuccess ? RTSDS_OK : RTSDS_ERR_LAUNCH;
+  }
   rtsds_conv_desc d;
   fwd_prepare(d0, x, w, ws, d, st);
   ConvArgs p = make_args(&d);
@@ -1593,6 +1590,10 @@ extern "C" int rtsds_conv2d_fwd_bn(const rtsds_conv_desc* d0, const void* x, con
   if (e) return e;
   if (ws_bytes < rtsds_conv2d_fwd_workspace(d0)) return RTSDS_ERR_WORKSPACE;
   hipStream_t st = (hipStream_t)stream;
+  if (hconv_ok(d0) && !res) {
+    hconv_fwd(d0, x, w, shift, scale, y, act & 0xff, nullptr, st);
+    return hipGetLastError() == hipSuccess ? RTSDS_OK : RTSDS_ERR_LAUNCH;
+  }
   rtsds_conv_desc d;
   fwd_prepare(d0, x, w, ws, d, st);
   ConvArgs p = make_args(&d);
@@ -1661,6 +1662,12 @@ extern "C" int rtsds_conv2d_dgrad(const rtsds_conv_desc* d0, const void* dy, con
   }
   const int k_real = d.k;
   d.k = kp;
+  if (kp == 32 && hconv_dgrad_ok(d0)) {
+    // narrow-output 3x3 conv: halo direct conv over dY with the flipped, transposed weights
+    repack_launch(d.dtype, w, wt, k_real, kp, d.kh, d.kw, d.c, d.kh, d.kw, d.kh - 1, d.kw - 1, -1, st);
+    hconv_dgrad(d0, dy, kp, wt, dx, accumulate, st);
+    return hipGetLastError() == hipSuccess ? RTSDS_OK : RTSDS_ERR_LAUNCH;
+  }
   if (d.sh == 2 && d.sw == 2) {
     // stride-2: the four parity phases, each a dense GEMM over only the taps that reach it,
     // repacked by one launch and computed by one launch (blockIdx.z = phase)

@@ -1,0 +1,281 @@
+// Halo-resident direct 3x3 convolution for narrow outputs (Cout <= 32) -- the BiSeNet feature
+// fusion ConvBlock, 1024 -> 19 channels at 1/8 resolution (build_bisenet.py:64-65 via
+// ConvBlock build_bisenet.py:9-18), forward only.
+//
+// As an implicit GEMM this conv is N = 19 wide: every input byte the im2col gathers feeds only
+// 19 outputs, and the 3x3 taps gather each input pixel 9 times, so the generic kernel is bound
+// by LDS-DMA throughput (36 KB staged per 64-deep K-step for 256 x 32 outputs).  Here a
+// workgroup owns a 4 x 64 output tile and walks the input channels in chunks of 32: per chunk
+// it stages the (4+2) x (64+2) input halo ONCE (25 KB) plus the chunk's weights for all 9 taps
+// (32 x 9 x 32, 18 KB) and runs the 9 taps out of LDS -- 1.7x fewer staged bytes per MFMA
+// than one tap per K-step, and no per-tap re-gather.  Both LDS images are double-buffered
+// (the next chunk's DMA is in flight while this one computes) and XOR-swizzled for
+// conflict-free ds_read_b128 fragments: 16-B chunk c of halo pixel p (weight row n) sits at
+// slot c ^ ((p >> 2) & 3) (c ^ ((n >> 2) & 3)).
+//
+// Wave w computes output row w of the tile: 4 x 2 MFMA 16x16x32 tiles (64 pixels x 32
+// channels).  Epilogue: bias (or eval-BN scale/shift), activation, the following BatchNorm's
+// per-tile partial statistics (count, mean, M2 -- the exact two-pass form, as the GEMM
+// epilogue), scalar bf16 stores of the Cout valid channels.
+#include "common.h"
+
+namespace {
+constexpr int kTR = 4, kTC = 64, kCK = 32;
+constexpr int kHR = kTR + 2, kHC = kTC + 2, kHaloPix = kHR * kHC;  // 6 x 66 = 396
+constexpr int kHaloInstr = 28;  // ceil(396 * 4 / 64) = 25 wave-instructions, padded to 7 per wave
+constexpr int kWInstr = 20;     // 9 taps x 32 rows x 4 chunks / 64 = 18, padded to 5 per wave
+constexpr int kHaloBytes = kHaloInstr * 1024, kWBytes = kWInstr * 1024;
+constexpr int kBuf = kHaloBytes + kWBytes;  // 48 KB per stage
+}  // namespace
+
+struct HconvArgs {
+  const bf16* x;       // NHWC [n][h][w][c]
+  const bf16* wt;      // [k][3][3][c]
+  const float* bias;   // [k] or null (eval fold: shift)
+  const float* scale;  // [k] or null (eval fold)
+  bf16* y;             // NHWC [n][h][w][k]
+  float* stats;        // [tiles][k][3] or null (single N tile only)
+  int n, h, w, c, k, act, accum;  // k = output channels, tiled by 32 over blockIdx.y
+};
+
+__global__ void __launch_bounds__(256, 1) hconv_fwd_kernel(const HconvArgs P) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];  // 2 x kBuf
+  __shared__ float red[4][32];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tw_n = P.w / kTC, th_n = P.h / kTR;
+  int bid;
+  {  // XCD-aware bijective remap: each XCD gets a contiguous run of tiles (shared halo rows)
+    const int nwg = gridDim.x, b = blockIdx.x;
+    const int xcd = b & 7, q = nwg >> 3, r = nwg & 7;
+    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
+  }
+  const int img = bid / (th_n * tw_n), rem = bid - img * th_n * tw_n;
+  const int trow = rem / tw_n, tcol = rem - trow * tw_n;
+  const int oh0 = trow * kTR, ow0 = tcol * kTC;
+  const int C = P.c, n0 = blockIdx.y * 32;
+  const rsrc_t rx = make_rsrc(P.x, P.n * P.h * P.w * C * 2);
+  const rsrc_t rw = make_rsrc(P.wt, P.k * 9 * C * 2);
+
+  // Per-lane DMA pieces (16 B each), fixed for the whole channel walk: wave w issues
+  // wave-instructions w, w + 4, ...; each lane's byte offset at channel chunk 0 (chunk q adds
+  // q * 64 B as soffset; invalid pieces carry an offset past num_records -> zero-filled).
+  int hoff[kHaloInstr / 4], woff[kWInstr / 4];
+#pragma unroll
+  for (int u = 0; u < kHaloInstr / 4; ++u) {
+    const int piece = (wave + 4 * u) * 64 + lane, hp = piece >> 2, slot = piece & 3;
+    int v = (int)0x80000000;
+    if (hp < kHaloPix) {
+      const int hr = hp / kHC, hc = hp - hr * kHC;
+      const int ih = oh0 - 1 + hr, iw = ow0 - 1 + hc;
+      const int ch = slot ^ ((hp >> 2) & 3);
+      if ((unsigned)ih < (unsigned)P.h && (unsigned)iw < (unsigned)P.w)
+        v = (((img * P.h + ih) * P.w + iw) * C + ch * 8) * 2;
+    }
+    hoff[u] = v;
+  }
+#pragma unroll
+  for (int u = 0; u < kWInstr / 4; ++u) {
+    const int piece = (wave + 4 * u) * 64 + lane;
+    int v = (int)0x80000000;
+    if (piece < 9 * 32 * 4) {
+      const int tap = piece >> 7, n = (piece >> 2) & 31, slot = piece & 3;
+      const int ch = slot ^ ((n >> 2) & 3);
+      v = (((n0 + n) * 9 + tap) * C + ch * 8) * 2;  // rows n0 + n >= k fall past num_records
+    }
+    woff[u] = v;
+  }
+  auto issue = [&](int q, int buf) {
+    unsigned char* hb = lds + buf * kBuf;
+    unsigned char* wb = hb + kHaloBytes;
+    const int qoff = q * kCK * 2;
+#pragma unroll
+    for (int u = 0; u < kHaloInstr / 4; ++u) buf_lds16(rx, hb + (wave + 4 * u) * 1024, hoff[u], qoff);
+#pragma unroll
+    for (int u = 0; u < kWInstr / 4; ++u) buf_lds16(rw, wb + (wave + 4 * u) * 1024, woff[u], qoff);
+  };
+
+  f32x4 acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int fr = lane & 15, fc = lane >> 4;  // fragment row, 16-B k-chunk
+  int bslot[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int n = 16 * j + fr;
+    bslot[j] = (n * 4 + (fc ^ ((n >> 2) & 3))) * 16;
+  }
+
+  const int Q = C / kCK;
+  issue(0, 0);
+  for (int q = 0; q < Q; ++q) {
+    if (q + 1 < Q) {
+      issue(q + 1, (q + 1) & 1);
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kHaloInstr / 4 + kWInstr / 4) : "memory");  // chunk q landed
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    const unsigned char* hb = lds + (q & 1) * kBuf;
+    const unsigned char* wb = hb + kHaloBytes;
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+      const int r = tap / 3, s = tap - 3 * r;
+      bf16x8 fa[4], fb[2];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int hp = (wave + r) * kHC + 16 * i + fr + s;
+        fa[i] = *(const bf16x8*)(hb + hp * 64 + ((fc ^ ((hp >> 2) & 3)) << 4));
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j) fb[j] = *(const bf16x8*)(wb + tap * 32 * 64 + bslot[j]);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    }
+    __builtin_amdgcn_s_barrier();  // every wave is done with this buffer before it is refilled
+    asm volatile("" ::: "memory");
+  }
+
+  // ---- epilogue: C[pixel = 16 i + 4 (lane >> 4) + e][channel = 16 j + (lane & 15)]
+  const int er = (lane >> 4) * 4;
+  float v[4][2][4];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int n = n0 + 16 * j + fr;
+    const bool ok = n < P.k;
+    const float bv = (P.bias && ok) ? P.bias[n] : 0.f;
+    const float sv = (P.scale && ok) ? P.scale[n] : 1.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[i][j][e] = fmaf(acc[i][j][e], sv, bv);
+  }
+  if (P.stats) {
+    // per-channel (count, mean, M2) over the tile's 256 pixels, exact two-pass
+    float mean[2];
+#pragma unroll
+    for (int pass = 0; pass < 2; ++pass) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        float sacc = 0.f;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float t = pass == 0 ? v[i][j][e] : (v[i][j][e] - mean[j]) * (v[i][j][e] - mean[j]);
+            sacc += t;
+          }
+        sacc += __shfl_xor(sacc, 16, 64);
+        sacc += __shfl_xor(sacc, 32, 64);
+        if (lane < 16) red[wave][16 * j + lane] = sacc;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int n = 16 * j + fr;
+        const float tot = (red[0][n] + red[1][n]) + (red[2][n] + red[3][n]);
+        if (pass == 0) {
+          mean[j] = tot / (float)(kTR * kTC);
+        } else if (wave == 0 && lane < 16 && n < P.k) {
+          float* o = P.stats + ((long)bid * P.k + n) * 3;
+          o[0] = (float)(kTR * kTC);
+          o[1] = mean[j];
+          o[2] = tot;
+        }
+      }
+      __syncthreads();
+    }
+  }
+  auto act_f = [&](float t) {
+    if (P.act == RTSDS_ACT_RELU) return fmaxf(t, 0.f);
+    if (P.act == RTSDS_ACT_LEAKY) return t > 0.f ? t : 0.2f * t;
+    if (P.act == RTSDS_ACT_SIGMOID) return 1.f / (1.f + expf(-t));
+    return t;
+  };
+  if (P.k % 8 == 0) {
+    // 16-B stores: the [256 px][32 ch] bf16 tile goes through LDS (the operand buffers are free
+    // after the loop's last barrier), then each thread writes 4 row chunks
+    bf16* cs = (bf16*)lds;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int px = wave * kTC + 16 * i + er + e;
+          cs[px * 32 + 16 * j + fr] = (bf16)(P.accum ? v[i][j][e] : act_f(v[i][j][e]));
+        }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int cidx = tid + 256 * u, px = cidx >> 2, n = n0 + (cidx & 3) * 8;
+      if (n >= P.k) continue;
+      const long o = (((long)img * P.h + oh0 + (px >> 6)) * P.w + ow0 + (px & 63)) * P.k + n;
+      bf16x8 t = *(const bf16x8*)(cs + px * 32 + (cidx & 3) * 8);
+      if (P.accum) {
+        const bf16x8 old = *(const bf16x8*)(P.y + o);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) t[q] = (bf16)act_f((float)t[q] + (float)old[q]);
+      }
+      *(bf16x8*)(P.y + o) = t;
+    }
+    return;
+  }
+  const long row = ((long)img * P.h + oh0 + wave) * P.w + ow0;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int n = n0 + 16 * j + fr;
+    if (n >= P.k) continue;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float t = v[i][j][e];
+        if (P.accum) t += (float)P.y[(row + 16 * i + er + e) * P.k + n];
+        P.y[(row + 16 * i + er + e) * P.k + n] = (bf16)act_f(t);
+      }
+  }
+}
+
+// ---- host -------------------------------------------------------------------------------
+static bool hconv_geom(const rtsds_conv_desc* d) {
+  return d->dtype == RTSDS_BF16 && d->kh == 3 && d->kw == 3 && d->sh == 1 && d->sw == 1 && d->ph == 1 && d->pw == 1 &&
+         d->dh == 1 && d->dw == 1 && d->h % kTR == 0 && d->w % kTC == 0;
+}
+// forward: narrow outputs (Cout <= 32)
+bool hconv_ok(const rtsds_conv_desc* d) {
+  if (!hconv_geom(d) || d->c % kCK != 0 || d->k > 32) return false;
+  return (long)d->n * d->h * d->w * d->c * 2 < (1L << 31);
+}
+// data gradient of a narrow-output conv (the same 3x3 same-padding conv run over dY with the
+// flipped, transposed weights): Cout <= 32 padded to 32 input channels, Cin outputs tiled by 32
+bool hconv_dgrad_ok(const rtsds_conv_desc* d) {
+  if (!hconv_geom(d) || d->k > 32) return false;
+  return (long)d->n * d->h * d->w * d->c * 2 < (1L << 31);
+}
+int hconv_tiles(const rtsds_conv_desc* d) { return d->n * (d->h / kTR) * (d->w / kTC); }
+static void hconv_launch(const HconvArgs& a, int tiles, int ntiles, hipStream_t st) {
+  static const bool lds_ok = hipFuncSetAttribute((const void*)hconv_fwd_kernel,
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, 2 * kBuf) == hipSuccess;
+  (void)lds_ok;
+  const int lds = a.c / kCK > 1 ? 2 * kBuf : kBuf;  // one channel chunk: a single stage
+  hipLaunchKernelGGL(hconv_fwd_kernel, dim3(tiles, ntiles), dim3(256), lds, st, a);
+}
+void hconv_fwd(const rtsds_conv_desc* d, const void* x, const void* w, const float* bias, const float* scale, void* y,
+               int act, float* stats, hipStream_t st) {
+  HconvArgs a;
+  a.x = (const bf16*)x; a.wt = (const bf16*)w; a.bias = bias; a.scale = scale; a.y = (bf16*)y; a.stats = stats;
+  a.n = d->n; a.h = d->h; a.w = d->w; a.c = d->c; a.k = d->k; a.act = act; a.accum = 0;
+  hconv_launch(a, hconv_tiles(d), 1, st);
+}
+// dx (+)= conv(dy_p, wt_flipped): dy_p [n][h][w][kp] (kp = 32), wt [c][3][3][kp]
+void hconv_dgrad(const rtsds_conv_desc* d, const void* dyp, int kp, const void* wt, void* dx, int accumulate, hipStream_t st) {
+  HconvArgs a;
+  a.x = (const bf16*)dyp; a.wt = (const bf16*)wt; a.bias = nullptr; a.scale = nullptr; a.y = (bf16*)dx; a.stats = nullptr;
+  a.n = d->n; a.h = d->h; a.w = d->w; a.c = kp; a.k = d->c; a.act = 0; a.accum = accumulate ? 1 : 0;
+  hconv_launch(a, hconv_tiles(d), (d->c + 31) / 32, st);
+}

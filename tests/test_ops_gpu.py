@@ -54,6 +54,8 @@ CONV_CASES = [
     (2, 8, 9, 11, 16, 4, 2, 1, 1, True),       # k4 s2 phases, odd sizes
     (2, 16, 7, 9, 32, 1, 2, 0, 1, False),      # 1x1 s2: odd phases receive nothing
     (8, 128, 64, 64, 128, 3, 1, 1, 1, False),  # 128x128 LDS-DMA tiles (fwd and dgrad)
+    (2, 128, 8, 128, 19, 3, 1, 1, 1, False),   # halo direct conv (hconv.hip): Cout 19, w % 64 == 0
+    (1, 64, 12, 64, 32, 3, 1, 1, 1, True),     # hconv with bias, Cout 32, edge tiles on 3 row-blocks
 ]
 
 
@@ -496,3 +498,23 @@ def test_bisenet_eval_fold_and_graph(dt):
     scale = ref.abs().max().item()
     assert (fused.float() - ref.float()).abs().max().item() <= tol * scale
     assert torch.equal(rep1, fused) and torch.equal(rep2, eager2)
+
+
+@pytest.mark.parametrize("shape", [(2, 128, 8, 128, 19), (2, 64, 8, 64, 32), (2, 64, 6, 20, 19)])
+def test_conv_bn_stats_epilogue(shape):
+    """Train-mode ConvBlock (conv -> BN with batch statistics from the conv epilogue -> ReLU):
+    the GEMM epilogue and the halo direct conv (hconv.hip, w % 64 == 0) both against ATen."""
+    from rtsds_amd import nn as rnn
+    n, c, h, w, k = shape
+    g = torch.Generator().manual_seed(7)
+    x = torch.randn(n, c, h, w, generator=g, dtype=torch.float64).bfloat16().double()
+    conv = rnn.Conv2d(c, k, 3, padding=1, bias=False).to(DEV)
+    bn = rnn.BatchNorm2d(k).to(DEV)
+    with torch.no_grad():
+        conv.weight.copy_((torch.randn(k, c, 3, 3, generator=g) / (9 * c) ** 0.5).bfloat16().float())
+    wr = conv.weight.detach().double().cpu()
+    yr = TF.relu(TF.batch_norm(TF.conv2d(x, wr, None, 1, 1), None, None, None, None, True, 0.1, 1e-5))
+    y = rnn.conv_bn(conv, bn, _dev(x, torch.bfloat16), "relu")
+    _close(y, yr, torch.bfloat16, "y")
+    rm_ref = 0.1 * TF.conv2d(x, wr, None, 1, 1).mean(dim=(0, 2, 3))
+    _close(bn.running_mean, rm_ref, torch.bfloat16, "running_mean")
