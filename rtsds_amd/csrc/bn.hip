@@ -186,18 +186,25 @@ RT_DEV void chan_merge_shfl(float& n, float& m, float& M) {
     chan_merge(n, m, M, nb, mb, Mb);
   }
 }
-__global__ void __launch_bounds__(64) bn_finalize_kernel(const float* __restrict__ part, int nrb, int c, long rows, const float* gamma,
+// 4 waves per channel: wave w merges partials b = w*64 + lane (+ 256 k), then the four wave
+// results are merged in wave order -- up to kBnMaxRB partials without a pre-merge launch.
+__global__ void __launch_bounds__(256) bn_finalize_kernel(const float* __restrict__ part, int nrb, int c, long rows, const float* gamma,
                                    const float* beta, float* rmean, float* rvar, float* smean, float* sinv,
                                    float* scale, float* shift, float momentum, float eps, long long* nbt) {
-  const int ch = blockIdx.x, lane = threadIdx.x;
-  if (nbt && ch == 0 && lane == 0) *nbt += 1;  // num_batches_tracked.add_(1)
+  __shared__ float wr[4][3];
+  const int ch = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (nbt && ch == 0 && threadIdx.x == 0) *nbt += 1;  // num_batches_tracked.add_(1)
   float n = 0.f, m = 0.f, M = 0.f;
-  for (int b = lane; b < nrb; b += 64) {
+  for (int b = threadIdx.x; b < nrb; b += 256) {
     const float* p = part + ((long)b * c + ch) * 3;
     chan_merge(n, m, M, p[0], p[1], p[2]);
   }
   chan_merge_shfl(n, m, M);
-  if (lane != 0) return;
+  if (lane == 0) { wr[wave][0] = n; wr[wave][1] = m; wr[wave][2] = M; }
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  n = wr[0][0]; m = wr[0][1]; M = wr[0][2];
+  for (int w = 1; w < 4; ++w) chan_merge(n, m, M, wr[w][0], wr[w][1], wr[w][2]);
   const float var = M / (float)rows;
   const float inv = 1.0f / sqrtf(var + eps);
   smean[ch] = m;
@@ -437,18 +444,23 @@ __global__ void __launch_bounds__(256) bn_bwd_stats_kernel(const T* __restrict__
 
 // Backward pass 2: coefficients  dx = A*g + B*(x-mean) + C  per channel (one wave each).
 // coef = [A | B | C | mean | scale | shift] x c  (the last three for the mask recompute).
-__global__ void __launch_bounds__(64) bn_bwd_finalize_kernel(const float* __restrict__ part, int nrb, int c, long rows, const float* gamma,
+__global__ void __launch_bounds__(256) bn_bwd_finalize_kernel(const float* __restrict__ part, int nrb, int c, long rows, const float* gamma,
                                        const float* beta, const float* smean, const float* sinv, float* dgamma, float* dbeta,
                                        float* coef, int training, int accumulate) {
-  const int ch = blockIdx.x, lane = threadIdx.x;
+  __shared__ float wr[4][2];
+  const int ch = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   float sg = 0.f, sgx = 0.f;
-  for (int b = lane; b < nrb; b += 64) {
+  for (int b = threadIdx.x; b < nrb; b += 256) {
     sg += part[((long)b * c + ch) * 2];
     sgx += part[((long)b * c + ch) * 2 + 1];
   }
   sg = wave_sum(sg);
   sgx = wave_sum(sgx);
-  if (lane != 0) return;
+  if (lane == 0) { wr[wave][0] = sg; wr[wave][1] = sgx; }
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  sg = (wr[0][0] + wr[1][0]) + (wr[2][0] + wr[3][0]);
+  sgx = (wr[0][1] + wr[1][1]) + (wr[2][1] + wr[3][1]);
   const float inv = sinv[ch], g = gamma ? gamma[ch] : 1.f;
   if (dgamma) dgamma[ch] = accumulate ? dgamma[ch] + sgx * inv : sgx * inv;
   if (dbeta) dbeta[ch] = accumulate ? dbeta[ch] + sg : sg;
@@ -585,8 +597,7 @@ static void bn_fwd_launch(const void* x, const void* res, void* y, long rows, in
       hipLaunchKernelGGL((bn_stats_kernel<T, VEC>), dim3(rb, rt_cdiv(c, 256 * VEC)), dim3(256), 0, st, (const T*)x, w.part, rows, c);
       part = w.part;
     }
-    part = bn_premerge<3>(part, rb, c, w.merged, st);
-    hipLaunchKernelGGL(bn_finalize_kernel, dim3(c), dim3(64), 0, st, part, rb, c, rows, gamma, beta, rm, rv,
+    hipLaunchKernelGGL(bn_finalize_kernel, dim3(c), dim3(256), 0, st, part, rb, c, rows, gamma, beta, rm, rv,
                        sm, si, scale, shift, mom, eps, nbt);
   } else {
     hipLaunchKernelGGL(bn_eval_coef_kernel, dim3(rt_cdiv(c, 256)), dim3(256), 0, st, c, gamma, beta, rm, rv, scale, shift, sm, si, eps);
@@ -626,8 +637,7 @@ static void bn_bwd_launch(const void* dy, const void* x, const void* y, void* dx
   float* part = w.part;
   hipLaunchKernelGGL((bn_bwd_stats_kernel<T, VEC>), dim3(rb, rt_cdiv(c, 256 * VEC)), dim3(256), 0, st, (const T*)dy, (const T*)x, (const T*)y, gamma, beta,
                      smean, sinv, part, rows, c, act);
-  const float* mp = bn_premerge<2>(part, rb, c, w.merged, st);
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(c), dim3(64), 0, st, mp, rb, c, rows, gamma, beta, smean, sinv,
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(c), dim3(256), 0, st, part, rb, c, rows, gamma, beta, smean, sinv,
                      dgamma, dbeta, w.coef, training, accumulate);
   if (dx || dres) {
     hipLaunchKernelGGL((bn_bwd_apply_kernel<T, VEC>), dim3(bn_apply_rb(rows, c, VEC), rt_cdiv(c, 256 * VEC)), dim3(256), 0, st,

@@ -1083,26 +1083,33 @@ __global__ void __launch_bounds__(256) pad_channels_kernel(const T* __restrict__
 // dw[co][tap][ci] = sum_s part[s][co][tap][ci_p]   (split-K reduce + channel unpad).
 // V consecutive input channels per thread (16-byte slab reads when c % 4 == 0), splits
 // summed in a fixed order -- deterministic, no atomics.
+// Block = 64 outputs x 4 split groups (wave g sums splits g, g + 4, ... in order; the four
+// group sums are then added in group order): the many-split reductions of small weight
+// tensors (ResNet layer1: ~100 splits) get 4x the parallelism of one thread per output.
 template <int V>
 __global__ void __launch_bounds__(256) split_reduce_kernel(const float* __restrict__ part, float* __restrict__ out, int nv,
                                                             int cv, FastDiv fcv, int cp, long slab, int splits, int accumulate) {
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += gridDim.x * blockDim.x) {
-    const int rt = (int)fdiv((uint32_t)i, fcv);  // co * taps + tap
-    const long src = (long)rt * cp + (long)(i - rt * cv) * V;
+  __shared__ float red[4][64][V];
+  const int lane = threadIdx.x & 63, sg = threadIdx.x >> 6;
+  for (int i0 = blockIdx.x * 64; i0 < nv; i0 += gridDim.x * 64) {
+    const int i = i0 + lane;
+    const bool ok = i < nv;
+    const int rt = (int)fdiv((uint32_t)(ok ? i : 0), fcv);  // co * taps + tap
+    const long src = (long)rt * cp + (long)((ok ? i : 0) - rt * cv) * V;
     float s[V];
 #pragma unroll
     for (int e = 0; e < V; ++e) s[e] = 0.f;
-    int q = 0;
-    for (; q + 4 <= splits; q += 4) {
+    int q = sg;
+    for (; ok && q + 12 < splits; q += 16) {
       float t[4][V];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         if constexpr (V == 4) {
-          const f32x4 v = *(const f32x4*)(part + (long)(q + u) * slab + src);
+          const f32x4 v = *(const f32x4*)(part + (long)(q + 4 * u) * slab + src);
 #pragma unroll
           for (int e = 0; e < V; ++e) t[u][e] = v[e];
         } else {
-          t[u][0] = part[(long)(q + u) * slab + src];
+          t[u][0] = part[(long)(q + 4 * u) * slab + src];
         }
       }
 #pragma unroll
@@ -1110,12 +1117,21 @@ __global__ void __launch_bounds__(256) split_reduce_kernel(const float* __restri
 #pragma unroll
         for (int e = 0; e < V; ++e) s[e] += t[u][e];
     }
-    for (; q < splits; ++q)
+    for (; ok && q < splits; q += 4)
 #pragma unroll
       for (int e = 0; e < V; ++e) s[e] += part[(long)q * slab + src + e];
-    float* o = out + (long)i * V;
 #pragma unroll
-    for (int e = 0; e < V; ++e) o[e] = accumulate ? o[e] + s[e] : s[e];
+    for (int e = 0; e < V; ++e) red[sg][lane][e] = s[e];
+    __syncthreads();
+    if (sg == 0 && ok) {
+      float* o = out + (long)i * V;
+#pragma unroll
+      for (int e = 0; e < V; ++e) {
+        const float t = (red[0][lane][e] + red[1][lane][e]) + (red[2][lane][e] + red[3][lane][e]);
+        o[e] = accumulate ? o[e] + t : t;
+      }
+    }
+    __syncthreads();
   }
 }
 
@@ -1845,7 +1861,7 @@ extern "C" int rtsds_conv2d_wgrad(const rtsds_conv_desc* d0, const void* x, cons
   else wgrad_launch<float>(p, pl.bm, pl.bn, pl.splits, st);
   if (sp) {
     const int nv = dv.k * dv.kh * dv.kw * 2;
-    hipLaunchKernelGGL(split_reduce_kernel<4>, dim3(std::min(8192, (nv + 255) / 256)), dim3(256), 0, st, (const float*)slab, dws,
+    hipLaunchKernelGGL(split_reduce_kernel<4>, dim3(std::min(8192, (nv + 63) / 64)), dim3(256), 0, st, (const float*)slab, dws,
                        nv, 2, fastdiv_make(2), 8, p.split_stride, pl.splits, 0);
     const int n = d0->k * d0->kh * d0->kw * 3;
     hipLaunchKernelGGL(sp_unpack_dw_kernel, dim3(rt_cdiv(n, 256)), dim3(256), 0, st, (const float*)dws, dw, d0->k, d0->kh,
@@ -1853,7 +1869,7 @@ extern "C" int rtsds_conv2d_wgrad(const rtsds_conv_desc* d0, const void* x, cons
   } else {
     const int V = d0->c % 4 == 0 ? 4 : 1, cv = d0->c / V;
     const int nv = d0->k * d0->kh * d0->kw * cv;
-    const int blocks = std::min(8192, (nv + 255) / 256);
+    const int blocks = std::min(8192, (nv + 63) / 64);
     if (V == 4)
       hipLaunchKernelGGL(split_reduce_kernel<4>, dim3(blocks), dim3(256), 0, st, (const float*)slab, dw, nv, cv, fastdiv_make(cv),
                          pl.cp, p.split_stride, pl.splits, accumulate);
