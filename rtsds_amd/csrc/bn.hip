@@ -368,16 +368,19 @@ __global__ void __launch_bounds__(256) bn_bwd_stats_kernel(const T* __restrict__
       float g[U][VEC], xv[U][VEC], yv[U][VEC];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const long rr = r + u * step;
-        if (rr < rows) {
-          load_vec<T, VEC>(dy + rr * c + ch0, g[u], c - ch0);
-          load_vec<T, VEC>(x + rr * c + ch0, xv[u], c - ch0);
-          if (y && act) load_vec<T, VEC>(y + rr * c + ch0, yv[u], c - ch0);
-        } else {
-#pragma unroll
-          for (int j = 0; j < VEC; ++j) { g[u][j] = 0.f; xv[u][j] = mu[j]; yv[u][j] = 0.f; }
-        }
+        // clamped, unconditional loads (all U rows in flight together); rows past the end
+        // contribute g = 0
+        const long rr = min(r + u * step, rows - 1);
+        load_vec<T, VEC>(dy + rr * c + ch0, g[u], c - ch0);
+        load_vec<T, VEC>(x + rr * c + ch0, xv[u], c - ch0);
+        if (y && act) load_vec<T, VEC>(y + rr * c + ch0, yv[u], c - ch0);
       }
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (r + u * step >= rows) {
+#pragma unroll
+          for (int j = 0; j < VEC; ++j) g[u][j] = 0.f;
+        }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         if (act) {

@@ -1511,6 +1511,8 @@ void hconv_fwd(const rtsds_conv_desc* d, const void* x, const void* w, const flo
                int act, float* stats, hipStream_t st);
 bool hconv_dgrad_ok(const rtsds_conv_desc* d);
 void hconv_dgrad(const rtsds_conv_desc* d, const void* dyp, int kp, const void* wt, void* dx, int accumulate, hipStream_t st);
+bool pw_ok(const rtsds_conv_desc* d);
+void pw_dgrad(const rtsds_conv_desc* d, const void* dy, const void* w, void* dx, int accum, hipStream_t st);
 
 // Number of M tiles (= BatchNorm partial-statistics rows) the forward launch of d uses.
 extern "C" int rtsds_conv2d_fwd_stats_tiles(const rtsds_conv_desc* d) {
@@ -1625,7 +1627,7 @@ extern "C" int rtsds_conv2d_fwd_bn(const rtsds_conv_desc* d0, const void* x, con
 
 // DGRAD workspace: repacked (and Cout-padded) weights + a Cout-padded copy of dy if needed.
 extern "C" size_t rtsds_conv2d_dgrad_workspace(const rtsds_conv_desc* d) {
-  if (pooled_1x1(d)) return 0;
+  if (pooled_1x1(d) || pw_ok(d)) return 0;
   const int kp = pad_c(d->k, d->dtype);
   const size_t es = esize(d->dtype);
   size_t b = al256((size_t)kp * d->kh * d->kw * d->c * es);
@@ -1665,6 +1667,10 @@ extern "C" int rtsds_conv2d_dgrad(const rtsds_conv_desc* d0, const void* dy, con
   if (pooled_1x1(d0)) {
     if (d0->dtype == RTSDS_BF16) pooled_dgrad_launch<bf16>(d0, dy, w, dx, accumulate ? 1 : 0, st);
     else pooled_dgrad_launch<float>(d0, dy, w, dx, accumulate ? 1 : 0, st);
+    return hipGetLastError() == hipSuccess ? RTSDS_OK : RTSDS_ERR_LAUNCH;
+  }
+  if (pw_ok(d0)) {  // narrow-output 1x1: direct FMA over dY rows (pw.hip)
+    pw_dgrad(d0, dy, w, dx, accumulate ? 1 : 0, st);
     return hipGetLastError() == hipSuccess ? RTSDS_OK : RTSDS_ERR_LAUNCH;
   }
   rtsds_conv_desc d = *d0;

@@ -56,6 +56,10 @@ CONV_CASES = [
     (8, 128, 64, 64, 128, 3, 1, 1, 1, False),  # 128x128 LDS-DMA tiles (fwd and dgrad)
     (2, 128, 8, 128, 19, 3, 1, 1, 1, False),   # halo direct conv (hconv.hip): Cout 19, w % 64 == 0
     (1, 64, 12, 64, 32, 3, 1, 1, 1, True),     # hconv with bias, Cout 32, edge tiles on 3 row-blocks
+    (2, 512, 32, 64, 19, 1, 1, 0, 1, True),    # supervision 1x1 (pw.hip backward): 1 row group
+    (2, 40, 32, 64, 32, 1, 1, 0, 1, True),     # pw.hip: Cout 32, 12 row groups
+    (4, 19, 32, 32, 19, 1, 1, 0, 1, True),     # pw.hip: final 19->19, odd Cin (scalar lanes)
+    (1, 1024, 64, 64, 16, 1, 1, 0, 1, False),  # pw.hip: two lane passes over 1024 channels
 ]
 
 
@@ -88,6 +92,45 @@ def test_conv_fwd_bwd(case, dt):
     _close(wp.grad, wr.grad, dt, "dw")
     if bias:
         _close(bp.grad, br.grad, dt, "db")
+
+
+@pytest.mark.parametrize("c", [512, 19])
+def test_pw_backward_accumulate(c):
+    """Narrow 1x1 backward with the accumulate flag (pw.hip dgrad, GEMM wgrad): dx += dgrad,
+    dw/db += wgrad (the flat-arena gradient sink and ConvSum paths), checked against the
+    non-accumulating call plus the prior contents."""
+    import ctypes
+    from rtsds_amd._lib import lib
+    from rtsds_amd.functional import _conv_desc, _P
+    from rtsds_amd.runtime import stream, workspace
+
+    g = torch.Generator().manual_seed(c)
+    n, h, w, k = 2, 32, 64, 19
+    x = _dev(torch.randn(n, c, h, w, generator=g), torch.bfloat16)
+    dy = _dev(torch.randn(n, k, h, w, generator=g), torch.bfloat16)
+    wq = _dev(torch.randn(k, c, 1, 1, generator=g) / c ** 0.5, torch.bfloat16)
+    d = _conv_desc(x, k, 1, 1, (1, 1), (0, 0), (1, 1))
+    dx0 = _dev(torch.randn(n, c, h, w, generator=g), torch.bfloat16)
+    dx = dx0.clone()
+    dx_fresh = torch.empty_like(dx0)
+    ws = workspace(lib.rtsds_conv2d_dgrad_workspace(ctypes.byref(d)), x.device)
+    assert lib.rtsds_conv2d_dgrad(ctypes.byref(d), _P(dy), _P(wq), _P(dx), 1, _P(ws), ws.numel(), stream()) == 0
+    assert lib.rtsds_conv2d_dgrad(ctypes.byref(d), _P(dy), _P(wq), _P(dx_fresh), 0, _P(ws), ws.numel(), stream()) == 0
+    dw0 = torch.randn(k, c, generator=g).to(DEV)
+    db0 = torch.randn(k, generator=g).to(DEV)
+    dw, db = dw0.clone(), db0.clone()
+    dw_f, db_f = torch.empty_like(dw0), torch.empty_like(db0)
+    ws = workspace(lib.rtsds_conv2d_wgrad_workspace(ctypes.byref(d)), x.device)
+    for out_w, out_b, acc in ((dw, db, 1), (dw_f, db_f, 0)):
+        assert lib.rtsds_conv2d_wgrad(ctypes.byref(d), _P(x), _P(dy), _P(out_w), _P(out_b), acc, _P(ws), ws.numel(),
+                                      stream()) == 0
+    torch.cuda.synchronize()
+    _close(dx, dx0.double() + dx_fresh.double(), torch.bfloat16, "dx accum", tol=1e-2)
+    _close(dw, dw0.double() + dw_f.double(), torch.float32, "dw accum", tol=1e-5)
+    _close(db, db0.double() + db_f.double(), torch.float32, "db accum", tol=1e-5)
+    ref_w = torch.einsum("nkhw,nchw->kc", dy.double(), x.double())
+    _close(dw_f, ref_w, torch.float32, "dw", tol=1e-4)
+    _close(db_f, dy.double().sum((0, 2, 3)), torch.float32, "db", tol=1e-4)
 
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
