@@ -116,11 +116,12 @@ int rtsds_bn_bwd(const void* dy, const void* x, const void* y, void* dx, void* d
 /* ---------------------------------------------------------------- layout / dtype
  * Input images arrive NCHW fp32 from the reference's loaders (datasets/cityscapes.py:62,
  * main.py:69-72).  cast: weight shadows (fp32 master -> bf16) and dtype round trips.
- * copy_channels: torch.cat along channels and its backward split (build_bisenet.py:72,153). */
+ * copy_channels: torch.cat along channels and its backward split (build_bisenet.py:72,153);
+ * accumulate != 0: dst += src (a split slice whose tensor also has another reader).      */
 int rtsds_nchw_to_nhwc(const float* x, void* y, int n, int c, int h, int w, int dtype, void* stream);
 int rtsds_cast(const void* src, int src_dtype, void* dst, int dst_dtype, long n, void* stream);
 int rtsds_copy_channels(const void* src, int src_ld, int src_off, void* dst, int dst_ld, int dst_off,
-                        long rows, int cnt, int dtype, void* stream);
+                        long rows, int cnt, int accumulate, int dtype, void* stream);
 
 /* ---------------------------------------------------------------- pointwise activations
  * act 1 ReLU (build_bisenet.py:77), 2 LeakyReLU(0.2) (model.py:62,73), 3 sigmoid

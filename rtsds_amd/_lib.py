@@ -47,7 +47,7 @@ SIGNATURES = {
                              P, c_size_t, P]),
     "rtsds_nchw_to_nhwc": (c_int, [P, P, c_int, c_int, c_int, c_int, c_int, P]),
     "rtsds_cast": (c_int, [P, c_int, P, c_int, c_long, P]),
-    "rtsds_copy_channels": (c_int, [P, c_int, c_int, P, c_int, c_int, c_long, c_int, c_int, P]),
+    "rtsds_copy_channels": (c_int, [P, c_int, c_int, P, c_int, c_int, c_long, c_int, c_int, c_int, P]),
     "rtsds_act_fwd": (c_int, [P, P, c_long, c_int, c_int, P]),
     "rtsds_act_bwd": (c_int, [P, P, P, c_long, c_int, c_float, c_int, P]),
     "rtsds_maxpool_fwd": (c_int, [P, P, P] + [c_int] * 10 + [P]),

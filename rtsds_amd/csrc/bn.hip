@@ -195,9 +195,21 @@ __global__ void __launch_bounds__(256) bn_finalize_kernel(const float* __restric
   const int ch = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   if (nbt && ch == 0 && threadIdx.x == 0) *nbt += 1;  // num_batches_tracked.add_(1)
   float n = 0.f, m = 0.f, M = 0.f;
-  for (int b = threadIdx.x; b < nrb; b += 256) {
-    const float* p = part + ((long)b * c + ch) * 3;
-    chan_merge(n, m, M, p[0], p[1], p[2]);
+  // up to 8 partials per thread loaded before any merge (one L2 round trip instead of eight);
+  // merge order b = tid, tid + 256, ... as before
+  for (int b0 = threadIdx.x; b0 < nrb; b0 += 256 * 8) {
+    float pn[8], pm[8], pM[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int b = min(b0 + 256 * u, nrb - 1);
+      const float* p = part + ((long)b * c + ch) * 3;
+      const float n0 = p[0];  // clamped index: unconditional loads, zero count past nrb
+      pn[u] = b0 + 256 * u < nrb ? n0 : 0.f;
+      pm[u] = p[1];
+      pM[u] = p[2];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) chan_merge(n, m, M, pn[u], pm[u], pM[u]);
   }
   chan_merge_shfl(n, m, M);
   if (lane == 0) { wr[wave][0] = n; wr[wave][1] = m; wr[wave][2] = M; }
@@ -453,9 +465,18 @@ __global__ void __launch_bounds__(256) bn_bwd_finalize_kernel(const float* __res
   __shared__ float wr[4][2];
   const int ch = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   float sg = 0.f, sgx = 0.f;
-  for (int b = threadIdx.x; b < nrb; b += 256) {
-    sg += part[((long)b * c + ch) * 2];
-    sgx += part[((long)b * c + ch) * 2 + 1];
+  for (int b0 = threadIdx.x; b0 < nrb; b0 += 256 * 8) {  // 8 partials in flight per thread
+    float pg[8], px[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int b = min(b0 + 256 * u, nrb - 1);
+      const bool ok = b0 + 256 * u < nrb;
+      const float g = part[((long)b * c + ch) * 2], gx = part[((long)b * c + ch) * 2 + 1];
+      pg[u] = ok ? g : 0.f;
+      px[u] = ok ? gx : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) { sg += pg[u]; sgx += px[u]; }
   }
   sg = wave_sum(sg);
   sgx = wave_sum(sgx);

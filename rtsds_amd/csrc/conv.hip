@@ -911,13 +911,16 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(const ConvArgs P0) {
     const bool has_res = MODE == MODE_FWD && P.res != nullptr;
     bool stored = false;
     if constexpr (sizeof(T) == 2) {
-      if (!P.accum && P.N % V == 0) {
+      if (P.N % V == 0) {
         // Row-vectorised store: the 16x16 C fragments (4 rows x 1 column per lane) go through
         // LDS as bf16 [BM][BN + 8] and leave as 16-B row chunks (8 global_store_dwordx4 per
-        // thread for a 128x128 tile instead of 64 scattered 2-byte stores).
+        // thread for a 128x128 tile instead of 64 scattered 2-byte stores).  Residual and
+        // accumulate (y += result: ConvSum, GradJoin'd dgrad) are added on the 16-B chunks,
+        // the activation after them.
         constexpr int CP = BN + 8, CPR = BN / V;
         static_assert(BM * CP <= NBUF * (A_EL + B_EL), "epilogue staging fits the operand LDS");
         T* cs = smem;
+        const bool post = has_res || P.accum;
         __syncthreads();
 #pragma unroll
         for (int j = 0; j < FN; ++j) {
@@ -930,7 +933,7 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(const ConvArgs P0) {
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
               const float v = fmaf(acc[i][j][e], sv, bv);
-              cs[(wm0 + i * 16 + er + e) * CP + col] = from_f<T>(has_res ? v : act_f(v));
+              cs[(wm0 + i * 16 + er + e) * CP + col] = from_f<T>(post ? v : act_f(v));
             }
         }
         __syncthreads();
@@ -941,10 +944,22 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(const ConvArgs P0) {
           if (gm < P.M && gn < P.N) {
             const long o = out_row(gm) * P.N + gn;
             V16 v = *(const V16*)(cs + row * CP + cc * V);
-            if (has_res) {
-              const V16 r = *(const V16*)((const T*)P.res + o);
+            if (post) {
+              float f[V];
 #pragma unroll
-              for (int q = 0; q < V; ++q) v[q] = from_f<T>(act_f(to_f(v[q]) + to_f(r[q])));
+              for (int q = 0; q < V; ++q) f[q] = to_f(v[q]);
+              if (has_res) {
+                const V16 r = *(const V16*)((const T*)P.res + o);
+#pragma unroll
+                for (int q = 0; q < V; ++q) f[q] += to_f(r[q]);
+              }
+              if (P.accum) {
+                const V16 r = *(const V16*)(out + o);
+#pragma unroll
+                for (int q = 0; q < V; ++q) f[q] += to_f(r[q]);
+              }
+#pragma unroll
+              for (int q = 0; q < V; ++q) v[q] = from_f<T>(act_f(f[q]));
             }
             *(V16*)(out + o) = v;
           }
@@ -1099,27 +1114,27 @@ __global__ void __launch_bounds__(256) split_reduce_kernel(const float* __restri
     float s[V];
 #pragma unroll
     for (int e = 0; e < V; ++e) s[e] = 0.f;
-    int q = sg;
-    for (; ok && q + 12 < splits; q += 16) {
-      float t[4][V];
+    // splits sg, sg + 4, ... summed in order; 8 loads in flight per thread (clamped,
+    // unconditional; past-the-end ones contribute nothing)
+    for (int q = sg; ok && q < splits; q += 32) {
+      float t[8][V];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < 8; ++u) {
+        const long off = (long)min(q + 4 * u, splits - 1) * slab + src;
         if constexpr (V == 4) {
-          const f32x4 v = *(const f32x4*)(part + (long)(q + 4 * u) * slab + src);
+          const f32x4 v = *(const f32x4*)(part + off);
 #pragma unroll
           for (int e = 0; e < V; ++e) t[u][e] = v[e];
         } else {
-          t[u][0] = part[(long)(q + 4 * u) * slab + src];
+          t[u][0] = part[off];
         }
       }
 #pragma unroll
-      for (int u = 0; u < 4; ++u)
+      for (int u = 0; u < 8; ++u)
+        if (q + 4 * u < splits)
 #pragma unroll
-        for (int e = 0; e < V; ++e) s[e] += t[u][e];
+          for (int e = 0; e < V; ++e) s[e] += t[u][e];
     }
-    for (; ok && q < splits; q += 4)
-#pragma unroll
-      for (int e = 0; e < V; ++e) s[e] += part[(long)q * slab + src + e];
 #pragma unroll
     for (int e = 0; e < V; ++e) red[sg][lane][e] = s[e];
     __syncthreads();

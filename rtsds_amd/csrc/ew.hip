@@ -56,16 +56,20 @@ extern "C" int rtsds_cast(const void* src, int src_dtype, void* dst, int dst_dty
 // Channel-slice copy: dst[r][doff + j] = src[r][soff + j], j < cnt  (torch.cat / its backward
 // split along channels, build_bisenet.py:72,153).
 template <typename T>
-__global__ void copy_channels_kernel(const T* __restrict__ s, int sld, int soff, T* __restrict__ d, int dld, int doff, long rows, int cnt) {
+__global__ void copy_channels_kernel(const T* __restrict__ s, int sld, int soff, T* __restrict__ d, int dld, int doff, long rows, int cnt,
+                                     int acc) {
   const long total = rows * cnt;
   GRID_STRIDE(i, total) {
     const long r = i / cnt;
     const int j = (int)(i - r * cnt);
-    d[r * dld + doff + j] = s[r * sld + soff + j];
+    T* o = d + r * dld + doff + j;
+    const T v = s[r * sld + soff + j];
+    *o = acc ? from_f<T>(to_f(*o) + to_f(v)) : v;
   }
 }
 template <typename T>
-__global__ void copy_channels_vec_kernel(const T* __restrict__ s, int sld, int soff, T* __restrict__ d, int dld, int doff, long rows, int cnt) {
+__global__ void copy_channels_vec_kernel(const T* __restrict__ s, int sld, int soff, T* __restrict__ d, int dld, int doff, long rows, int cnt,
+                                         int acc) {
   typedef typename VecT<T>::v16 V16;
   constexpr int V = VecT<T>::N;
   const int cv = cnt / V;
@@ -73,19 +77,28 @@ __global__ void copy_channels_vec_kernel(const T* __restrict__ s, int sld, int s
   GRID_STRIDE(i, total) {
     const long r = i / cv;
     const int j = (int)(i - r * cv) * V;
-    *(V16*)(d + r * dld + doff + j) = *(const V16*)(s + r * sld + soff + j);
+    V16* o = (V16*)(d + r * dld + doff + j);
+    V16 v = *(const V16*)(s + r * sld + soff + j);
+    if (acc) {
+      const V16 a = *o;
+#pragma unroll
+      for (int q = 0; q < V; ++q) v[q] = from_f<T>(to_f(a[q]) + to_f(v[q]));
+    }
+    *o = v;
   }
 }
 extern "C" int rtsds_copy_channels(const void* src, int src_ld, int src_off, void* dst, int dst_ld, int dst_off, long rows,
-                                   int cnt, int dtype, void* stream) {
+                                   int cnt, int accumulate, int dtype, void* stream) {
   if (rows <= 0 || cnt <= 0) return RTSDS_ERR_SHAPE;
   hipStream_t st = (hipStream_t)stream;
   DISPATCH_T(dtype, {
     constexpr int V = VecT<T>::N;
     if (cnt % V == 0 && src_ld % V == 0 && dst_ld % V == 0 && src_off % V == 0 && dst_off % V == 0)
-      hipLaunchKernelGGL(copy_channels_vec_kernel<T>, dim3(ew_blocks(rows * cnt / V)), dim3(256), 0, st, (const T*)src, src_ld, src_off, (T*)dst, dst_ld, dst_off, rows, cnt);
+      hipLaunchKernelGGL(copy_channels_vec_kernel<T>, dim3(ew_blocks(rows * cnt / V)), dim3(256), 0, st, (const T*)src, src_ld, src_off, (T*)dst, dst_ld, dst_off, rows, cnt,
+                         accumulate ? 1 : 0);
     else
-      hipLaunchKernelGGL(copy_channels_kernel<T>, dim3(ew_blocks(rows * cnt)), dim3(256), 0, st, (const T*)src, src_ld, src_off, (T*)dst, dst_ld, dst_off, rows, cnt);
+      hipLaunchKernelGGL(copy_channels_kernel<T>, dim3(ew_blocks(rows * cnt)), dim3(256), 0, st, (const T*)src, src_ld, src_off, (T*)dst, dst_ld, dst_off, rows, cnt,
+                         accumulate ? 1 : 0);
   });
   RET_LAUNCH();
 }

@@ -78,6 +78,39 @@ def _conv_desc(x, k, kh, kw, stride, padding, dilation):
     return d
 
 
+class GradJoin:
+    """Gradient of a tensor read by ``n`` rtsds Functions -- a residual block's input, read by
+    conv1 and by the identity (BatchNorm residual) or downsample branch
+    (build_contextpath.py BasicBlock / Bottleneck; torchvision resnet.py semantics).
+
+    Autograd would sum the ``n`` contributions with its own elementwise add over the whole
+    activation.  Instead the first contribution's buffer is kept here and handed to the next
+    producer, whose kernel accumulates into it (conv dgrad ``accumulate`` flag); the first
+    ``n - 1`` backward calls return None for the tensor and the last returns the sum, so the
+    engine sees one gradient.  Order-independent: whichever producer runs last returns."""
+
+    __slots__ = ("left", "buf")
+
+    def __init__(self, n):
+        self.left = n
+        self.buf = None
+
+    def put(self, g):
+        """Record this producer's finished contribution (``g`` already includes ``buf``)."""
+        self.buf = g
+        self.left -= 1
+        return g if self.left == 0 else None
+
+
+def _join_add(join, g):
+    """Contribution ``g`` computed into its own buffer: fold any earlier one in, then put."""
+    if join is None:
+        return g
+    if join.buf is not None:  # not reached in the residual blocks (the BN runs first)
+        g.add_(join.buf)
+    return join.put(g)
+
+
 class ConvFn(torch.autograd.Function):
     """nn.Conv2d forward / backward (bias and LeakyReLU/ReLU epilogue optionally fused).
 
@@ -85,7 +118,7 @@ class ConvFn(torch.autograd.Function):
     parameter itself or its bf16 shadow); gradients are returned for ``weight``."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, wq, stride, padding, dilation, act, stats):
+    def forward(ctx, x, weight, bias, wq, stride, padding, dilation, act, stats, join=None):
         require_hip(x, weight)
         x = nhwc(x)
         k, _, kh, kw = weight.shape
@@ -97,6 +130,7 @@ class ConvFn(torch.autograd.Function):
                                  ws.numel(), stream())
         ctx.d, ctx.act, ctx.has_bias = d, act, bias is not None
         ctx.params = (weight, bias)
+        ctx.join = join
         ctx.save_for_backward(x, wq, y if act else None)
         return y
 
@@ -114,11 +148,15 @@ class ConvFn(torch.autograd.Function):
             g = dy
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
-            dx = empty_nhwc(d.n, d.c, d.h, d.w, x.dtype, x.device)
+            join = ctx.join
+            acc = join is not None and join.buf is not None  # accumulate onto the earlier contribution
+            dx = join.buf if acc else empty_nhwc(d.n, d.c, d.h, d.w, x.dtype, x.device)
             ws = workspace(lib.rtsds_conv2d_dgrad_workspace(ctypes.byref(d)), x.device)
             with _Timed(d, "dgrad"):
-                lib.rtsds_conv2d_dgrad(ctypes.byref(d), _P(g), _P(wq), _P(dx), 0, _P(ws), ws.numel(),
-                                       stream())
+                lib.rtsds_conv2d_dgrad(ctypes.byref(d), _P(g), _P(wq), _P(dx), 1 if acc else 0, _P(ws),
+                                       ws.numel(), stream())
+            if join is not None:
+                dx = join.put(dx)
         if ctx.needs_input_grad[1] or ctx.needs_input_grad[2]:
             weight, bias = ctx.params
             sinks = _sinks(weight, bias if ctx.needs_input_grad[2] else None) if ctx.needs_input_grad[1] else None
@@ -138,12 +176,14 @@ class ConvFn(torch.autograd.Function):
                                            ws.numel(), stream())
                 if not ctx.needs_input_grad[1]:
                     dw = None
-        return dx, dw, db, None, None, None, None, None, None
+        return dx, dw, db, None, None, None, None, None, None, None
 
 
-def conv2d(x, weight, bias, wq, stride=(1, 1), padding=(0, 0), dilation=(1, 1), act=0, bn_stats=False):
+def conv2d(x, weight, bias, wq, stride=(1, 1), padding=(0, 0), dilation=(1, 1), act=0, bn_stats=False,
+           join=None):
     """bn_stats=True: the conv epilogue also emits the following BatchNorm's per-tile batch
-    statistics, attached to the output as ``_rt_bn_stats`` and consumed by batch_norm()."""
+    statistics, attached to the output as ``_rt_bn_stats`` and consumed by batch_norm().
+    ``join``: GradJoin shared with the other readers of ``x``."""
     stats = nrb = None
     if bn_stats and act == 0:
         n, _, h, w = x.shape
@@ -151,7 +191,7 @@ def conv2d(x, weight, bias, wq, stride=(1, 1), padding=(0, 0), dilation=(1, 1), 
         d = _conv_desc(x, k, kh, kw, stride, padding, dilation)
         nrb = lib.rtsds_conv2d_fwd_stats_tiles(ctypes.byref(d))
         stats = torch.empty(nrb * k * 3, dtype=torch.float32, device=x.device)
-    y = ConvFn.apply(x, weight, bias, wq, tuple(stride), tuple(padding), tuple(dilation), act, stats)
+    y = ConvFn.apply(x, weight, bias, wq, tuple(stride), tuple(padding), tuple(dilation), act, stats, join)
     if stats is not None:
         y._rt_bn_stats = (stats, nrb)
     return y
@@ -253,7 +293,7 @@ class BatchNormFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, gamma, beta, res, running_mean, running_var, training, momentum, eps, act,
-                stats, stats_nrb, nbt):
+                stats, stats_nrb, nbt, res_join=None):
         require_hip(x)
         x = nhwc(x)
         if res is not None:
@@ -270,6 +310,7 @@ class BatchNormFn(torch.autograd.Function):
                          ws.numel(), stream())
         ctx.meta = (rows, c, int(training), act, res is not None)
         ctx.gamma, ctx.beta = gamma, beta
+        ctx.res_join = res_join
         # Without a residual the ReLU/LeakyReLU mask is recomputed from x in the backward
         # (bit-identical pre-activation), so y is neither kept nor re-read.
         keep_y = res is not None or act == ACT_SIGMOID
@@ -298,16 +339,19 @@ class BatchNormFn(torch.autograd.Function):
                          stream())
         if acc:
             dg = db = None
-        return dx, dg, db, dres, None, None, None, None, None, None, None, None, None
+        if dres is not None:
+            dres = _join_add(ctx.res_join, dres)
+        return dx, dg, db, dres, None, None, None, None, None, None, None, None, None, None
 
 
 def batch_norm(x, gamma, beta, running_mean, running_var, training, momentum, eps, act=0,
-               residual=None, num_batches_tracked=None):
-    """``num_batches_tracked`` (int64, optional) is incremented by the finalize kernel."""
+               residual=None, num_batches_tracked=None, res_join=None):
+    """``num_batches_tracked`` (int64, optional) is incremented by the finalize kernel.
+    ``res_join``: GradJoin shared with the other readers of ``residual``."""
     st = getattr(x, "_rt_bn_stats", None) if training else None
     stats, nrb = st if st is not None else (None, None)
     return BatchNormFn.apply(x, gamma, beta, residual, running_mean, running_var, training,
-                             momentum, eps, act, stats, nrb, num_batches_tracked)
+                             momentum, eps, act, stats, nrb, num_batches_tracked, res_join)
 
 
 # ----------------------------------------------------------------------------- layout / dtype
@@ -338,10 +382,11 @@ def cast(t, dtype):
 
 
 class CatFn(torch.autograd.Function):
-    """torch.cat(dim=1) of NHWC tensors (build_bisenet.py:72,153)."""
+    """torch.cat(dim=1) of NHWC tensors (build_bisenet.py:72,153).  ``joins[i]``: GradJoin of
+    input i when it has other readers (the split slice is accumulated into their gradient)."""
 
     @staticmethod
-    def forward(ctx, *xs):
+    def forward(ctx, joins, *xs):
         xs = [nhwc(x) for x in xs]
         n, _, h, w = xs[0].shape
         ct = sum(x.shape[1] for x in xs)
@@ -349,29 +394,34 @@ class CatFn(torch.autograd.Function):
         off = 0
         for x in xs:
             c = x.shape[1]
-            lib.rtsds_copy_channels(_P(x), c, 0, _P(y), ct, off, n * h * w, c, dcode(x), stream())
+            lib.rtsds_copy_channels(_P(x), c, 0, _P(y), ct, off, n * h * w, c, 0, dcode(x), stream())
             off += c
         ctx.split = [x.shape[1] for x in xs]
+        ctx.joins = joins
         return y
 
     @staticmethod
     def backward(ctx, dy):
         dy = nhwc(dy)
         n, ct, h, w = dy.shape
-        outs, off = [], 0
+        outs, off = [None], 0
         for i, c in enumerate(ctx.split):
-            if ctx.needs_input_grad[i]:
-                g = empty_nhwc(n, c, h, w, dy.dtype, dy.device)
-                lib.rtsds_copy_channels(_P(dy), ct, off, _P(g), c, 0, n * h * w, c, dcode(dy), stream())
-                outs.append(g)
+            if ctx.needs_input_grad[1 + i]:
+                join = ctx.joins[i] if ctx.joins else None
+                acc = join is not None and join.buf is not None
+                g = join.buf if acc else empty_nhwc(n, c, h, w, dy.dtype, dy.device)
+                lib.rtsds_copy_channels(_P(dy), ct, off, _P(g), c, 0, n * h * w, c, 1 if acc else 0, dcode(dy),
+                                        stream())
+                outs.append(join.put(g) if join is not None else g)
             else:
                 outs.append(None)
             off += c
         return tuple(outs)
 
 
-def cat(xs):
-    return CatFn.apply(*xs)
+def cat(xs, joins=None):
+    """``joins``: per-input GradJoin (or None) for inputs that have other readers."""
+    return CatFn.apply(joins, *xs)
 
 
 # ----------------------------------------------------------------------------- pointwise

@@ -12,7 +12,7 @@ import torch
 from torch import nn
 
 from rtsds_amd import functional as F
-from rtsds_amd.nn import AdaptiveAvgPool2d, BatchNorm2d, Conv2d, ReLU, Sigmoid, conv_bn, to_input
+from rtsds_amd.nn import AdaptiveAvgPool2d, BatchNorm2d, Conv2d, ReLU, Sigmoid, conv_bn, grad_join, to_input
 from .build_contextpath import build_contextpath
 
 
@@ -76,8 +76,12 @@ class FeatureFusionModule(torch.nn.Module):
         self.sigmoid = Sigmoid()
         self.avgpool = AdaptiveAvgPool2d(output_size=(1, 1))
 
-    def forward(self, input_1, input_2):
-        x = F.cat([input_1, input_2])
+    def forward(self, input_1, input_2, joins=None):
+        # input_2 may be the (cx1, cx2) pair itself: one concat pass instead of the
+        # reference's nested cat (build_bisenet.py:153 then :72), same channel order.
+        # joins: GradJoin per concatenated input (functional.cat)
+        parts = [input_1, *input_2] if isinstance(input_2, (tuple, list)) else [input_1, input_2]
+        x = F.cat(parts, joins)
         assert self.in_channels == x.size(1), \
             "in_channels of ConvBlock should be {}".format(x.size(1))
         feature = self.convblock(x)
@@ -137,11 +141,16 @@ class BiSeNet(torch.nn.Module):
         cx2 = F.interpolate_bilinear(cx2, size=hw)
         heads = []
         aux_on = self.training and not main_only
+        joins = None
         if aux_on:
+            # cx1 / cx2 are read by the concat and by a supervision conv: their gradients
+            # meet in one buffer (nn.grad_join) instead of an autograd add
+            j1, j2 = grad_join(cx1, 2), grad_join(cx2, 2)
+            joins = (None, j1, j2)
             full = input.shape[-2:]
-            s1, s2 = self.supervision1(cx1), self.supervision2(cx2)
+            s1, s2 = self.supervision1(cx1, join=j1), self.supervision2(cx2, join=j2)
             aux = [(s1, F.upsample_geometry(s1, size=full)), (s2, F.upsample_geometry(s2, size=full))]
-        result = self.feature_fusion_module(sx, F.cat([cx1, cx2]))
+        result = self.feature_fusion_module(sx, (cx1, cx2), joins)
         if self.with_interpolation:
             # reference: conv(up8(result)) (build_bisenet.py:165-167).  A 1x1 conv mixes channels
             # per pixel and bilinear resize mixes pixels per channel with weights summing to 1,

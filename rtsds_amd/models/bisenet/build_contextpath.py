@@ -13,7 +13,7 @@ import torch
 from torch import nn
 
 from rtsds_amd import functional as F
-from rtsds_amd.nn import BatchNorm2d, Conv2d, MaxPool2d, ReLU, conv_bn
+from rtsds_amd.nn import BatchNorm2d, Conv2d, MaxPool2d, ReLU, conv_bn, grad_join
 
 
 class BasicBlock(nn.Module):
@@ -30,12 +30,16 @@ class BasicBlock(nn.Module):
         self.stride = stride
 
     def forward(self, x):
+        # x has two readers (conv1 and the identity / downsample branch): their gradients meet
+        # in one buffer (the later producer's kernel accumulates) instead of an autograd add
+        join = grad_join(x, 2)
         skip = x
         if self.downsample is not None:
-            skip = conv_bn(self.downsample[0], self.downsample[1], x)
-        t = conv_bn(self.conv1, self.bn1, x, "relu")
+            skip = conv_bn(self.downsample[0], self.downsample[1], x, join=join)
+        t = conv_bn(self.conv1, self.bn1, x, "relu", join=join)
         # bn2 + residual add + ReLU in one pass
-        return conv_bn(self.conv2, self.bn2, t, "relu", skip)
+        return conv_bn(self.conv2, self.bn2, t, "relu", skip,
+                       res_join=join if self.downsample is None else None)
 
 
 class Bottleneck(nn.Module):
@@ -55,12 +59,14 @@ class Bottleneck(nn.Module):
         self.stride = stride
 
     def forward(self, x):
+        join = grad_join(x, 2)  # as BasicBlock
         skip = x
         if self.downsample is not None:
-            skip = conv_bn(self.downsample[0], self.downsample[1], x)
-        t = conv_bn(self.conv1, self.bn1, x, "relu")
+            skip = conv_bn(self.downsample[0], self.downsample[1], x, join=join)
+        t = conv_bn(self.conv1, self.bn1, x, "relu", join=join)
         t = conv_bn(self.conv2, self.bn2, t, "relu")
-        return conv_bn(self.conv3, self.bn3, t, "relu", skip)
+        return conv_bn(self.conv3, self.bn3, t, "relu", skip,
+                       res_join=join if self.downsample is None else None)
 
 
 class ResNet(nn.Module):

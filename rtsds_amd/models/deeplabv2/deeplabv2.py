@@ -11,7 +11,7 @@ import torch
 import torch.nn as nn
 
 from rtsds_amd import functional as F
-from rtsds_amd.nn import BatchNorm2d, Conv2d, MaxPool2d, ReLU, conv_bn, to_input
+from rtsds_amd.nn import BatchNorm2d, Conv2d, MaxPool2d, ReLU, conv_bn, grad_join, to_input
 from rtsds_amd.nn import _shadow
 
 affine_par = True
@@ -40,10 +40,13 @@ class Bottleneck(nn.Module):
         self.stride = stride
 
     def forward(self, x):
-        skip = x if self.downsample is None else conv_bn(self.downsample[0], self.downsample[1], x)
-        t = conv_bn(self.conv1, self.bn1, x, "relu")
+        # x's two readers accumulate their gradients into one buffer (nn.grad_join)
+        join = grad_join(x, 2)
+        skip = x if self.downsample is None else conv_bn(self.downsample[0], self.downsample[1], x, join=join)
+        t = conv_bn(self.conv1, self.bn1, x, "relu", join=join)
         t = conv_bn(self.conv2, self.bn2, t, "relu")
-        return conv_bn(self.conv3, self.bn3, t, "relu", skip)
+        return conv_bn(self.conv3, self.bn3, t, "relu", skip,
+                       res_join=join if self.downsample is None else None)
 
 
 class ClassifierModule(nn.Module):
