@@ -11,7 +11,7 @@ import numpy as np
 import torch
 
 from ._lib import ACT_SIGMOID, ConvDesc, lib
-from .runtime import CL, dcode, dp_world, empty_nhwc, nhwc, require_hip, stream, workspace
+from .runtime import CL, dcode, dp_world, empty_nhwc, nhwc, require_hip, side_enabled, side_fork, stream, workspace
 
 _P = lambda t: None if t is None else t.data_ptr()  # noqa: E731
 
@@ -147,6 +147,18 @@ class ConvFn(torch.autograd.Function):
         else:
             g = dy
         dx = dw = db = None
+        # weight gradient into the optimizer's arena: on the side stream, overlapping the
+        # data-gradient chain (runtime.side_fork); forked before the dgrad launch
+        wg_side = None
+        if ctx.needs_input_grad[1] and side_enabled(d.n * d.ho * d.wo) and CONV_PROFILE is None:
+            weight, bias = ctx.params
+            sinks = _sinks(weight, bias if ctx.needs_input_grad[2] else None)
+            if sinks is not None:
+                ws = workspace(lib.rtsds_conv2d_wgrad_workspace(ctypes.byref(d)), x.device)
+                side = side_fork(x, g, ws)
+                lib.rtsds_conv2d_wgrad(ctypes.byref(d), _P(x), _P(g), _P(sinks[0]), _P(sinks[1]), 1,
+                                       _P(ws), ws.numel(), side.cuda_stream)
+                wg_side = True
         if ctx.needs_input_grad[0]:
             join = ctx.join
             acc = join is not None and join.buf is not None  # accumulate onto the earlier contribution
@@ -157,7 +169,7 @@ class ConvFn(torch.autograd.Function):
                                        ws.numel(), stream())
             if join is not None:
                 dx = join.put(dx)
-        if ctx.needs_input_grad[1] or ctx.needs_input_grad[2]:
+        if (ctx.needs_input_grad[1] or ctx.needs_input_grad[2]) and not wg_side:
             weight, bias = ctx.params
             sinks = _sinks(weight, bias if ctx.needs_input_grad[2] else None) if ctx.needs_input_grad[1] else None
             ws = workspace(lib.rtsds_conv2d_wgrad_workspace(ctypes.byref(d)), x.device)

@@ -381,3 +381,48 @@ def test_graphed_step_equals_eager(da):
             states[-1]["_loss"] = core_out[0].float().cpu().clone()
     for k in states[0]:
         assert torch.equal(states[0][k], states[1][k]), k
+
+
+@pytest.mark.parametrize("da", [False, True])
+def test_side_stream_wgrad_equals_serial(da):
+    """Weight gradients on the side stream (runtime.side_fork, joined at the end of each
+    backward) leave parameters, optimizer state and BN buffers bit-identical to the serial
+    schedule after 3 iterations -- eager and hipGraph-replayed."""
+    from rtsds_amd import runtime
+    from rtsds_amd.runtime import GraphedStep
+
+    g = torch.Generator().manual_seed(7)
+    x = torch.randn(2, 3, 64, 128, generator=g).to(DEV)
+    xt = torch.randn(2, 3, 64, 128, generator=g).to(DEV)
+    y = torch.randint(0, 20, (2, 64, 128), generator=g).to(DEV)
+    ce, bce = losses.CrossEntropyLoss(ignore_index=19), losses.BCEWithLogitsLoss()
+    states = []
+    prev = runtime.side_enabled()
+    try:
+        with rtsds_amd.precision(torch.bfloat16):
+            for overlap, graphed in ((False, False), (True, False), (True, True)):
+                runtime.set_side_enabled(overlap)
+                torch.manual_seed(3)
+                net = BiSeNet(19, "resnet18").to(DEV).train()
+                disc = TinyDomainDiscriminator(19).to(DEV).train()
+                opt = optim.Adam(net.parameters(), lr=1e-3)
+                dopt = optim.Adam(disc.parameters(), lr=1e-3, weight_decay=1e-4)
+
+                def core():
+                    if da:
+                        return rtrain.da_step(net, disc, opt, dopt, ce, bce, x, y, xt, 0.1, 100)[0]
+                    return rtrain.seg_step(net, ce, opt, x, y)[0]
+
+                run = core
+                for i in range(3):
+                    if graphed and i == 1:
+                        run = GraphedStep(core, [opt, dopt] if da else [opt], warmup=0)
+                    run()
+                torch.cuda.synchronize()
+                states.append({k: v.detach().float().cpu().clone() for k, v in
+                               list(net.state_dict().items()) + list(disc.state_dict().items())})
+    finally:
+        runtime.set_side_enabled(prev)
+    for s in states[1:]:
+        for k in states[0]:
+            assert torch.equal(states[0][k], s[k]), k
