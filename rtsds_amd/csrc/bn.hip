@@ -68,7 +68,8 @@ RT_DEV void chan_merge(float& na, float& ma, float& Ma, float nb, float mb, floa
   na = n;
 }
 
-// Pass 1 (forward): part[(rb * c + ch) * 3 + {0,1,2}] = (count, mean, M2) of block rb.
+// Pass 1 (forward): part[(ch * RB + rb) * 3 + {0,1,2}] = (count, mean, M2) of block rb
+// (channel-major: the finalize reads one contiguous run per channel).
 template <typename T, int VEC>
 __global__ void __launch_bounds__(256) bn_stats_kernel(const T* __restrict__ x, float* __restrict__ part, long rows, int c) {
   __shared__ float sh[3][256][VEC];
@@ -120,62 +121,13 @@ __global__ void __launch_bounds__(256) bn_stats_kernel(const T* __restrict__ x, 
         chan_merge(n, m, M, sh[0][t][j], sh[1][t][j], sh[2][t][j]);
       }
       if (ch0 + j < c) {
-        float* o = part + ((long)blockIdx.x * c + ch0 + j) * 3;
+        float* o = part + ((long)(ch0 + j) * gridDim.x + blockIdx.x) * 3;
         o[0] = n; o[1] = m; o[2] = M;
       }
     }
   }
 }
 
-// Optional pre-merge when there are many row-block partials (the conv epilogue emits one per
-// 128-row M-tile): out[s][c][W] merges part[b][c][W] for b = s*4 + wave (+= 4*S).  Lanes run
-// across channels, so every wave-load is a contiguous 64-channel record run; loads of four
-// partials are issued before they are merged.  W = 3: (count, mean, M2) Chan merge;
-// W = 2: plain sums.  Fixed merge order -> deterministic.
-template <int W>
-RT_DEV void rec_merge(float* a, const float* b) {
-  if constexpr (W == 3) chan_merge(a[0], a[1], a[2], b[0], b[1], b[2]);
-  else { a[0] += b[0]; a[1] += b[1]; }
-}
-template <int W>
-__global__ void __launch_bounds__(256) bn_premerge_kernel(const float* __restrict__ part, int nrb, int c, float* __restrict__ out) {
-  __shared__ float red[4][64][W];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int ch = blockIdx.x * 64 + lane, S = gridDim.y, s = blockIdx.y;
-  float acc[W];
-#pragma unroll
-  for (int k = 0; k < W; ++k) acc[k] = 0.f;
-  if (ch < c) {
-    int b = s * 4 + w;
-    const int stride = 4 * S;
-    for (; b + 3 * stride < nrb; b += 4 * stride) {
-      float t[4][W];
-#pragma unroll
-      for (int u = 0; u < 4; ++u)
-#pragma unroll
-        for (int k = 0; k < W; ++k) t[u][k] = part[((long)(b + u * stride) * c + ch) * W + k];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) rec_merge<W>(acc, t[u]);
-    }
-    for (; b < nrb; b += stride) {
-      float t[W];
-#pragma unroll
-      for (int k = 0; k < W; ++k) t[k] = part[((long)b * c + ch) * W + k];
-      rec_merge<W>(acc, t);
-    }
-  }
-#pragma unroll
-  for (int k = 0; k < W; ++k) red[w][lane][k] = acc[k];
-  __syncthreads();
-  if (w == 0 && ch < c) {
-#pragma unroll
-    for (int q = 1; q < 4; ++q) rec_merge<W>(acc, red[q][lane]);
-#pragma unroll
-    for (int k = 0; k < W; ++k) out[((long)s * c + ch) * W + k] = acc[k];
-  }
-}
-static const int kBnMergeMax = 256;   // stage-2 partial count bound
-static int bn_premerge_s(int nrb) { return nrb <= kBnMergeMax ? 0 : std::min(kBnMergeMax, (nrb + 15) / 16); }
 
 // Pass 2 (forward): one wave per channel merges the row-block partials (Chan, lane-strided,
 // then a shuffle tree), updates running stats and emits scale/shift.
@@ -202,7 +154,7 @@ __global__ void __launch_bounds__(256) bn_finalize_kernel(const float* __restric
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       const int b = min(b0 + 256 * u, nrb - 1);
-      const float* p = part + ((long)b * c + ch) * 3;
+      const float* p = part + ((long)ch * nrb + b) * 3;
       const float n0 = p[0];  // clamped index: unconditional loads, zero count past nrb
       pn[u] = b0 + 256 * u < nrb ? n0 : 0.f;
       pm[u] = p[1];
@@ -352,7 +304,7 @@ RT_DEV void bn_bwd_coef(int ch0, int c, const float* gamma, const float* beta, c
   }
 }
 
-// Backward pass 1: part[(rb*c+ch)*2 + {0,1}] = (sum g, sum g*(x-mean)) with g = dy*act'(y).
+// Backward pass 1: part[(ch*RB+rb)*2 + {0,1}] = (sum g, sum g*(x-mean)) with g = dy*act'(y).
 template <typename T, int VEC>
 __global__ void __launch_bounds__(256) bn_bwd_stats_kernel(const T* __restrict__ dy, const T* __restrict__ x,
                                                             const T* __restrict__ y, const float* __restrict__ gamma,
@@ -431,7 +383,7 @@ __global__ void __launch_bounds__(256) bn_bwd_stats_kernel(const T* __restrict__
         const float a = (red[0][tid][j] + red[0][64 + tid][j]) + (red[0][128 + tid][j] + red[0][192 + tid][j]);
         const float b = (red[1][tid][j] + red[1][64 + tid][j]) + (red[1][128 + tid][j] + red[1][192 + tid][j]);
         if (ch0 + j < c) {
-          float* o = part + ((long)blockIdx.x * c + ch0 + j) * 2;
+          float* o = part + ((long)(ch0 + j) * gridDim.x + blockIdx.x) * 2;
           o[0] = a; o[1] = b;
         }
       }
@@ -450,7 +402,7 @@ __global__ void __launch_bounds__(256) bn_bwd_stats_kernel(const T* __restrict__
         b += red[1][gi * L.tpr + cv][j];
       }
       if (ch0 + j < c) {
-        float* o = part + ((long)blockIdx.x * c + ch0 + j) * 2;
+        float* o = part + ((long)(ch0 + j) * gridDim.x + blockIdx.x) * 2;
         o[0] = a; o[1] = b;
       }
     }
@@ -471,7 +423,7 @@ __global__ void __launch_bounds__(256) bn_bwd_finalize_kernel(const float* __res
     for (int u = 0; u < 8; ++u) {
       const int b = min(b0 + 256 * u, nrb - 1);
       const bool ok = b0 + 256 * u < nrb;
-      const float g = part[((long)b * c + ch) * 2], gx = part[((long)b * c + ch) * 2 + 1];
+      const float g = part[((long)ch * nrb + b) * 2], gx = part[((long)ch * nrb + b) * 2 + 1];
       pg[u] = ok ? g : 0.f;
       px[u] = ok ? gx : 0.f;
     }
@@ -578,34 +530,24 @@ static int bn_apply_rb(long rows, int c, int vec) {
 
 static size_t bn_part_floats(long rows, int c) { return (size_t)bn_rb(rows, c, 1) * c * 3; }
 
-// Workspace: [row-block partials | pre-merged partials | 8 coefficient arrays], each part
+// Workspace: [row-block partials | 8 coefficient arrays], each part
 // 256-B aligned (coefficient arrays are read with 16-B vector loads).
 static size_t al64f(size_t n) { return (n + 63) & ~(size_t)63; }
 struct BnWs {
-  float *part, *merged, *coef;
+  float *part, *coef;
 };
 static BnWs bn_ws(void* ws, long rows, int c) {
   BnWs w;
   w.part = (float*)ws;
-  w.merged = w.part + al64f(bn_part_floats(rows, c));
-  w.coef = w.merged + al64f((size_t)kBnMergeMax * c * 3);
+  w.coef = w.part + al64f(bn_part_floats(rows, c));
   return w;
 }
 extern "C" size_t rtsds_bn_workspace(long rows, int c) {
   if (rows <= 0 || c <= 0) return 256;
-  // partials (3 floats x RB x c; VEC=1 gives the most row blocks) + pre-merge + 8 x c
-  return (al64f(bn_part_floats(rows, c)) + al64f((size_t)kBnMergeMax * c * 3) + al64f((size_t)c * 8)) * 4 + 256;
+  // partials (3 floats x RB x c; VEC=1 gives the most row blocks) + 8 x c
+  return (al64f(bn_part_floats(rows, c)) + al64f((size_t)c * 8)) * 4 + 256;
 }
 
-// Merge nrb partials down to <= kBnMergeMax when needed; returns the (pointer, count) to finalize.
-template <int W>
-static const float* bn_premerge(const float* part, int& nrb, int c, float* merged, hipStream_t st) {
-  const int S = bn_premerge_s(nrb);
-  if (!S) return part;
-  hipLaunchKernelGGL(bn_premerge_kernel<W>, dim3(rt_cdiv(c, 64), S), dim3(256), 0, st, part, nrb, c, merged);
-  nrb = S;
-  return merged;
-}
 
 template <typename T, int VEC>
 static void bn_fwd_launch(const void* x, const void* res, void* y, long rows, int c, const float* gamma, const float* beta,

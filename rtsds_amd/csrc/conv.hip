@@ -37,7 +37,7 @@ struct ConvArgs {
   FastDiv f_tkw;
   int act;
   int accum;          // FWD/DGRAD: y += result
-  float* stats;       // FWD: per-M-tile BatchNorm partials [mtile][N][count, mean, M2] (or null)
+  float* stats;       // FWD: per-M-tile BatchNorm partials [N][mtile][count, mean, M2] (or null)
   long split_stride;  // elements between WGRAD split slabs
   // FWD eval-mode BatchNorm fold: y = act(acc * scale[co] + bias[co] (+ res)), scale/bias the
   // running-statistics BN folded with the conv bias (rtsds_bn_fold); res = residual, same
@@ -1028,7 +1028,7 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(const ConvArgs P0) {
         if (pass == 0) {
           mean[j] = tot / (float)nvalid;
         } else if (wmi == 0 && lane < 16 && n0 + col < P.N) {
-          float* o = P.stats + ((long)mt * P.N + n0 + col) * 3;
+          float* o = P.stats + ((long)(n0 + col) * gridDim.x + mt) * 3;  // [channel][M tile][3]
           o[0] = (float)nvalid;
           o[1] = mean[j];
           o[2] = tot;

@@ -181,7 +181,7 @@ __global__ void __launch_bounds__(256, 1) hconv_fwd_kernel(const HconvArgs P) {
         if (pass == 0) {
           mean[j] = tot / (float)(kTR * kTC);
         } else if (wave == 0 && lane < 16 && n < P.k) {
-          float* o = P.stats + ((long)bid * P.k + n) * 3;
+          float* o = P.stats + ((long)n * gridDim.x + bid) * 3;  // [channel][tile][3]
           o[0] = (float)(kTR * kTC);
           o[1] = mean[j];
           o[2] = tot;
