@@ -139,17 +139,21 @@ int rtsds_maxpool_fwd(const void* x, void* y, uint8_t* idx, int n, int h, int w,
 int rtsds_maxpool_bwd(const void* dy, const uint8_t* idx, void* dx, int n, int h, int w, int c,
                       int ho, int wo, int k, int s, int p, int dtype, void* stream);
 /* Global average pool over H*W (build_bisenet.py:46,75; build_contextpath.py:27-28;
- * model.py:63,82).  y: [n][c].                                                            */
-int rtsds_gap_fwd(const void* x, void* y, int n, long hw, int c, int dtype, void* stream);
+ * model.py:63,82).  y: [n][c].  ws: rtsds_gap_workspace(n, hw, c) bytes (row-slice
+ * partials of the two-stage reduction; also used by rtsds_chscale_bwd's da).              */
+size_t rtsds_gap_workspace(int n, long hw, int c);
+int rtsds_gap_fwd(const void* x, void* y, int n, long hw, int c, int dtype, void* ws, size_t ws_bytes,
+                  void* stream);
 int rtsds_gap_bwd(const void* dy, void* dx, int n, long hw, int c, int dtype, void* stream);
 
 /* ---------------------------------------------------------------- channel attention
  * mode 0: y = x*a[n][c] (build_bisenet.py:52,149); mode 1: y = x*a + x (build_bisenet.py:79-80).
- * Backward: dx (may be NULL), da[n][c] = sum_hw dy*x (may be NULL).                       */
+ * Backward: dx (may be NULL), da[n][c] = sum_hw dy*x (may be NULL; needs
+ * ws = rtsds_gap_workspace(n, hw, c) bytes).                                              */
 int rtsds_chscale_fwd(const void* x, const void* a, void* y, int n, long hw, int c, int mode,
                       int dtype, void* stream);
 int rtsds_chscale_bwd(const void* dy, const void* x, const void* a, void* dx, void* da, int n,
-                      long hw, int c, int mode, int dtype, void* stream);
+                      long hw, int c, int mode, int dtype, void* ws, size_t ws_bytes, void* stream);
 
 /* ---------------------------------------------------------------- bilinear resize
  * F.interpolate(mode='bilinear', align_corners=False) (build_bisenet.py:151-152,158-159,166;

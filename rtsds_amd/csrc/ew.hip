@@ -305,30 +305,55 @@ extern "C" int rtsds_maxpool_bwd(const void* dy, const uint8_t* idx, void* dx, i
 // y[img][c] = mean_hw x[img][hw][c]   (AdaptiveAvgPool2d(1) / torch.mean over H,W:
 // build_bisenet.py:46,75, build_contextpath.py:27-28, model.py:63,82).
 //
-// Shared per-image channel reduction: out[img][c] = scale * sum_hw a (* b if DOT).  A 1024-thread
-// block is laid out [row group][16-B channel vector] (VEC = 8 bf16 / 4 f32 when c allows, else
-// 1), so each iteration reads rpi whole rows coalesced; grid = (img, channel chunk).
+// Shared per-image channel reduction: out[img][c] = scale * sum_hw a (* b if DOT), in two
+// deterministic stages.  Stage 1: grid (S row slices, img, channel chunk) of 256-thread blocks
+// laid out [row group][16-B channel vector] (VEC = 8 bf16 / 4 f32 when c allows, else 1) ->
+// part[img][s][c] fp32.  Stage 2 sums the S slices in order.  (One block per image would
+// leave all but n CUs idle: the ARM / FFM / tail pools have n = 8 images.)
+static int chan_slices(int n, long hw) {
+  return (int)std::max<long>(1, std::min<long>(hw / 32, std::max(1, 1024 / std::max(1, n))));
+}
 template <typename T, int VEC, bool DOT>
-__global__ void __launch_bounds__(1024) chan_reduce_kernel(const T* __restrict__ a, const T* __restrict__ b, T* __restrict__ out,
-                                                           long hw, int c, float scale) {
-  __shared__ float red[1024 * VEC];
-  const int img = blockIdx.x;
-  const int cbase = blockIdx.y * 1024 * VEC;
-  const int cl = min(c - cbase, 1024 * VEC);
-  const int tpr = (cl + VEC - 1) / VEC, rpi = 1024 / tpr;
+__global__ void __launch_bounds__(256) chan_part_kernel(const T* __restrict__ a, const T* __restrict__ b, float* __restrict__ part,
+                                                        long hw, int c) {
+  __shared__ float red[256 * VEC];
+  const int s = blockIdx.x, S = gridDim.x, img = blockIdx.y;
+  const int cbase = blockIdx.z * 256 * VEC;
+  const int cl = min(c - cbase, 256 * VEC);
+  const int tpr = (cl + VEC - 1) / VEC, rpi = 256 / tpr;
   const int tid = threadIdx.x, cv = tid % tpr, rg = tid / tpr;
   const int ch0 = cbase + cv * VEC;
+  const long per = (hw + S - 1) / S, r0 = s * per, r1 = min(hw, r0 + per);
   float acc[VEC];
 #pragma unroll
   for (int j = 0; j < VEC; ++j) acc[j] = 0.f;
   if (rg < rpi) {
     const long base = (long)img * hw * c + ch0;
-    for (long r = rg; r < hw; r += rpi) {
+    long r = r0 + rg;
+    for (; r + rpi < r1; r += 2 * rpi) {  // two rows in flight
+      const long o0 = base + r * c, o1 = o0 + (long)rpi * c;
+      if (VEC > 1) {
+        typedef typename VecT<T>::v16 V16;
+        const V16 a0 = *(const V16*)(a + o0), a1 = *(const V16*)(a + o1);
+        if (DOT) {
+          const V16 b0 = *(const V16*)(b + o0), b1 = *(const V16*)(b + o1);
+#pragma unroll
+          for (int j = 0; j < VEC; ++j) acc[j] = fmaf(to_f(a1[j]), to_f(b1[j]), fmaf(to_f(a0[j]), to_f(b0[j]), acc[j]));
+        } else {
+#pragma unroll
+          for (int j = 0; j < VEC; ++j) acc[j] += to_f(a0[j]) + to_f(a1[j]);
+        }
+      } else {
+        acc[0] = DOT ? fmaf(to_f(a[o1]), to_f(b[o1]), fmaf(to_f(a[o0]), to_f(b[o0]), acc[0])) : acc[0] + (to_f(a[o0]) + to_f(a[o1]));
+      }
+    }
+    for (; r < r1; r += rpi) {
       const long o = base + r * c;
       if (VEC > 1) {
-        typename VecT<T>::v16 va = *(const typename VecT<T>::v16*)(a + o);
+        typedef typename VecT<T>::v16 V16;
+        const V16 va = *(const V16*)(a + o);
         if (DOT) {
-          typename VecT<T>::v16 vb = *(const typename VecT<T>::v16*)(b + o);
+          const V16 vb = *(const V16*)(b + o);
 #pragma unroll
           for (int j = 0; j < VEC; ++j) acc[j] = fmaf(to_f(va[j]), to_f(vb[j]), acc[j]);
         } else {
@@ -343,20 +368,45 @@ __global__ void __launch_bounds__(1024) chan_reduce_kernel(const T* __restrict__
 #pragma unroll
   for (int j = 0; j < VEC; ++j) red[tid * VEC + j] = acc[j];
   __syncthreads();
-  if (rg == 0) {
+  if (rg == 0 && cv * VEC < cl) {
     for (int g = 1; g < rpi; ++g)
 #pragma unroll
       for (int j = 0; j < VEC; ++j) acc[j] += red[(g * tpr + cv) * VEC + j];
 #pragma unroll
     for (int j = 0; j < VEC; ++j)
-      if (ch0 + j < c) out[(long)img * c + ch0 + j] = from_f<T>(acc[j] * scale);
+      if (ch0 + j < c) part[((long)img * S + s) * c + ch0 + j] = acc[j];
   }
 }
+template <typename T>
+__global__ void __launch_bounds__(256) chan_final_kernel(const float* __restrict__ part, T* __restrict__ out, int S, int c, float scale) {
+  const int img = blockIdx.y, ch = blockIdx.x * 256 + threadIdx.x;
+  if (ch >= c) return;
+  const float* p = part + (long)img * S * c + ch;
+  float s = 0.f;
+  int q = 0;
+  for (; q + 8 <= S; q += 8) {  // 8 slices in flight, summed in order
+    float t[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) t[u] = p[(long)(q + u) * c];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s += t[u];
+  }
+  for (; q < S; ++q) s += p[(long)q * c];
+  out[(long)img * c + ch] = from_f<T>(s * scale);
+}
+extern "C" size_t rtsds_gap_workspace(int n, long hw, int c) {
+  if (n <= 0 || hw <= 0 || c <= 0) return 256;
+  return (size_t)n * chan_slices(n, hw) * c * 4 + 256;
+}
 template <typename T, bool DOT>
-static void chan_reduce(const T* a, const T* b, T* out, int n, long hw, int c, float scale, hipStream_t st) {
+static void chan_reduce(const T* a, const T* b, T* out, int n, long hw, int c, float scale, float* part, hipStream_t st) {
   constexpr int V = VecT<T>::N;
-  if (c % V == 0) hipLaunchKernelGGL((chan_reduce_kernel<T, V, DOT>), dim3(n, rt_cdiv(c, 1024 * V)), dim3(1024), 0, st, a, b, out, hw, c, scale);
-  else hipLaunchKernelGGL((chan_reduce_kernel<T, 1, DOT>), dim3(n, rt_cdiv(c, 1024)), dim3(1024), 0, st, a, b, out, hw, c, scale);
+  const int S = chan_slices(n, hw);
+  if (c % V == 0)
+    hipLaunchKernelGGL((chan_part_kernel<T, V, DOT>), dim3(S, n, rt_cdiv(c, 256 * V)), dim3(256), 0, st, a, b, part, hw, c);
+  else
+    hipLaunchKernelGGL((chan_part_kernel<T, 1, DOT>), dim3(S, n, rt_cdiv(c, 256)), dim3(256), 0, st, a, b, part, hw, c);
+  hipLaunchKernelGGL(chan_final_kernel<T>, dim3(rt_cdiv(c, 256), n), dim3(256), 0, st, (const float*)part, out, S, c, scale);
 }
 template <typename T>
 __global__ void gap_bwd_kernel(const T* __restrict__ dy, T* __restrict__ dx, int n, long hw, int c) {
@@ -368,9 +418,10 @@ __global__ void gap_bwd_kernel(const T* __restrict__ dy, T* __restrict__ dx, int
     dx[i] = from_f<T>(to_f(dy[img * c + ch]) * inv);
   }
 }
-extern "C" int rtsds_gap_fwd(const void* x, void* y, int n, long hw, int c, int dtype, void* stream) {
+extern "C" int rtsds_gap_fwd(const void* x, void* y, int n, long hw, int c, int dtype, void* ws, size_t ws_bytes, void* stream) {
   if (n <= 0 || hw <= 0 || c <= 0) return RTSDS_ERR_SHAPE;
-  DISPATCH_T(dtype, (chan_reduce<T, false>((const T*)x, nullptr, (T*)y, n, hw, c, 1.f / (float)hw, (hipStream_t)stream)));
+  if (ws_bytes < rtsds_gap_workspace(n, hw, c)) return RTSDS_ERR_WORKSPACE;
+  DISPATCH_T(dtype, (chan_reduce<T, false>((const T*)x, nullptr, (T*)y, n, hw, c, 1.f / (float)hw, (float*)ws, (hipStream_t)stream)));
   RET_LAUNCH();
 }
 extern "C" int rtsds_gap_bwd(const void* dy, void* dx, int n, long hw, int c, int dtype, void* stream) {
@@ -409,13 +460,14 @@ extern "C" int rtsds_chscale_fwd(const void* x, const void* a, void* y, int n, l
   RET_LAUNCH();
 }
 extern "C" int rtsds_chscale_bwd(const void* dy, const void* x, const void* a, void* dx, void* da, int n, long hw, int c, int mode,
-                                 int dtype, void* stream) {
+                                 int dtype, void* ws, size_t ws_bytes, void* stream) {
   const long total = (long)n * hw * c;
   if (total <= 0) return RTSDS_ERR_SHAPE;
+  if (da && ws_bytes < rtsds_gap_workspace(n, hw, c)) return RTSDS_ERR_WORKSPACE;
   hipStream_t st = (hipStream_t)stream;
   DISPATCH_T(dtype, {
     if (dx) hipLaunchKernelGGL(chscale_bwd_dx_kernel<T>, dim3(ew_blocks(total)), dim3(256), 0, st, (const T*)dy, (const T*)a, (T*)dx, n, hw, c, mode);
-    if (da) chan_reduce<T, true>((const T*)dy, (const T*)x, (T*)da, n, hw, c, 1.f, st);
+    if (da) chan_reduce<T, true>((const T*)dy, (const T*)x, (T*)da, n, hw, c, 1.f, (float*)ws, st);
   });
   RET_LAUNCH();
 }

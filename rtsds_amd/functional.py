@@ -535,7 +535,8 @@ class GapFn(torch.autograd.Function):
         x = nhwc(x)
         n, c, h, w = x.shape
         y = empty_nhwc(n, c, 1, 1, x.dtype, x.device)
-        lib.rtsds_gap_fwd(_P(x), _P(y), n, h * w, c, dcode(x), stream())
+        ws = workspace(lib.rtsds_gap_workspace(n, h * w, c), x.device)
+        lib.rtsds_gap_fwd(_P(x), _P(y), n, h * w, c, dcode(x), _P(ws), ws.numel(), stream())
         ctx.shape = (n, c, h, w)
         return y
 
@@ -576,8 +577,9 @@ class ChScaleFn(torch.autograd.Function):
         dy = nhwc(dy)
         dx = torch.empty_like(x, memory_format=CL) if ctx.needs_input_grad[0] else None
         da = torch.empty_like(a) if ctx.needs_input_grad[1] else None
+        ws = workspace(lib.rtsds_gap_workspace(n, h * w, c) if da is not None else 0, x.device)
         lib.rtsds_chscale_bwd(_P(dy), _P(x), _P(a), _P(dx), _P(da), n, h * w, c, ctx.mode,
-                              dcode(x), stream())
+                              dcode(x), _P(ws), ws.numel(), stream())
         return dx, da, None
 
 

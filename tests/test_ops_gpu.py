@@ -302,6 +302,24 @@ def test_gap_chscale_cat_act(dt):
     _close(x2d.grad, x2r.grad, dt, "dx2", 1e-6 if dt == torch.float32 else 1e-2)
 
 
+@pytest.mark.parametrize("shape", [(8, 512, 16, 32), (8, 19, 64, 128), (3, 40, 33, 47)])
+def test_gap_chscale_row_slices(shape):
+    """Two-stage channel reductions (row-slice partials, ragged last slice, VEC 1 and 8):
+    global average pool and the channel-scale weight gradient sum_hw dy * x."""
+    g = torch.Generator().manual_seed(sum(shape))
+    x = torch.randn(*shape, generator=g, dtype=torch.float64).bfloat16().double()
+    a = torch.rand(shape[0], shape[1], 1, 1, generator=g, dtype=torch.float64).bfloat16().double()
+    xr, ar = x.clone().requires_grad_(), a.clone().requires_grad_()
+    yr = xr * ar
+    gy = torch.randn(yr.shape, generator=g, dtype=torch.float64).bfloat16().double()
+    yr.backward(gy)
+    xd, ad = _dev(x, torch.bfloat16).requires_grad_(), a.to(DEV, torch.bfloat16).requires_grad_()
+    y = F.channel_scale(xd, ad)
+    y.backward(_dev(gy, torch.bfloat16))
+    _close(ad.grad.reshape(ar.grad.shape), ar.grad, torch.bfloat16, "da", 1e-2)
+    _close(F.global_avg_pool(xd), x.mean((2, 3), keepdim=True), torch.bfloat16, "gap", 1e-2)
+
+
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 def test_softmax_ce_argmax(dt):
     g = torch.Generator().manual_seed(9)
