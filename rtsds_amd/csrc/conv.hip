@@ -1287,7 +1287,14 @@ static void pick_tile(long M, int N, bool b16, int& bm, int& bn) {
     if (N <= 32) { bn = 32; bm = blocks(256, 32) >= 256 ? 256 : 128; }
 #endif
     else if (N <= 64) { bn = 64; bm = blocks(128, 64) >= 256 ? 128 : 64; }
-    else if (blocks(128, 128) >= 256) { bm = 128; bn = 128; }
+#ifndef RTSDS_T128_MIN
+#define RTSDS_T128_MIN 512
+#endif
+#ifndef RTSDS_T12864_MIN
+#define RTSDS_T12864_MIN 384
+#endif
+    else if (blocks(128, 128) >= RTSDS_T128_MIN) { bm = 128; bn = 128; }
+    else if (blocks(128, 64) >= RTSDS_T12864_MIN) { bm = 128; bn = 64; }
     else { bm = 64; bn = 64; }
   } else {
     if (N <= 32) { bm = 128; bn = 32; } else { bm = 64; bn = 64; }
@@ -1699,7 +1706,7 @@ extern "C" int rtsds_conv2d_dgrad(const rtsds_conv_desc* d0, const void* dy, con
   }
   const int k_real = d.k;
   d.k = kp;
-  if (kp == 32 && hconv_dgrad_ok(d0)) {
+  if (kp % 32 == 0 && hconv_dgrad_ok(d0)) {
     // narrow-output 3x3 conv: halo direct conv over dY with the flipped, transposed weights
     repack_launch(d.dtype, w, wt, k_real, kp, d.kh, d.kw, d.c, d.kh, d.kw, d.kh - 1, d.kw - 1, -1, st);
     hconv_dgrad(d0, dy, kp, wt, dx, accumulate, st);

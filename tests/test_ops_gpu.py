@@ -56,6 +56,7 @@ CONV_CASES = [
     (8, 128, 64, 64, 128, 3, 1, 1, 1, False),  # 128x128 LDS-DMA tiles (fwd and dgrad)
     (2, 128, 8, 128, 19, 3, 1, 1, 1, False),   # halo direct conv (hconv.hip): Cout 19, w % 64 == 0
     (1, 64, 12, 64, 32, 3, 1, 1, 1, True),     # hconv with bias, Cout 32, edge tiles on 3 row-blocks
+    (1, 256, 8, 64, 64, 3, 1, 1, 1, True),     # hconv N-tiled (Cin >= 256, Cout 2 x 32), fwd and dgrad
     (2, 512, 32, 64, 19, 1, 1, 0, 1, True),    # supervision 1x1 (pw.hip backward): 1 row group
     (2, 40, 32, 64, 32, 1, 1, 0, 1, True),     # pw.hip: Cout 32, 12 row groups
     (4, 19, 32, 32, 19, 1, 1, 0, 1, True),     # pw.hip: final 19->19, odd Cin (scalar lanes)
@@ -561,7 +562,7 @@ def test_bisenet_eval_fold_and_graph(dt):
     assert torch.equal(rep1, fused) and torch.equal(rep2, eager2)
 
 
-@pytest.mark.parametrize("shape", [(2, 128, 8, 128, 19), (2, 64, 8, 64, 32), (2, 64, 6, 20, 19)])
+@pytest.mark.parametrize("shape", [(2, 128, 8, 128, 19), (2, 64, 8, 64, 32), (2, 64, 6, 20, 19), (2, 256, 8, 64, 64)])
 def test_conv_bn_stats_epilogue(shape):
     """Train-mode ConvBlock (conv -> BN with batch statistics from the conv epilogue -> ReLU):
     the GEMM epilogue and the halo direct conv (hconv.hip, w % 64 == 0) both against ATen."""
