@@ -1,6 +1,8 @@
 """Per-step HBM traffic by kernel from tools/pmc_bench.sh's two --pmc passes.
 
-Usage: pmc_traffic.py DIR STEPS [OUT.json]
+Usage: pmc_traffic.py DIR STEPS|auto [OUT.json]
+(auto: steps = dispatches of upce_fwd_kernel, which runs once per training step -- the
+bench's eager warm-up and GraphedStep warm-up iterations are profiled too)
 FETCH_SIZE and WRITE_SIZE are in KB per dispatch (rocprofv3); on gfx950 FETCH_SIZE reports
 half the bytes of wide (16 B/lane) streaming reads (MI355X_MICROARCH.md, HBM section), so
 fetch bytes = 2 x FETCH_SIZE x 1024.  WRITE_SIZE is exact for 16-B stores."""
@@ -32,7 +34,13 @@ def short(names):
 
 
 def main():
-    d, steps = sys.argv[1], float(sys.argv[2])
+    d = sys.argv[1]
+    if sys.argv[2] == "auto":
+        path = glob.glob(f"{d}/fetch/**/*counter_collection.csv", recursive=True)[0]
+        steps = float(len({r["Dispatch_Id"] for r in csv.DictReader(open(path))
+                           if "upce_fwd_kernel" in r["Kernel_Name"]}))
+    else:
+        steps = float(sys.argv[2])
     fetch, write = load(d + "/fetch", "FETCH_SIZE"), load(d + "/write", "WRITE_SIZE")
     names = sorted(set(fetch) | set(write))
     per = collections.defaultdict(lambda: [0.0, 0.0])
