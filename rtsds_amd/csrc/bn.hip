@@ -305,7 +305,8 @@ RT_DEV void bn_bwd_coef(int ch0, int c, const float* gamma, const float* beta, c
 }
 
 // Backward pass 1: part[(ch*RB+rb)*2 + {0,1}] = (sum g, sum g*(x-mean)) with g = dy*act'(y).
-template <typename T, int VEC>
+// HAS_Y: the activation mask comes from y (residual BNs); otherwise from x (no y registers).
+template <typename T, int VEC, bool HAS_Y>
 __global__ void __launch_bounds__(256) bn_bwd_stats_kernel(const T* __restrict__ dy, const T* __restrict__ x,
                                                             const T* __restrict__ y, const float* __restrict__ gamma,
                                                             const float* __restrict__ beta, const float* __restrict__ mean,
@@ -329,7 +330,7 @@ __global__ void __launch_bounds__(256) bn_bwd_stats_kernel(const T* __restrict__
 #endif
     constexpr int U = RTSDS_BN_U;  // rows in flight per thread (loads issued before any use)
     for (long r = (long)blockIdx.x * L.rpi + rg; r < rows; r += U * step) {
-      float g[U][VEC], xv[U][VEC], yv[U][VEC];
+      float g[U][VEC], xv[U][VEC], yv[HAS_Y ? U : 1][VEC];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         // clamped, unconditional loads (all U rows in flight together); rows past the end
@@ -337,7 +338,7 @@ __global__ void __launch_bounds__(256) bn_bwd_stats_kernel(const T* __restrict__
         const long rr = min(r + u * step, rows - 1);
         load_vec<T, VEC>(dy + rr * c + ch0, g[u], c - ch0);
         load_vec<T, VEC>(x + rr * c + ch0, xv[u], c - ch0);
-        if (y && act) load_vec<T, VEC>(y + rr * c + ch0, yv[u], c - ch0);
+        if constexpr (HAS_Y) load_vec<T, VEC>(y + rr * c + ch0, yv[u], c - ch0);
       }
 #pragma unroll
       for (int u = 0; u < U; ++u)
@@ -350,7 +351,8 @@ __global__ void __launch_bounds__(256) bn_bwd_stats_kernel(const T* __restrict__
         if (act) {
 #pragma unroll
           for (int j = 0; j < VEC; ++j)
-            g[u][j] *= y ? act_grad(yv[u][j], act) : (fmaf(xv[u][j], sc[j], sh[j]) > 0.f ? 1.f : (act == RTSDS_ACT_LEAKY ? 0.2f : 0.f));
+            g[u][j] *= HAS_Y ? act_grad(yv[HAS_Y ? u : 0][j], act)
+                             : (fmaf(xv[u][j], sc[j], sh[j]) > 0.f ? 1.f : (act == RTSDS_ACT_LEAKY ? 0.2f : 0.f));
         }
 #pragma unroll
         for (int j = 0; j < VEC; ++j) {
@@ -601,8 +603,12 @@ static void bn_bwd_launch(const void* dy, const void* x, const void* y, void* dx
                           int act, int accumulate, const BnWs& w, hipStream_t st) {
   int rb = bn_rb(rows, c, VEC);
   float* part = w.part;
-  hipLaunchKernelGGL((bn_bwd_stats_kernel<T, VEC>), dim3(rb, rt_cdiv(c, 256 * VEC)), dim3(256), 0, st, (const T*)dy, (const T*)x, (const T*)y, gamma, beta,
-                     smean, sinv, part, rows, c, act);
+  if (y && act)
+    hipLaunchKernelGGL((bn_bwd_stats_kernel<T, VEC, true>), dim3(rb, rt_cdiv(c, 256 * VEC)), dim3(256), 0, st, (const T*)dy, (const T*)x,
+                       (const T*)y, gamma, beta, smean, sinv, part, rows, c, act);
+  else
+    hipLaunchKernelGGL((bn_bwd_stats_kernel<T, VEC, false>), dim3(rb, rt_cdiv(c, 256 * VEC)), dim3(256), 0, st, (const T*)dy, (const T*)x,
+                       (const T*)y, gamma, beta, smean, sinv, part, rows, c, act);
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(c), dim3(256), 0, st, part, rb, c, rows, gamma, beta, smean, sinv,
                      dgamma, dbeta, w.coef, training, accumulate);
   if (dx || dres) {
