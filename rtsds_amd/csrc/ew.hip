@@ -9,6 +9,14 @@ static inline int ew_blocks(long work, int per_block = 256, int cap = 8192) {
   return (int)std::max<long>(1, std::min<long>(cap, (work + per_block - 1) / per_block));
 }
 #define GRID_STRIDE(i, n) for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < (n); i += (long)gridDim.x * blockDim.x)
+// XCD-aware variant: workgroups b and b + 8 run on one XCD, so logical block = the XCD's
+// contiguous run (bijective) -- neighbouring output rows (which share input rows) stay in one
+// XCD's L2.
+RT_DEV long xcd_block() {
+  const int nwg = gridDim.x, b = blockIdx.x, xcd = b & 7, q = nwg >> 3, r = nwg & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
+}
+#define GRID_STRIDE_XCD(i, n) for (long i = xcd_block() * (long)blockDim.x + threadIdx.x; i < (n); i += (long)gridDim.x * blockDim.x)
 #define DISPATCH_T(dtype, ...)                                \
   do {                                                        \
     if ((dtype) == RTSDS_BF16) { typedef bf16 T; __VA_ARGS__; } \
@@ -276,12 +284,120 @@ __global__ void maxpool_bwd_vec(const T* __restrict__ dy, const uint8_t* __restr
   }
 }
 
+// 3x3 windows (the ResNet stem pool, build_contextpath.py via torchvision resnet.py:
+// MaxPool2d(3, 2, 1)): all nine 16-B window loads issued unconditionally from clamped
+// coordinates before any compare (the generic loop's bounds branches serialised them), the
+// out-of-image taps masked afterwards in the same a-major order; the argmax bytes of a
+// channel vector leave as one 8-B store.
+template <typename T>
+__global__ void __launch_bounds__(256) maxpool_fwd_k3(const T* __restrict__ x, T* __restrict__ y, uint8_t* __restrict__ idx, int n,
+                                                     int h, int w, int c, int ho, int wo, int s, int p, FastDiv f_cv, FastDiv f_wo,
+                                                     FastDiv f_ho) {
+  typedef typename VecT<T>::v16 V16;
+  constexpr int V = VecT<T>::N;
+  const int cv = c / V;
+  const long total = (long)n * ho * wo * cv;  // < 2^31 (host-checked): 32-bit index math
+  GRID_STRIDE_XCD(i, total) {
+    const uint32_t ii = (uint32_t)i, q0 = fdiv(ii, f_cv), q1 = fdiv(q0, f_wo), img = fdiv(q1, f_ho);
+    const int ch = (int)(ii - q0 * cv) * V;
+    const int ow = (int)(q0 - q1 * wo), oh = (int)(q1 - img * ho);
+    const int h0 = oh * s - p, w0 = ow * s - p;
+    V16 v[9];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int hh = min(max(h0 + t / 3, 0), h - 1), ww = min(max(w0 + t % 3, 0), w - 1);
+      v[t] = *(const V16*)(x + (((long)img * h + hh) * w + ww) * c + ch);
+    }
+    float best[V];
+    int bi[V];
+#pragma unroll
+    for (int j = 0; j < V; ++j) { best[j] = -INFINITY; bi[j] = -1; }
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int hh = h0 + t / 3, ww = w0 + t % 3;
+      if ((unsigned)hh >= (unsigned)h || (unsigned)ww >= (unsigned)w) continue;
+#pragma unroll
+      for (int j = 0; j < V; ++j) {
+        const float f = to_f(v[t][j]);
+        if (bi[j] < 0 || f > best[j] || (f != f && best[j] == best[j])) { best[j] = f; bi[j] = t; }
+      }
+    }
+    V16 o;
+    const long oi = (((long)img * ho + oh) * wo + ow) * c + ch;
+    unsigned long long ib = 0;
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+      o[j] = from_f<T>(best[j]);
+      ib |= (unsigned long long)(bi[j] < 0 ? 0 : bi[j]) << (8 * j);
+    }
+    *(V16*)(y + oi) = o;
+    if constexpr (V == 8) {
+      *(unsigned long long*)(idx + oi) = ib;
+    } else {
+#pragma unroll
+      for (int j = 0; j < V; ++j) idx[oi + j] = (uint8_t)(ib >> (8 * j));
+    }
+  }
+}
+// Backward of the 3x3 stride-2 pool: an input pixel is covered by at most 2 x 2 windows; their
+// dY vectors and argmax bytes are loaded unconditionally (clamped), then matched.
+template <typename T>
+__global__ void __launch_bounds__(256) maxpool_bwd_k3s2(const T* __restrict__ dy, const uint8_t* __restrict__ idx, T* __restrict__ dx,
+                                                       int n, int h, int w, int c, int ho, int wo, int p, FastDiv f_cv, FastDiv f_w,
+                                                       FastDiv f_h) {
+  typedef typename VecT<T>::v16 V16;
+  constexpr int V = VecT<T>::N;
+  const int cv = c / V;
+  const long total = (long)n * h * w * cv;  // < 2^31 (host-checked)
+  GRID_STRIDE_XCD(i, total) {
+    const uint32_t ii = (uint32_t)i, q0 = fdiv(ii, f_cv), q1 = fdiv(q0, f_w), img = fdiv(q1, f_h);
+    const int ch = (int)(ii - q0 * cv) * V;
+    const int iw = (int)(q0 - q1 * w), ih = (int)(q1 - img * h);
+    const int oh_lo = max(0, (ih + p - 1) / 2), ow_lo = max(0, (iw + p - 1) / 2);  // (ih + p - k + s) / s
+    V16 g[4];
+    unsigned long long ib[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int oh = min(oh_lo + (t >> 1), ho - 1), ow = min(ow_lo + (t & 1), wo - 1);
+      const long o = (((long)img * ho + oh) * wo + ow) * c + ch;
+      g[t] = *(const V16*)(dy + o);
+      if constexpr (V == 8) {
+        ib[t] = *(const unsigned long long*)(idx + o);
+      } else {
+        ib[t] = 0;
+#pragma unroll
+        for (int j = 0; j < V; ++j) ib[t] |= (unsigned long long)idx[o + j] << (8 * j);
+      }
+    }
+    float acc[V];
+#pragma unroll
+    for (int j = 0; j < V; ++j) acc[j] = 0.f;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int oh = oh_lo + (t >> 1), ow = ow_lo + (t & 1);
+      const int a = ih - (oh * 2 - p), b = iw - (ow * 2 - p);
+      if (oh >= ho || ow >= wo || a < 0 || a >= 3 || b < 0 || b >= 3) continue;
+      const unsigned want = (unsigned)(a * 3 + b);
+#pragma unroll
+      for (int j = 0; j < V; ++j)
+        if (((ib[t] >> (8 * j)) & 0xff) == want) acc[j] += to_f(g[t][j]);
+    }
+    V16 r;
+#pragma unroll
+    for (int j = 0; j < V; ++j) r[j] = from_f<T>(acc[j]);
+    *(V16*)(dx + (((long)img * h + ih) * w + iw) * c + ch) = r;
+  }
+}
+
 extern "C" int rtsds_maxpool_fwd(const void* x, void* y, uint8_t* idx, int n, int h, int w, int c, int ho, int wo, int k, int s,
                                  int p, int dtype, void* stream) {
   if (k * k > 255 || n <= 0 || ho <= 0 || wo <= 0) return RTSDS_ERR_SHAPE;
   const long total = (long)n * ho * wo * c;
   DISPATCH_T(dtype, {
-    if (c % VecT<T>::N == 0)
+    if (c % VecT<T>::N == 0 && k == 3 && total < (1L << 31))
+      hipLaunchKernelGGL(maxpool_fwd_k3<T>, dim3(ew_blocks(total / VecT<T>::N, 256, 1 << 20)), dim3(256), 0, (hipStream_t)stream, (const T*)x, (T*)y, idx,
+                         n, h, w, c, ho, wo, s, p, fastdiv_make(c / VecT<T>::N), fastdiv_make(wo), fastdiv_make(ho));
+    else if (c % VecT<T>::N == 0)
       hipLaunchKernelGGL(maxpool_fwd_vec<T>, dim3(ew_blocks(total / VecT<T>::N)), dim3(256), 0, (hipStream_t)stream, (const T*)x, (T*)y, idx, n, h, w, c, ho, wo, k, s, p);
     else
       hipLaunchKernelGGL(maxpool_fwd_kernel<T>, dim3(ew_blocks(total)), dim3(256), 0, (hipStream_t)stream, (const T*)x, (T*)y, idx, n, h, w, c, ho, wo, k, s, p);
@@ -293,7 +409,10 @@ extern "C" int rtsds_maxpool_bwd(const void* dy, const uint8_t* idx, void* dx, i
   const long total = (long)n * h * w * c;
   if (total <= 0) return RTSDS_ERR_SHAPE;
   DISPATCH_T(dtype, {
-    if (c % VecT<T>::N == 0)
+    if (c % VecT<T>::N == 0 && k == 3 && s == 2 && total < (1L << 31))
+      hipLaunchKernelGGL(maxpool_bwd_k3s2<T>, dim3(ew_blocks(total / VecT<T>::N, 256, 1 << 20)), dim3(256), 0, (hipStream_t)stream, (const T*)dy, idx, (T*)dx,
+                         n, h, w, c, ho, wo, p, fastdiv_make(c / VecT<T>::N), fastdiv_make(w), fastdiv_make(h));
+    else if (c % VecT<T>::N == 0)
       hipLaunchKernelGGL(maxpool_bwd_vec<T>, dim3(ew_blocks(total / VecT<T>::N)), dim3(256), 0, (hipStream_t)stream, (const T*)dy, idx, (T*)dx, n, h, w, c, ho, wo, k, s, p);
     else
       hipLaunchKernelGGL(maxpool_bwd_kernel<T>, dim3(ew_blocks(total)), dim3(256), 0, (hipStream_t)stream, (const T*)dy, idx, (T*)dx, n, h, w, c, ho, wo, k, s, p);

@@ -243,11 +243,16 @@ def test_batchnorm_module_counter():
 
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("geo", [(3, 2, 1, False, 17, 23), (3, 2, 1, True, 17, 23), (3, 2, 1, True, 16, 16)])
+@pytest.mark.parametrize("geo", [(3, 2, 1, False, 17, 23), (3, 2, 1, True, 17, 23), (3, 2, 1, True, 16, 16),
+                                 (3, 2, 1, False, 32, 64, "relu"), (3, 1, 1, False, 9, 12), (2, 2, 0, False, 8, 10)])
 def test_maxpool(geo, dt):
-    k, s, p, ceil, h, w = geo
+    """Incl. post-ReLU input (ties at 0: the first maximum in window order wins, as ATen)
+    and the generic (non 3x3 / stride-2) kernels."""
+    k, s, p, ceil, h, w = geo[:6]
     g = torch.Generator().manual_seed(1)
     x = torch.randn(2, 8, h, w, generator=g, dtype=torch.float64)
+    if len(geo) > 6:
+        x = x.clamp_min(0)
     if dt == torch.bfloat16:
         x = x.bfloat16().double()
     xr = x.clone().requires_grad_()
