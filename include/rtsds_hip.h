@@ -113,6 +113,25 @@ int rtsds_bn_bwd(const void* dy, const void* x, const void* y, void* dx, void* d
                  const float* beta, const float* save_mean, const float* save_invstd, int training, int act,
                  int accumulate_params, int dtype, void* ws, size_t ws_bytes, void* stream);
 
+/* BatchNorm2d + ReLU + MaxPool2d(3, 2, p in {0,1}) fused -- the ResNet stem bn1 -> relu ->
+ * maxpool (build_contextpath.py:15-18 via torchvision resnet.py; deeplabv2.py:106-110, ceil
+ * mode via ho / wo).  bf16, c % 8 == 0.  x: the conv output [n][h][w][c]; y: pooled
+ * [n][ho][wo][c]; idx: window argmax 0..8 per output element (first maximum in window order,
+ * as ATen).  Statistics, running buffers and workspace as rtsds_bn_fwd (rows = n*h*w).  The
+ * backward gathers dy_pool through idx inside the BatchNorm backward passes: dx = d(bn+relu)
+ * of the pooled gradient; dgamma / dbeta as rtsds_bn_bwd.                                  */
+int rtsds_bn_relu_maxpool_fwd(const void* x, void* y, uint8_t* idx, int n, int h, int w, int c, int ho, int wo,
+                              int p, const float* gamma, const float* beta, float* running_mean,
+                              float* running_var, long long* num_batches_tracked, float* save_mean,
+                              float* save_invstd, float momentum, float eps, int training,
+                              const float* stats_part, int stats_nrb, int dtype, void* ws, size_t ws_bytes,
+                              void* stream);
+int rtsds_bn_relu_maxpool_bwd(const void* dy_pool, const uint8_t* idx, const void* x, void* dx, float* dgamma,
+                              float* dbeta, int n, int h, int w, int c, int ho, int wo, int p,
+                              const float* gamma, const float* beta, const float* save_mean,
+                              const float* save_invstd, int training, int accumulate_params, int dtype,
+                              void* ws, size_t ws_bytes, void* stream);
+
 /* ---------------------------------------------------------------- layout / dtype
  * Input images arrive NCHW fp32 from the reference's loaders (datasets/cityscapes.py:62,
  * main.py:69-72).  cast: weight shadows (fp32 master -> bf16) and dtype round trips.

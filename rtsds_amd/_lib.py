@@ -45,6 +45,10 @@ SIGNATURES = {
     "rtsds_bn_fold": (c_int, [P, P, P, P, P, c_float, c_int, P, P, P]),
     "rtsds_bn_bwd": (c_int, [P, P, P, P, P, P, P, c_long, c_int, P, P, P, P, c_int, c_int, c_int, c_int,
                              P, c_size_t, P]),
+    "rtsds_bn_relu_maxpool_fwd": (c_int, [P, P, P] + [c_int] * 7 + [P, P, P, P, P, P, P, c_float, c_float, c_int, P,
+                                                                   c_int, c_int, P, c_size_t, P]),
+    "rtsds_bn_relu_maxpool_bwd": (c_int, [P, P, P, P, P, P] + [c_int] * 7 + [P, P, P, P, c_int, c_int, c_int, P,
+                                                                            c_size_t, P]),
     "rtsds_nchw_to_nhwc": (c_int, [P, P, c_int, c_int, c_int, c_int, c_int, P]),
     "rtsds_cast": (c_int, [P, c_int, P, c_int, c_long, P]),
     "rtsds_copy_channels": (c_int, [P, c_int, c_int, P, c_int, c_int, c_long, c_int, c_int, c_int, P]),

@@ -293,6 +293,53 @@ RT_DEV void bn_act_grad(float* g, const T* y, const float* xv, const float* sc, 
   }
 }
 
+// Where the backward passes read g (before the activation mask): the stored dY, or -- for a
+// BatchNorm + ReLU feeding a 3x3 stride-2 max pool (the ResNet stem, fused forward in
+// bn_relu_pool_fwd_kernel) -- a gather of the pooled gradient: input pixel r of channel vector
+// ch0 receives dY_pool[o] from each of the <= 2 x 2 windows o covering it whose argmax byte
+// names r.  The dY of the BatchNorm never exists in memory.
+template <typename T>
+struct GradDirect {
+  const T* dy;
+  int c;
+  template <int VEC> RT_DEV void load(long r, int ch0, float* g, int cvalid) const { load_vec<T, VEC>(dy + r * c + ch0, g, cvalid); }
+};
+template <typename T>
+struct GradPool {
+  const T* dyp;
+  const uint8_t* idx;
+  int c, h, w, ho, wo, p;
+  FastDiv f_w, f_h;
+  template <int VEC> RT_DEV void load(long r, int ch0, float* g, int cvalid) const {
+    static_assert(VEC == 8 && sizeof(T) == 2, "pooled gradient source: bf16 vectors of 8 channels");
+    typedef typename VecT<T>::v16 V16;
+    const uint32_t q = fdiv((uint32_t)r, f_w), img = fdiv(q, f_h);
+    const int iw = (int)((uint32_t)r - q * w), ih = (int)(q - img * h);
+    const int oh_lo = max(0, (ih + p - 1) / 2), ow_lo = max(0, (iw + p - 1) / 2);
+    V16 gv[4];
+    unsigned long long ib[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {  // clamped, unconditional (all in flight together)
+      const int oh = min(oh_lo + (t >> 1), ho - 1), ow = min(ow_lo + (t & 1), wo - 1);
+      const long o = (((long)img * ho + oh) * wo + ow) * c + ch0;
+      gv[t] = *(const V16*)(dyp + o);
+      ib[t] = *(const unsigned long long*)(idx + o);
+    }
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) g[j] = 0.f;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int oh = oh_lo + (t >> 1), ow = ow_lo + (t & 1);
+      const int a = ih - (oh * 2 - p), b = iw - (ow * 2 - p);
+      if (oh >= ho || ow >= wo || a < 0 || a >= 3 || b < 0 || b >= 3) continue;
+      const unsigned want = (unsigned)(a * 3 + b);
+#pragma unroll
+      for (int j = 0; j < VEC; ++j)
+        if (((ib[t] >> (8 * j)) & 0xff) == want) g[j] += to_f(gv[t][j]);
+    }
+  }
+};
+
 template <int VEC>
 RT_DEV void bn_bwd_coef(int ch0, int c, const float* gamma, const float* beta, const float* mean, const float* sinv,
                         float* mu, float* sc, float* sh) {
@@ -306,8 +353,8 @@ RT_DEV void bn_bwd_coef(int ch0, int c, const float* gamma, const float* beta, c
 
 // Backward pass 1: part[(ch*RB+rb)*2 + {0,1}] = (sum g, sum g*(x-mean)) with g = dy*act'(y).
 // HAS_Y: the activation mask comes from y (residual BNs); otherwise from x (no y registers).
-template <typename T, int VEC, bool HAS_Y>
-__global__ void __launch_bounds__(256) bn_bwd_stats_kernel(const T* __restrict__ dy, const T* __restrict__ x,
+template <typename T, int VEC, bool HAS_Y, class GS>
+__global__ void __launch_bounds__(256) bn_bwd_stats_kernel(const GS gs, const T* __restrict__ x,
                                                             const T* __restrict__ y, const float* __restrict__ gamma,
                                                             const float* __restrict__ beta, const float* __restrict__ mean,
                                                             const float* __restrict__ sinv, float* __restrict__ part,
@@ -336,7 +383,7 @@ __global__ void __launch_bounds__(256) bn_bwd_stats_kernel(const T* __restrict__
         // clamped, unconditional loads (all U rows in flight together); rows past the end
         // contribute g = 0
         const long rr = min(r + u * step, rows - 1);
-        load_vec<T, VEC>(dy + rr * c + ch0, g[u], c - ch0);
+        gs.template load<VEC>(rr, ch0, g[u], c - ch0);
         load_vec<T, VEC>(x + rr * c + ch0, xv[u], c - ch0);
         if constexpr (HAS_Y) load_vec<T, VEC>(y + rr * c + ch0, yv[u], c - ch0);
       }
@@ -452,8 +499,8 @@ __global__ void __launch_bounds__(256) bn_bwd_finalize_kernel(const float* __res
 }
 
 // Backward pass 3: dx = A*g + B*(x - mean) + C;  dres = g.  Layout as bn_apply_kernel.
-template <typename T, int VEC>
-__global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const T* __restrict__ dy, const T* __restrict__ x,
+template <typename T, int VEC, class GS>
+__global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const GS gs, const T* __restrict__ x,
                                                             const T* __restrict__ y, T* __restrict__ dx, T* __restrict__ dres,
                                                             const float* __restrict__ coef, long rows, int c, int act) {
   const int cbase = blockIdx.y * 256 * VEC;
@@ -476,9 +523,9 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const T* __restrict__
   for (; r + step < rows; r += 2 * step) {  // two independent rows in flight per thread
     const long o0 = r * c + ch0, o1 = o0 + step * c;
     float g0[VEC], x0[VEC], g1[VEC], x1[VEC];
-    load_vec<T, VEC>(dy + o0, g0, cvalid);
+    gs.template load<VEC>(r, ch0, g0, cvalid);
     load_vec<T, VEC>(x + o0, x0, cvalid);
-    load_vec<T, VEC>(dy + o1, g1, cvalid);
+    gs.template load<VEC>(r + step, ch0, g1, cvalid);
     load_vec<T, VEC>(x + o1, x1, cvalid);
     bn_act_grad<T, VEC>(g0, y ? y + o0 : nullptr, x0, sc, sh, act, cvalid);
     bn_act_grad<T, VEC>(g1, y ? y + o1 : nullptr, x1, sc, sh, act, cvalid);
@@ -499,7 +546,7 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const T* __restrict__
   if (r < rows) {
     const long off = r * c + ch0;
     float g[VEC], xv[VEC];
-    load_vec<T, VEC>(dy + off, g, cvalid);
+    gs.template load<VEC>(r, ch0, g, cvalid);
     load_vec<T, VEC>(x + off, xv, cvalid);
     bn_act_grad<T, VEC>(g, y ? y + off : nullptr, xv, sc, sh, act, cvalid);
 #pragma unroll
@@ -597,24 +644,32 @@ extern "C" int rtsds_bn_fwd(const void* x, const void* res, void* y, long rows, 
   return hipGetLastError() == hipSuccess ? RTSDS_OK : RTSDS_ERR_LAUNCH;
 }
 
-template <typename T, int VEC>
-static void bn_bwd_launch(const void* dy, const void* x, const void* y, void* dx, void* dres, float* dgamma, float* dbeta,
+template <typename T, int VEC, class GS>
+static void bn_bwd_launch(const GS& gs, const void* x, const void* y, void* dx, void* dres, float* dgamma, float* dbeta,
                           long rows, int c, const float* gamma, const float* beta, const float* smean, const float* sinv, int training,
                           int act, int accumulate, const BnWs& w, hipStream_t st) {
   int rb = bn_rb(rows, c, VEC);
   float* part = w.part;
   if (y && act)
-    hipLaunchKernelGGL((bn_bwd_stats_kernel<T, VEC, true>), dim3(rb, rt_cdiv(c, 256 * VEC)), dim3(256), 0, st, (const T*)dy, (const T*)x,
+    hipLaunchKernelGGL((bn_bwd_stats_kernel<T, VEC, true, GS>), dim3(rb, rt_cdiv(c, 256 * VEC)), dim3(256), 0, st, gs, (const T*)x,
                        (const T*)y, gamma, beta, smean, sinv, part, rows, c, act);
   else
-    hipLaunchKernelGGL((bn_bwd_stats_kernel<T, VEC, false>), dim3(rb, rt_cdiv(c, 256 * VEC)), dim3(256), 0, st, (const T*)dy, (const T*)x,
+    hipLaunchKernelGGL((bn_bwd_stats_kernel<T, VEC, false, GS>), dim3(rb, rt_cdiv(c, 256 * VEC)), dim3(256), 0, st, gs, (const T*)x,
                        (const T*)y, gamma, beta, smean, sinv, part, rows, c, act);
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(c), dim3(256), 0, st, part, rb, c, rows, gamma, beta, smean, sinv,
                      dgamma, dbeta, w.coef, training, accumulate);
   if (dx || dres) {
-    hipLaunchKernelGGL((bn_bwd_apply_kernel<T, VEC>), dim3(bn_apply_rb(rows, c, VEC), rt_cdiv(c, 256 * VEC)), dim3(256), 0, st,
-                       (const T*)dy, (const T*)x, (const T*)y, (T*)dx, (T*)dres, w.coef, rows, c, act);
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<T, VEC, GS>), dim3(bn_apply_rb(rows, c, VEC), rt_cdiv(c, 256 * VEC)), dim3(256), 0, st,
+                       gs, (const T*)x, (const T*)y, (T*)dx, (T*)dres, w.coef, rows, c, act);
   }
+}
+template <typename T, int VEC>
+static void bn_bwd_launch(const void* dy, const void* x, const void* y, void* dx, void* dres, float* dgamma, float* dbeta,
+                          long rows, int c, const float* gamma, const float* beta, const float* smean, const float* sinv, int training,
+                          int act, int accumulate, const BnWs& w, hipStream_t st) {
+  const GradDirect<T> gs{(const T*)dy, c};
+  bn_bwd_launch<T, VEC, GradDirect<T>>(gs, x, y, dx, dres, dgamma, dbeta, rows, c, gamma, beta, smean, sinv, training, act,
+                                       accumulate, w, st);
 }
 
 extern "C" int rtsds_bn_bwd(const void* dy, const void* x, const void* y, void* dx, void* dres, float* dgamma, float* dbeta,
@@ -634,6 +689,116 @@ extern "C" int rtsds_bn_bwd(const void* dy, const void* x, const void* y, void* 
     if (c % 4 == 0) bn_bwd_launch<float, 4>(dy, x, y, dx, dres, dgamma, dbeta, rows, c, gamma, beta, save_mean, save_invstd, training, act, accumulate_params, w, st);
     else bn_bwd_launch<float, 1>(dy, x, y, dx, dres, dgamma, dbeta, rows, c, gamma, beta, save_mean, save_invstd, training, act, accumulate_params, w, st);
   } else return RTSDS_ERR_UNSUPPORTED;
+  return hipGetLastError() == hipSuccess ? RTSDS_OK : RTSDS_ERR_LAUNCH;
+}
+
+// ---- BatchNorm + ReLU + MaxPool2d(3, 2, p) (the ResNet stem: bn1 -> relu -> maxpool,
+// build_contextpath.py:15-18 / torchvision resnet.py; deeplabv2.py:106-110 with ceil mode).
+// Forward: the pool reads the conv output and applies the BatchNorm scale / shift + ReLU to
+// each window value (rounded to the storage dtype, exactly the value the separate bn_apply
+// would have stored), so the full-resolution activation is never written; the window argmax
+// bytes are stored for the backward, which gathers the pooled gradient inside the BatchNorm
+// backward passes (GradPool) -- the full-resolution gradient is never written either.
+template <typename T>
+__global__ void __launch_bounds__(256) bn_relu_pool_fwd_kernel(const T* __restrict__ x, const float* __restrict__ scale,
+                                                              const float* __restrict__ shift, T* __restrict__ y,
+                                                              uint8_t* __restrict__ idx, int h, int w, int c, int ho, int wo, int p,
+                                                              long total, FastDiv f_cv, FastDiv f_wo, FastDiv f_ho) {
+  typedef typename VecT<T>::v16 V16;
+  constexpr int V = VecT<T>::N;
+  const int cv = c / V;
+  const int nwg = gridDim.x, bx = blockIdx.x, xcd = bx & 7, qq = nwg >> 3, rr = nwg & 7;  // XCD-contiguous blocks
+  const long lb = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (bx >> 3);
+  for (long i = lb * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const uint32_t ii = (uint32_t)i, q0 = fdiv(ii, f_cv), q1 = fdiv(q0, f_wo), img = fdiv(q1, f_ho);
+    const int ch = (int)(ii - q0 * cv) * V;
+    const int ow = (int)(q0 - q1 * wo), oh = (int)(q1 - img * ho);
+    const int h0 = oh * 2 - p, w0 = ow * 2 - p;
+    V16 v[9];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int hh = min(max(h0 + t / 3, 0), h - 1), ww = min(max(w0 + t % 3, 0), w - 1);
+      v[t] = *(const V16*)(x + (((long)img * h + hh) * w + ww) * c + ch);
+    }
+    float sc[V], sh[V];
+    load_coef<V>(scale, ch, c, sc);
+    load_coef<V>(shift, ch, c, sh);
+    float best[V];
+    int bi[V];
+#pragma unroll
+    for (int j = 0; j < V; ++j) { best[j] = -INFINITY; bi[j] = -1; }
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int hh = h0 + t / 3, ww = w0 + t % 3;
+      if ((unsigned)hh >= (unsigned)h || (unsigned)ww >= (unsigned)w) continue;
+#pragma unroll
+      for (int j = 0; j < V; ++j) {
+        const float f = to_f(from_f<T>(fmaxf(fmaf(to_f(v[t][j]), sc[j], sh[j]), 0.f)));
+        if (bi[j] < 0 || f > best[j] || (f != f && best[j] == best[j])) { best[j] = f; bi[j] = t; }
+      }
+    }
+    V16 o;
+    const long oi = (((long)img * ho + oh) * wo + ow) * c + ch;
+    unsigned long long ib = 0;
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+      o[j] = from_f<T>(best[j]);
+      ib |= (unsigned long long)(bi[j] < 0 ? 0 : bi[j]) << (8 * j);
+    }
+    *(V16*)(y + oi) = o;
+    *(unsigned long long*)(idx + oi) = ib;
+  }
+}
+static bool bn_pool_ok(int n, int h, int w, int c, int ho, int wo, int p, int dtype) {
+  return dtype == RTSDS_BF16 && c % 8 == 0 && n > 0 && ho > 0 && wo > 0 && (p == 0 || p == 1) &&
+         (long)n * h * w * c < (1L << 31) && (long)n * ho * wo * c < (1L << 31);
+}
+extern "C" int rtsds_bn_relu_maxpool_fwd(const void* x, void* y, uint8_t* idx, int n, int h, int w, int c, int ho, int wo, int p,
+                                         const float* gamma, const float* beta, float* running_mean, float* running_var,
+                                         long long* num_batches_tracked, float* save_mean, float* save_invstd, float momentum,
+                                         float eps, int training, const float* stats_part, int stats_nrb, int dtype, void* ws,
+                                         size_t ws_bytes, void* stream) {
+  const long rows = (long)n * h * w;
+  if (!bn_pool_ok(n, h, w, c, ho, wo, p, dtype)) return RTSDS_ERR_UNSUPPORTED;
+  if (ws_bytes < rtsds_bn_workspace(rows, c)) return RTSDS_ERR_WORKSPACE;
+  if (!training && (!running_mean || !running_var)) return RTSDS_ERR_UNSUPPORTED;
+  if (training && (!save_mean || !save_invstd)) return RTSDS_ERR_UNSUPPORTED;
+  hipStream_t st = (hipStream_t)stream;
+  const BnWs wsb = bn_ws(ws, rows, c);
+  float* scale = wsb.coef;
+  float* shift = wsb.coef + c;
+  long long* nbt = training ? num_batches_tracked : nullptr;
+  if (training) {
+    int rb = stats_nrb;
+    const float* part = stats_part;
+    if (!part) {
+      rb = bn_rb(rows, c, 8);
+      hipLaunchKernelGGL((bn_stats_kernel<bf16, 8>), dim3(rb, rt_cdiv(c, 256 * 8)), dim3(256), 0, st, (const bf16*)x, wsb.part, rows, c);
+      part = wsb.part;
+    }
+    hipLaunchKernelGGL(bn_finalize_kernel, dim3(c), dim3(256), 0, st, part, rb, c, rows, gamma, beta, running_mean, running_var,
+                       save_mean, save_invstd, scale, shift, momentum, eps, nbt);
+  } else {
+    hipLaunchKernelGGL(bn_eval_coef_kernel, dim3(rt_cdiv(c, 256)), dim3(256), 0, st, c, gamma, beta, running_mean, running_var,
+                       scale, shift, save_mean, save_invstd, eps);
+  }
+  const long total = (long)n * ho * wo * (c / 8);
+  const int blocks = (int)std::max<long>(1, std::min<long>((total + 255) / 256, 1L << 20));
+  hipLaunchKernelGGL(bn_relu_pool_fwd_kernel<bf16>, dim3(blocks), dim3(256), 0, st, (const bf16*)x, (const float*)scale,
+                     (const float*)shift, (bf16*)y, idx, h, w, c, ho, wo, p, total, fastdiv_make(c / 8), fastdiv_make(wo),
+                     fastdiv_make(ho));
+  return hipGetLastError() == hipSuccess ? RTSDS_OK : RTSDS_ERR_LAUNCH;
+}
+extern "C" int rtsds_bn_relu_maxpool_bwd(const void* dy_pool, const uint8_t* idx, const void* x, void* dx, float* dgamma,
+                                         float* dbeta, int n, int h, int w, int c, int ho, int wo, int p, const float* gamma,
+                                         const float* beta, const float* save_mean, const float* save_invstd, int training,
+                                         int accumulate_params, int dtype, void* ws, size_t ws_bytes, void* stream) {
+  const long rows = (long)n * h * w;
+  if (!bn_pool_ok(n, h, w, c, ho, wo, p, dtype)) return RTSDS_ERR_UNSUPPORTED;
+  if (ws_bytes < rtsds_bn_workspace(rows, c)) return RTSDS_ERR_WORKSPACE;
+  const GradPool<bf16> gs{(const bf16*)dy_pool, idx, c, h, w, ho, wo, p, fastdiv_make(w), fastdiv_make(h)};
+  bn_bwd_launch<bf16, 8, GradPool<bf16>>(gs, x, nullptr, dx, nullptr, dgamma, dbeta, rows, c, gamma, beta, save_mean, save_invstd,
+                                         training, RTSDS_ACT_RELU, accumulate_params, bn_ws(ws, rows, c), (hipStream_t)stream);
   return hipGetLastError() == hipSuccess ? RTSDS_OK : RTSDS_ERR_LAUNCH;
 }
 

@@ -13,7 +13,7 @@ import torch
 from torch import nn
 
 from rtsds_amd import functional as F
-from rtsds_amd.nn import BatchNorm2d, Conv2d, MaxPool2d, ReLU, conv_bn, grad_join
+from rtsds_amd.nn import BatchNorm2d, Conv2d, MaxPool2d, ReLU, conv_bn, conv_bn_relu_maxpool, grad_join
 
 
 class BasicBlock(nn.Module):
@@ -118,7 +118,7 @@ class _ContextPath(nn.Module):
 
     def forward(self, x):
         """x: NHWC compute-dtype batch -> (1/16 features, 1/32 features, GAP(1/32))."""
-        t = self.maxpool1(conv_bn(self.conv1, self.bn1, x, "relu"))
+        t = conv_bn_relu_maxpool(self.conv1, self.bn1, self.maxpool1, x)
         f3 = self.layer3(self.layer2(self.layer1(t)))
         f4 = self.layer4(f3)
         return f3, f4, F.global_avg_pool(f4)

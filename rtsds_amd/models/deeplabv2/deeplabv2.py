@@ -11,7 +11,7 @@ import torch
 import torch.nn as nn
 
 from rtsds_amd import functional as F
-from rtsds_amd.nn import BatchNorm2d, Conv2d, MaxPool2d, ReLU, conv_bn, grad_join, to_input
+from rtsds_amd.nn import BatchNorm2d, Conv2d, MaxPool2d, ReLU, conv_bn, conv_bn_relu_maxpool, grad_join, to_input
 from rtsds_amd.nn import _shadow
 
 affine_par = True
@@ -107,7 +107,7 @@ class ResNetMulti(nn.Module):
         (deeplabv2.py:126), so the training loop can fuse the resize into the loss."""
         _, _, H, W = x.size()
         t = to_input(x)
-        t = self.maxpool(conv_bn(self.conv1, self.bn1, t, "relu"))
+        t = conv_bn_relu_maxpool(self.conv1, self.bn1, self.maxpool, t)
         t = self.layer4(self.layer3(self.layer2(self.layer1(t))))
         t = self.layer6(t)
         return [(t, F.upsample_geometry(t, size=(H, W)))]

@@ -140,6 +140,27 @@ def conv_bn(conv, bn, x, act=None, residual=None, join=None, res_join=None):
     return bn(conv(x, bn_stats=use_batch, join=join), act=act, residual=residual, res_join=res_join)
 
 
+def conv_bn_relu_maxpool(conv, bn, pool, x):
+    """pool(relu(bn(conv(x)))) -- the ResNet stem.  Train-mode (batch statistics) bf16 with a
+    3x3 stride-2 pool: the BN apply, ReLU and pool run as one pass (functional.bn_relu_maxpool,
+    statistics from the conv epilogue); otherwise the separate ops (eval: BN folded into the
+    conv, then the pool)."""
+    use_batch = bn.training or not bn.track_running_stats
+    k = pool.kernel_size if isinstance(pool.kernel_size, int) else pool.kernel_size[0]
+    s = pool.stride if isinstance(pool.stride, int) else pool.stride[0]
+    p = pool.padding if isinstance(pool.padding, int) else pool.padding[0]
+    if use_batch and bn.momentum is not None and x.dtype == torch.bfloat16 and conv.out_channels % 8 == 0 \
+            and k == 3 and s == 2 and p in (0, 1):
+        y = conv(x, bn_stats=True)
+        if F.bn_relu_maxpool_ok(y, k, s, p):
+            rm = bn.running_mean if bn.track_running_stats else None
+            rv = bn.running_var if bn.track_running_stats else None
+            nbt = bn.num_batches_tracked if (bn.training and bn.track_running_stats) else None
+            return F.bn_relu_maxpool(y, bn.weight, bn.bias, rm, rv, True, bn.momentum, bn.eps, p, pool.ceil_mode, nbt)
+        return pool(bn(y, act="relu"))
+    return pool(conv_bn(conv, bn, x, "relu"))
+
+
 def grad_join(x, n):
     """A functional.GradJoin for ``x`` read by ``n`` rtsds Functions, or None when no
     gradient flows to ``x``."""

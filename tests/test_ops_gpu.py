@@ -326,6 +326,78 @@ def test_gap_chscale_row_slices(shape):
     _close(F.global_avg_pool(xd), x.mean((2, 3), keepdim=True), torch.bfloat16, "gap", 1e-2)
 
 
+@pytest.mark.parametrize("geo", [(2, 64, 32, 64, False), (2, 64, 33, 65, True), (1, 16, 20, 24, False)])
+def test_bn_relu_maxpool_fused(geo):
+    """The fused stem (BN train stats from the conv epilogue -> ReLU -> MaxPool 3/2/1) against
+    the separate rtsds ops: pooled output and argmax bit-identical; gradients equal up to the
+    bf16 rounding of the materialised pool gradient the unfused path sums in; BN buffers."""
+    from rtsds_amd import nn as rnn
+    n, c, h, w, ceil = geo
+    g = torch.Generator().manual_seed(h * w)
+    x = torch.randn(n, 3, 2 * h, 2 * w, generator=g).bfloat16()
+    outs = []
+    for fused in (True, False):
+        torch.manual_seed(0)
+        conv = rnn.Conv2d(3, c, 7, 2, 3, bias=False).to(DEV)
+        bn = rnn.BatchNorm2d(c).to(DEV)
+        pool = rnn.MaxPool2d(3, 2, 1, ceil_mode=ceil)
+        with torch.no_grad():
+            bn.weight.uniform_(0.5, 1.5)
+            bn.bias.uniform_(-0.5, 0.5)
+        xd = _dev(x.double(), torch.bfloat16).requires_grad_()
+        if fused:
+            y = rnn.conv_bn_relu_maxpool(conv, bn, pool, xd)
+        else:
+            y = pool(bn(conv(xd, bn_stats=True), act="relu"))
+        gy = torch.randn(y.shape, generator=torch.Generator().manual_seed(1)).to(DEV, torch.bfloat16)
+        y.backward(gy.contiguous(memory_format=CL))
+        torch.cuda.synchronize()
+        outs.append((y.detach().float().cpu(), xd.grad.float().cpu(), conv.weight.grad.cpu(), bn.weight.grad.cpu(),
+                     bn.bias.grad.cpu(), bn.running_mean.cpu(), bn.running_var.cpu(), int(bn.num_batches_tracked)))
+    (yf, dxf, dwf, dgf, dbf, rmf, rvf, nf), (yu, dxu, dwu, dgu, dbu, rmu, rvu, nu) = outs
+    assert torch.equal(yf, yu)
+    # the gather-in-BatchNorm backward entry (rtsds_bn_relu_maxpool_bwd) on the same tensors
+    import ctypes
+    from rtsds_amd._lib import lib
+    from rtsds_amd.runtime import stream, workspace
+    conv = rnn.Conv2d(3, c, 7, 2, 3, bias=False).to(DEV)
+    bn = rnn.BatchNorm2d(c).to(DEV)
+    with torch.no_grad():
+        xc = conv(_dev(x.double(), torch.bfloat16))
+        ho, wo = F.pool_out(h, 3, 2, 1, ceil), F.pool_out(w, 3, 2, 1, ceil)
+        y = torch.empty((n, c, ho, wo), device=DEV, dtype=torch.bfloat16, memory_format=CL)
+        idx = torch.empty((n, ho, wo, c), device=DEV, dtype=torch.uint8)
+        sm, si = torch.empty(c, device=DEV), torch.empty(c, device=DEV)
+        ws = workspace(lib.rtsds_bn_workspace(n * h * w, c), xc.device)
+        P = lambda t: None if t is None else t.data_ptr()  # noqa: E731
+        lib.rtsds_bn_relu_maxpool_fwd(P(xc), P(y), P(idx), n, h, w, c, ho, wo, 1, P(bn.weight), P(bn.bias),
+                                      P(bn.running_mean), P(bn.running_var), None, P(sm), P(si), 0.1, 1e-5, 1, None, 0,
+                                      1, P(ws), ws.numel(), stream())
+        dyp = torch.randn(y.shape, generator=torch.Generator().manual_seed(2)).to(DEV, torch.bfloat16)
+        dyp = dyp.contiguous(memory_format=CL)
+        outs2 = []
+        for fusedb in (True, False):
+            dx = torch.empty_like(xc)
+            dg, db = torch.empty(c, device=DEV), torch.empty(c, device=DEV)
+            if fusedb:
+                lib.rtsds_bn_relu_maxpool_bwd(P(dyp), P(idx), P(xc), P(dx), P(dg), P(db), n, h, w, c, ho, wo, 1,
+                                              P(bn.weight), P(bn.bias), P(sm), P(si), 1, 0, 1, P(ws), ws.numel(), stream())
+            else:
+                gfull = torch.empty_like(xc)
+                lib.rtsds_maxpool_bwd(P(dyp), P(idx), P(gfull), n, h, w, c, ho, wo, 3, 2, 1, 1, stream())
+                lib.rtsds_bn_bwd(P(gfull), P(xc), None, P(dx), None, P(dg), P(db), n * h * w, c, P(bn.weight),
+                                 P(bn.bias), P(sm), P(si), 1, 1, 0, 1, P(ws), ws.numel(), stream())
+            outs2.append((dx.float().cpu(), dg.cpu(), db.cpu()))
+        torch.cuda.synchronize()
+    for a, b, nm in zip(outs2[0], outs2[1], ("dx", "dgamma", "dbeta")):
+        _close(a, b.double(), torch.bfloat16, "gather-bwd " + nm, 2e-2)
+    assert torch.equal(rmf, rmu) and torch.equal(rvf, rvu) and nf == nu == 1
+    _close(dxf, dxu.double(), torch.bfloat16, "dx", 2e-2)
+    _close(dwf, dwu.double(), torch.bfloat16, "dw", 2e-2)
+    _close(dgf, dgu.double(), torch.bfloat16, "dgamma", 2e-2)
+    _close(dbf, dbu.double(), torch.bfloat16, "dbeta", 2e-2)
+
+
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 def test_softmax_ce_argmax(dt):
     g = torch.Generator().manual_seed(9)
