@@ -61,7 +61,8 @@ def parse():
     ap.add_argument("--conv-report", action="store_true")
     ap.add_argument("--no-conv-profile", action="store_true", help="skip the event-timed roofline step")
     ap.add_argument("--graph", default="auto", choices=["auto", "on", "off"],
-                    help="replay the iteration as a hipGraph (auto: single process)")
+                    help="replay the iteration as hipGraph segments (auto = on; under data parallelism "
+                         "the RCCL collectives run between the segments, runtime.GraphedStep)")
     return ap.parse_args()
 
 
@@ -169,7 +170,7 @@ def main():
     optim.set_allreduce_dtype({"fp32": torch.float32, "fp16": torch.float16, "bf16": torch.bfloat16}[args.allreduce_dtype])
     torch.manual_seed(42)
     net, x, set_lr, core, opts = build(args, dev, rank)
-    use_graph = args.graph == "on" or (args.graph == "auto" and world == 1)
+    use_graph = args.graph in ("on", "auto")
 
     def step(i):
         set_lr(i)
@@ -178,11 +179,18 @@ def main():
     for i in range(args.warmup):
         step(i)
     if use_graph:
-        # the whole iteration as one hipGraph replay (runtime.GraphedStep): same kernels, no
-        # per-kernel host launches; lr / Adam step advance through a device buffer
+        # the whole iteration as hipGraph replays (runtime.GraphedStep): same kernels, no
+        # per-kernel host launches; lr / Adam step advance through a device buffer; under data
+        # parallelism the collectives run between the graph segments
         from rtsds_amd.runtime import GraphedStep
-        graphed = GraphedStep(core, opts, warmup=1)
-
+        try:
+            graphed = GraphedStep(core, opts, warmup=1)
+        except Exception as e:  # keep the measurement alive on the eager path
+            print(f"bench: hipGraph capture failed ({e!r}); timing eager iterations", file=sys.stderr)
+            for o in opts:
+                o.set_graph_mode(False)
+            use_graph = False
+    if use_graph:
         def step(i):
             set_lr(i)
             return graphed()

@@ -11,7 +11,8 @@ import numpy as np
 import torch
 
 from ._lib import ACT_RELU, ACT_SIGMOID, ConvDesc, lib
-from .runtime import CL, dcode, dp_world, empty_nhwc, nhwc, require_hip, side_enabled, side_fork, stream, workspace
+from .runtime import (CL, collective, dcode, dp_world, empty_nhwc, nhwc, require_hip, side_enabled, side_fork,
+                      stream, workspace)
 
 _P = lambda t: None if t is None else t.data_ptr()  # noqa: E731
 
@@ -759,7 +760,8 @@ class CrossEntropyFn(torch.autograd.Function):
                          dcode(x), _P(ws), ws.numel(), stream())
         if dp_world() > 1:  # global-batch mean: local loss sum over the all-reduced count
             import torch.distributed as dist
-            dist.all_reduce(ws.view(torch.float32)[2048:2049])
+            cnt = ws.view(torch.float32)[2048:2049]
+            collective(lambda: dist.all_reduce(cnt))
             lib.rtsds_ce_finish(_P(ws), _P(loss), stream())
         ctx.ignore = ignore_index
         ctx.save_for_backward(x, target, ws)
@@ -836,7 +838,8 @@ class UpsampleCrossEntropyFn(torch.autograd.Function):
             # (its contribution; the ranks' losses and gradients then SUM to the single-device
             # values, see runtime.dp_world)
             import torch.distributed as dist
-            dist.all_reduce(ws.view(torch.float32)[:1])
+            cnt = ws.view(torch.float32)[:1]
+            collective(lambda: dist.all_reduce(cnt))
             lib.rtsds_upce_finish(k, _P(ws), _P(per_head), _P(total), stream())
         ctx.geo, ctx.k, ctx.dt, ctx.dtype = geo, k, dt, xs[0].dtype
         ctx.ws = ws

@@ -20,7 +20,7 @@ import torch
 import torch.distributed as dist
 
 from ._lib import lib
-from .runtime import stream
+from .runtime import collective, dp_world, stream
 
 
 _ALLREDUCE = {"dtype": torch.float32}
@@ -43,14 +43,14 @@ def allreduce_flat(buffers):
     gradient scale the Adam kernel applies (1.0)."""
     if not (dist.is_available() and dist.is_initialized()):
         return 1.0
-    if dist.get_world_size() > 1:
+    if dp_world() > 1:
         wire = _ALLREDUCE["dtype"]
         for b in buffers:
             if wire == torch.float32:
-                dist.all_reduce(b)
+                collective(lambda b=b: dist.all_reduce(b))
             else:
                 t = b.to(wire)
-                dist.all_reduce(t)
+                collective(lambda t=t: dist.all_reduce(t))  # a graph-segment break under capture
                 b.copy_(t)
     return 1.0
 

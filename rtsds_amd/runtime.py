@@ -169,6 +169,21 @@ class GraphedForward:
         return self.static_out
 
 
+_capture = {"step": None}  # the GraphedStep currently capturing, if any
+
+
+def collective(fn):
+    """Run ``fn`` (a collective on device tensors, e.g. ``dist.all_reduce(t)``) -- eagerly, or,
+    while a GraphedStep is capturing, as a break between two captured graph segments: the
+    collective is not captured but re-issued between the segments' replays (RCCL's own launch
+    path, stream-ordered with the graphs)."""
+    cap = _capture["step"]
+    if cap is None:
+        return fn()
+    cap._break(fn)
+    return None
+
+
 class GraphedStep:
     """hipGraph of a whole training iteration (zero_grad, forward, losses, backward, optimizer
     step).  ``fn()`` runs one iteration on fixed input buffers and returns device tensors; the
@@ -177,8 +192,13 @@ class GraphedStep:
     (``param_groups[..]["lr"]``, e.g. set by utils.poly_lr_scheduler before the call) and the
     advancing Adam step count, staged by a stream-ordered H2D copy before the replay.  The
     iteration must keep its launch structure (same shapes, same parameters receiving
-    gradients); no host synchronisation may happen inside ``fn``.  Single process: collectives
-    are not captured (data-parallel runs stay eager)."""
+    gradients); no host synchronisation may happen inside ``fn``.
+
+    Data parallelism: every collective of the iteration goes through ``runtime.collective``
+    (the global valid-pixel count of each loss, the gradient all-reduce); under capture each
+    one ends the current graph segment and starts the next in the same memory pool, and a
+    replay runs segment, collective, segment, ... -- so a data-parallel step is replayed too,
+    with its RCCL calls issued eagerly between the graphs."""
 
     def __init__(self, fn, optimizers, warmup=2):
         self.fn = fn
@@ -197,22 +217,43 @@ class GraphedStep:
                 raise RuntimeError("GraphedStep: run one eager iteration before capturing")
             o.stage_hyper()  # allocates the device hyper buffer outside the capture
         torch.cuda.synchronize()
-        self.graph = torch.cuda.CUDAGraph()
+        self.segments = []  # [(graph, collective run after it or None)]
+        self._pool = torch.cuda.graph_pool_handle()
+        cap_stream = torch.cuda.Stream(device=cur.device)
         for o in self.optimizers:
             o._capturing = True
         try:
-            with torch.cuda.graph(self.graph):
-                self.outputs = fn()
+            with torch.cuda.stream(cap_stream):
+                self._graph = torch.cuda.CUDAGraph()
+                self._graph.capture_begin(pool=self._pool)
+                _capture["step"] = self
+                try:
+                    self.outputs = fn()
+                finally:
+                    _capture["step"] = None
+                    self._graph.capture_end()
+                self.segments.append((self._graph, None))
         finally:
             for o in self.optimizers:
                 o._capturing = False
+        cur.wait_stream(cap_stream)
+        self.graph = self.segments[0][0]
         # the capture ran the optimizers' Python bookkeeping once without executing a step
         for o in self.optimizers:
             o.advance_steps(-1)
+
+    def _break(self, coll):
+        self._graph.capture_end()
+        self.segments.append((self._graph, coll))
+        self._graph = torch.cuda.CUDAGraph()
+        self._graph.capture_begin(pool=self._pool)
 
     def __call__(self):
         for o in self.optimizers:
             o.stage_hyper()
             o.advance_steps()
-        self.graph.replay()
+        for g, coll in self.segments:
+            g.replay()
+            if coll is not None:
+                coll()
         return self.outputs

@@ -426,3 +426,62 @@ def test_side_stream_wgrad_equals_serial(da):
     for s in states[1:]:
         for k in states[0]:
             assert torch.equal(states[0][k], s[k]), k
+
+
+@pytest.mark.parametrize("da", [False, True])
+def test_graphed_step_with_collectives(da, monkeypatch):
+    """Data-parallel iterations under runtime.GraphedStep: every collective (the losses'
+    global valid-pixel counts, the gradient all-reduce) is a break between captured graph
+    segments and is re-issued eagerly between their replays.  A one-rank RCCL group with the
+    data-parallel code paths forced on (dp_world patched to 2; all_reduce over one rank is the
+    identity) must leave parameters, optimizer state and BN buffers bit-identical to the same
+    iterations run eagerly."""
+    import socket
+
+    import torch.distributed as dist
+    from rtsds_amd import functional as rf
+    from rtsds_amd import losses as rl
+    from rtsds_amd import runtime
+    from rtsds_amd.runtime import GraphedStep
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+    try:
+        for mod in (rf, optim, rl, rtrain):
+            monkeypatch.setattr(mod, "dp_world", lambda: 2)
+        g = torch.Generator().manual_seed(11)
+        x = torch.randn(2, 3, 64, 128, generator=g).to(DEV)
+        xt = torch.randn(2, 3, 64, 128, generator=g).to(DEV)
+        y = torch.randint(0, 20, (2, 64, 128), generator=g).to(DEV)
+        ce, bce = losses.CrossEntropyLoss(ignore_index=19), losses.BCEWithLogitsLoss()
+        states, nseg = [], None
+        with rtsds_amd.precision(torch.bfloat16):
+            for graphed in (False, True):
+                torch.manual_seed(3)
+                net = BiSeNet(19, "resnet18").to(DEV).train()
+                disc = TinyDomainDiscriminator(19).to(DEV).train()
+                opt = optim.Adam(net.parameters(), lr=1e-3)
+                dopt = optim.Adam(disc.parameters(), lr=1e-3, weight_decay=1e-4)
+
+                def core():
+                    if da:
+                        return rtrain.da_step(net, disc, opt, dopt, ce, bce, x, y, xt, 0.1, 100)[0]
+                    return rtrain.seg_step(net, ce, opt, x, y)[0]
+
+                run = core
+                for i in range(4):
+                    if graphed and i == 1:
+                        run = GraphedStep(core, [opt, dopt] if da else [opt], warmup=0)
+                        nseg = len(run.segments)
+                    run()
+                torch.cuda.synchronize()
+                states.append({k: v.detach().float().cpu().clone() for k, v in
+                               list(net.state_dict().items()) + list(disc.state_dict().items())})
+        assert nseg is not None and nseg >= 3, nseg  # count all-reduce(s) + gradient all-reduce
+        for k in states[0]:
+            assert torch.equal(states[0][k], states[1][k]), k
+    finally:
+        dist.destroy_process_group()
+        assert runtime._capture["step"] is None
