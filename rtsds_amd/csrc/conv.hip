@@ -38,7 +38,8 @@ struct ConvArgs {
   int act;
   int accum;          // FWD/DGRAD: y += result
   float* stats;       // FWD: per-M-tile BatchNorm partials [N][mtile][count, mean, M2] (or null)
-  long split_stride;  // elements between WGRAD split slabs
+  long split_stride;  // elements between WGRAD split slabs (and DGRAD split-K slabs)
+  float* slab;        // DGRAD split-K: fp32 partials [split][M][N] instead of the bf16 epilogue
   // FWD eval-mode BatchNorm fold: y = act(acc * scale[co] + bias[co] (+ res)), scale/bias the
   // running-statistics BN folded with the conv bias (rtsds_bn_fold); res = residual, same
   // layout as y (or null).
@@ -852,8 +853,8 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(const ConvArgs P0) {
 
   // ---- epilogue: C[row][col], row = (lane>>4)*4 + e, col = lane&15 within each 16x16 block
   const int er = (lane >> 4) * 4, ec = lane & 15;
-  if (MODE == MODE_WGRAD) {
-    float* out = (float*)P.out + (long)kz * P.split_stride;
+  if (MODE == MODE_WGRAD || (MODE == MODE_DGRAD && P.slab != nullptr)) {
+    float* out = (MODE == MODE_WGRAD ? (float*)P.out : P.slab) + (long)kz * P.split_stride;
     if (P.N % 4 == 0) {
       // fp32 slab rows leave as 16-B chunks: the C fragments are staged through LDS one
       // wave-row band (WTM rows) at a time, [WTM][BN + 4] fp32.
@@ -1304,7 +1305,7 @@ static void pick_tile(long M, int N, bool b16, int& bm, int& bn) {
 // BK per tile: 64 where the tile is MFMA-dense (128x128, 64x64: one barrier per 64-deep
 // K-step), 32 for 128x64 / narrow-N tiles whose LDS footprint would otherwise cut occupancy.
 template <typename T, int MODE, int BM, int BN, int BK, int WM, int WN>
-static void launch_al(const ConvArgs& p, int cr, hipStream_t st) {
+static void launch_al(const ConvArgs& p, int cr, hipStream_t st, int splits = 1) {
   if constexpr (sizeof(T) == 2 && BM % 32 == 0 && BN % 32 == 0) {
     // LDS-DMA path: every bf16 tile at BK = 64 (16-B chunks never straddle a tap: cr % 8 == 0)
     // (not for 3-channel images padded to 8: eight taps per K-tile gathered per chunk lose
@@ -1315,13 +1316,13 @@ static void launch_al(const ConvArgs& p, int cr, hipStream_t st) {
 #endif
       // ALA 2 (buffer-offset DMA): DGRAD only at stride 1 or in the stride-2 parity phases
       const bool gb_ok = p.gbuf && (MODE != MODE_DGRAD || (p.sh == p.sw && (p.sh == 1 || (p.sh == 2 && p.psh == 2))));
-      if (cr % 64 == 0 && gb_ok) launch<T, MODE, BM, BN, 64, WM, WN, 2, 1, RTSDS_GLN>(p, 1, st);
-      else launch<T, MODE, BM, BN, 64, WM, WN, 1, 1, RTSDS_GLN>(p, 1, st);
+      if (cr % 64 == 0 && gb_ok) launch<T, MODE, BM, BN, 64, WM, WN, 2, 1, RTSDS_GLN>(p, splits, st);
+      else launch<T, MODE, BM, BN, 64, WM, WN, 1, 1, RTSDS_GLN>(p, splits, st);
       return;
     }
   }
-  if (cr % BK == 0) launch<T, MODE, BM, BN, BK, WM, WN, 2, 1>(p, 1, st);
-  else launch<T, MODE, BM, BN, BK, WM, WN, 1, 1>(p, 1, st);
+  if (cr % BK == 0) launch<T, MODE, BM, BN, BK, WM, WN, 2, 1>(p, splits, st);
+  else launch<T, MODE, BM, BN, BK, WM, WN, 1, 1>(p, splits, st);
 }
 
 template <typename T, int MODE>
@@ -1647,6 +1648,64 @@ extern "C" int rtsds_conv2d_fwd_bn(const rtsds_conv_desc* d0, const void* x, con
   return hipGetLastError() == hipSuccess ? RTSDS_OK : RTSDS_ERR_LAUNCH;
 }
 
+// DGRAD split-K for small-M deep stride-1 convs (ResNet layer4: M = 4096 pixels, K = 4608):
+// the occupancy rule would fall back to 64x64 tiles (AI 32 flop/B of staged operands); 128x128
+// tiles x S K-splits keep the MFMA-dense tile and still put >= 512 workgroups on the chip.
+// fp32 slabs [S][M][N] summed in split order (+ accumulate) into the bf16 dx.
+struct DgradSplit {
+  int splits, tps;
+  size_t slab_bytes;
+};
+static DgradSplit dgrad_split(const rtsds_conv_desc* d, int kp) {
+  DgradSplit s = {1, 1 << 30, 0};
+#ifdef RTSDS_NO_DGRAD_SPLIT
+  return s;
+#endif
+  if (d->dtype != RTSDS_BF16 || d->sh != 1 || d->sw != 1 || kp % 64 != 0 || d->c % 8 != 0) return s;
+  const long M = (long)d->n * d->h * d->w;
+  const int N = d->c, K = d->kh * d->kw * kp;
+  int bm, bn;
+  pick_tile(M, N, true, bm, bn);
+  if (!(bm == 64 && bn == 64)) return s;  // the wide tiles already fill the chip
+  const long tiles = ((M + 127) / 128) * ((N + 127) / 128);
+  const int nk = (K + 63) / 64;
+  int want = (int)std::min<long>(8, (512 + tiles - 1) / tiles);
+  want = std::min(want, nk / 16);  // >= 16 K-tiles per split
+  if (want < 2) return s;
+  s.tps = (nk + want - 1) / want;
+  s.splits = (nk + s.tps - 1) / s.tps;
+  s.slab_bytes = al256((size_t)s.splits * M * N * 4);
+  return s;
+}
+// dx (+)= sum_s slab[s] -> bf16; 8 channels per thread
+__global__ void __launch_bounds__(256) dgrad_split_reduce_kernel(const float* __restrict__ slab, bf16* __restrict__ dx, long nv8,
+                                                                long stride, int splits, int accum) {
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < nv8; i += (long)gridDim.x * 256) {
+    float s[8];
+    {
+      const f32x4 a = *(const f32x4*)(slab + i * 8), b = *(const f32x4*)(slab + i * 8 + 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { s[e] = a[e]; s[4 + e] = b[e]; }
+    }
+    for (int q = 1; q < splits; ++q) {
+      const f32x4 a = *(const f32x4*)(slab + q * stride + i * 8), b = *(const f32x4*)(slab + q * stride + i * 8 + 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { s[e] += a[e]; s[4 + e] += b[e]; }
+    }
+    bf16x8* o = (bf16x8*)(dx + i * 8);
+    bf16x8 r;
+    if (accum) {
+      const bf16x8 old = *o;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) r[e] = (bf16)(s[e] + (float)old[e]);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) r[e] = (bf16)s[e];
+    }
+    *o = r;
+  }
+}
+
 // DGRAD workspace: repacked (and Cout-padded) weights + a Cout-padded copy of dy if needed.
 extern "C" size_t rtsds_conv2d_dgrad_workspace(const rtsds_conv_desc* d) {
   if (pooled_1x1(d) || pw_ok(d)) return 0;
@@ -1654,7 +1713,7 @@ extern "C" size_t rtsds_conv2d_dgrad_workspace(const rtsds_conv_desc* d) {
   const size_t es = esize(d->dtype);
   size_t b = al256((size_t)kp * d->kh * d->kw * d->c * es);
   if (kp != d->k) b += al256((size_t)d->n * d->ho * d->wo * kp * es);
-  return b;
+  return b + dgrad_split(d, kp).slab_bytes;
 }
 
 static void repack_launch(int dtype, const void* w, void* wt, int co_n, int co_p, int kh, int kw, int ci_n, int tkh, int tkw,
@@ -1772,7 +1831,20 @@ extern "C" int rtsds_conv2d_dgrad(const rtsds_conv_desc* d0, const void* dy, con
     p.M = d.n * d.h * d.w;
     p.N = d.c;
     p.K = d.kh * d.kw * kp;
-    if (d.dtype == RTSDS_BF16) dispatch_align<bf16, MODE_DGRAD>(p, kp, st);
+    const DgradSplit sk = dgrad_split(d0, kp);
+    if (sk.splits > 1) {
+      // slab region: after the repacked weights and the (optional) Cout-padded dy
+      size_t off = al256((size_t)kp * d.kh * d.kw * d.c * es);
+      if (kp != k_real) off += al256((size_t)d.n * d.ho * d.wo * kp * es);
+      p.slab = (float*)((char*)ws + off);
+      p.split_stride = (long)p.M * p.N;
+      p.tiles_per_split = sk.tps;
+      p.accum = 0;
+      launch_al<bf16, MODE_DGRAD, 128, 128, 64, 2, 2>(p, kp, st, sk.splits);
+      const long nv8 = (long)p.M * p.N / 8;
+      hipLaunchKernelGGL(dgrad_split_reduce_kernel, dim3((int)std::min<long>(8192, (nv8 + 255) / 256)), dim3(256), 0, st,
+                         (const float*)p.slab, (bf16*)dx, nv8, p.split_stride, sk.splits, accumulate ? 1 : 0);
+    } else if (d.dtype == RTSDS_BF16) dispatch_align<bf16, MODE_DGRAD>(p, kp, st);
     else dispatch_align<float, MODE_DGRAD>(p, kp, st);
   }
   return hipGetLastError() == hipSuccess ? RTSDS_OK : RTSDS_ERR_LAUNCH;

@@ -57,6 +57,7 @@ CONV_CASES = [
     (2, 128, 8, 128, 19, 3, 1, 1, 1, False),   # halo direct conv (hconv.hip): Cout 19, w % 64 == 0
     (1, 64, 12, 64, 32, 3, 1, 1, 1, True),     # hconv with bias, Cout 32, edge tiles on 3 row-blocks
     (1, 256, 8, 64, 64, 3, 1, 1, 1, True),     # hconv N-tiled (Cin >= 256, Cout 2 x 32), fwd and dgrad
+    (2, 512, 16, 32, 512, 3, 1, 1, 1, False),  # layer4-like: DGRAD split-K (128x128 tiles, fp32 slabs)
     (2, 512, 32, 64, 19, 1, 1, 0, 1, True),    # supervision 1x1 (pw.hip backward): 1 row group
     (2, 40, 32, 64, 32, 1, 1, 0, 1, True),     # pw.hip: Cout 32, 12 row groups
     (4, 19, 32, 32, 19, 1, 1, 0, 1, True),     # pw.hip: final 19->19, odd Cin (scalar lanes)
@@ -93,6 +94,30 @@ def test_conv_fwd_bwd(case, dt):
     _close(wp.grad, wr.grad, dt, "dw")
     if bias:
         _close(bp.grad, br.grad, dt, "db")
+
+
+def test_dgrad_split_k_accumulate():
+    """DGRAD split-K (small-M deep conv) with the accumulate flag: dx += dgrad."""
+    import ctypes
+    from rtsds_amd._lib import lib
+    from rtsds_amd.functional import _conv_desc, _P
+    from rtsds_amd.runtime import stream, workspace
+
+    g = torch.Generator().manual_seed(5)
+    n, c, h, w, k = 2, 512, 16, 32, 512
+    dy = _dev(torch.randn(n, k, h, w, generator=g), torch.bfloat16)
+    wq = _dev(torch.randn(k, c, 3, 3, generator=g) / (9 * c) ** 0.5, torch.bfloat16)
+    x = _dev(torch.zeros(n, c, h, w), torch.bfloat16)
+    d = _conv_desc(x, k, 3, 3, (1, 1), (1, 1), (1, 1))
+    dx0 = _dev(torch.randn(n, c, h, w, generator=g), torch.bfloat16)
+    dx, fresh = dx0.clone(), torch.empty_like(dx0)
+    ws = workspace(lib.rtsds_conv2d_dgrad_workspace(ctypes.byref(d)), x.device)
+    for out, acc in ((dx, 1), (fresh, 0)):
+        assert lib.rtsds_conv2d_dgrad(ctypes.byref(d), _P(dy), _P(wq), _P(out), acc, _P(ws), ws.numel(), stream()) == 0
+    torch.cuda.synchronize()
+    ref = TF.conv_transpose2d(dy.double().cpu(), wq.double().cpu(), padding=1)
+    _close(fresh, ref, torch.bfloat16, "dx")
+    _close(dx, dx0.double() + fresh.double(), torch.bfloat16, "dx accum", tol=1e-2)
 
 
 @pytest.mark.parametrize("c", [512, 19])
