@@ -53,7 +53,7 @@ typedef struct {
 
 /* y = act(conv(x, w) + bias [+ y if act & RTSDS_ACCUMULATE]).  bias may be NULL (fp32 [k]).
  * bn_stats (may be NULL; act must be NONE): receives the following BatchNorm's per-tile
- * partial statistics, fp32 [k][rtsds_conv2d_fwd_stats_tiles(d)][count, mean, M2] (channel-major), consumed
+ * partial statistics, fp32 [k][rtsds_conv2d_fwd_stats_tiles(d)][count, mean, M2, 0] (channel-major), consumed
  * by rtsds_bn_fwd(stats_part=...) -- the statistics pass over y is then skipped.
  * ws >= rtsds_conv2d_fwd_workspace(d) (non-zero only when Cin needs channel padding).   */
 size_t rtsds_conv2d_fwd_workspace(const rtsds_conv_desc* d);
@@ -89,7 +89,7 @@ int rtsds_conv2d_wgrad(const rtsds_conv_desc* d, const void* x, const void* dy, 
  * semantics).  Forward (eval): running stats are used and copied to save_* when non-NULL.
  * y = act(gamma * (x - mean) * invstd + beta [+ res]).  gamma/beta may be NULL (1 / 0).   */
 size_t rtsds_bn_workspace(long rows, int c);
-/* stats_part (may be NULL): [c][stats_nrb][count, mean, M2] partials from the producing
+/* stats_part (may be NULL): [c][stats_nrb][count, mean, M2, 0] partials from the producing
  * conv (rtsds_conv2d_fwd bn_stats) -- training mode then skips its own statistics pass.   */
 int rtsds_bn_fwd(const void* x, const void* res, void* y, long rows, int c, const float* gamma,
                  const float* beta, float* running_mean, float* running_var,

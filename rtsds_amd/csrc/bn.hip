@@ -68,7 +68,8 @@ RT_DEV void chan_merge(float& na, float& ma, float& Ma, float nb, float mb, floa
   na = n;
 }
 
-// Pass 1 (forward): part[(ch * RB + rb) * 3 + {0,1,2}] = (count, mean, M2) of block rb
+// Pass 1 (forward): part[(ch * RB + rb) * 4 + {0,1,2}] = (count, mean, M2) of block rb (16-B
+// records: one vector store / load each)
 // (channel-major: the finalize reads one contiguous run per channel).
 template <typename T, int VEC>
 __global__ void __launch_bounds__(256) bn_stats_kernel(const T* __restrict__ x, float* __restrict__ part, long rows, int c) {
@@ -121,8 +122,7 @@ __global__ void __launch_bounds__(256) bn_stats_kernel(const T* __restrict__ x, 
         chan_merge(n, m, M, sh[0][t][j], sh[1][t][j], sh[2][t][j]);
       }
       if (ch0 + j < c) {
-        float* o = part + ((long)(ch0 + j) * gridDim.x + blockIdx.x) * 3;
-        o[0] = n; o[1] = m; o[2] = M;
+        *(f32x4*)(part + ((long)(ch0 + j) * gridDim.x + blockIdx.x) * 4) = f32x4{n, m, M, 0.f};
       }
     }
   }
@@ -154,9 +154,8 @@ __global__ void __launch_bounds__(256) bn_finalize_kernel(const float* __restric
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       const int b = min(b0 + 256 * u, nrb - 1);
-      const float* p = part + ((long)ch * nrb + b) * 3;
-      const float n0 = p[0];  // clamped index: unconditional loads, zero count past nrb
-      pn[u] = b0 + 256 * u < nrb ? n0 : 0.f;
+      const f32x4 p = *(const f32x4*)(part + ((long)ch * nrb + b) * 4);  // clamped: unconditional
+      pn[u] = b0 + 256 * u < nrb ? p[0] : 0.f;                             // zero count past nrb
       pm[u] = p[1];
       pM[u] = p[2];
     }
@@ -577,7 +576,7 @@ static int bn_apply_rb(long rows, int c, int vec) {
   return (int)std::max<long>(1, std::min<long>((need + 1) / 2, 1L << 24));
 }
 
-static size_t bn_part_floats(long rows, int c) { return (size_t)bn_rb(rows, c, 1) * c * 3; }
+static size_t bn_part_floats(long rows, int c) { return (size_t)bn_rb(rows, c, 1) * c * 4; }
 
 // Workspace: [row-block partials | 8 coefficient arrays], each part
 // 256-B aligned (coefficient arrays are read with 16-B vector loads).

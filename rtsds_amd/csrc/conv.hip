@@ -37,7 +37,7 @@ struct ConvArgs {
   FastDiv f_tkw;
   int act;
   int accum;          // FWD/DGRAD: y += result
-  float* stats;       // FWD: per-M-tile BatchNorm partials [N][mtile][count, mean, M2] (or null)
+  float* stats;       // FWD: per-M-tile BatchNorm partials [N][mtile][count, mean, M2, 0] (or null)
   long split_stride;  // elements between WGRAD split slabs (and DGRAD split-K slabs)
   float* slab;        // DGRAD split-K: fp32 partials [split][M][N] instead of the bf16 epilogue
   // FWD eval-mode BatchNorm fold: y = act(acc * scale[co] + bias[co] (+ res)), scale/bias the
@@ -1029,10 +1029,8 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(const ConvArgs P0) {
         if (pass == 0) {
           mean[j] = tot / (float)nvalid;
         } else if (wmi == 0 && lane < 16 && n0 + col < P.N) {
-          float* o = P.stats + ((long)(n0 + col) * gridDim.x + mt) * 3;  // [channel][M tile][3]
-          o[0] = (float)nvalid;
-          o[1] = mean[j];
-          o[2] = tot;
+          // [channel][M tile][4]: one 16-B record store
+          *(f32x4*)(P.stats + ((long)(n0 + col) * gridDim.x + mt) * 4) = f32x4{(float)nvalid, mean[j], tot, 0.f};
         }
       }
       __syncthreads();
@@ -1390,9 +1388,7 @@ __global__ void __launch_bounds__(256) pooled_fwd_kernel(const T* __restrict__ x
 #pragma unroll
     for (int m = 0; m < MR; ++m)
       if (m < m_n) m2 += (acc[m] - mean) * (acc[m] - mean);
-    stats[k * 3 + 0] = (float)m_n;
-    stats[k * 3 + 1] = mean;
-    stats[k * 3 + 2] = m2;
+    *(f32x4*)(stats + k * 4) = f32x4{(float)m_n, mean, m2, 0.f};
   }
 }
 

@@ -34,7 +34,7 @@ struct HconvArgs {
   const float* bias;   // [k] or null (eval fold: shift)
   const float* scale;  // [k] or null (eval fold)
   bf16* y;             // NHWC [n][h][w][k]
-  float* stats;        // [k][tiles][3] or null
+  float* stats;        // [k][tiles][4] or null
   int n, h, w, c, k, act, accum;  // k = output channels, tiled by 32 over blockIdx.y
 };
 
@@ -181,10 +181,8 @@ __global__ void __launch_bounds__(256, 1) hconv_fwd_kernel(const HconvArgs P) {
         if (pass == 0) {
           mean[j] = tot / (float)(kTR * kTC);
         } else if (wave == 0 && lane < 16 && n0 + n < P.k) {
-          float* o = P.stats + ((long)(n0 + n) * gridDim.x + bid) * 3;  // [channel][tile][3]
-          o[0] = (float)(kTR * kTC);
-          o[1] = mean[j];
-          o[2] = tot;
+          *(f32x4*)(P.stats + ((long)(n0 + n) * gridDim.x + bid) * 4) =  // [channel][tile][4]
+              f32x4{(float)(kTR * kTC), mean[j], tot, 0.f};
         }
       }
       __syncthreads();

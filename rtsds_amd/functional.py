@@ -203,7 +203,7 @@ def conv2d(x, weight, bias, wq, stride=(1, 1), padding=(0, 0), dilation=(1, 1), 
         k, _, kh, kw = weight.shape
         d = _conv_desc(x, k, kh, kw, stride, padding, dilation)
         nrb = lib.rtsds_conv2d_fwd_stats_tiles(ctypes.byref(d))
-        stats = torch.empty(nrb * k * 3, dtype=torch.float32, device=x.device)
+        stats = torch.empty(nrb * k * 4, dtype=torch.float32, device=x.device)  # [k][nrb][4]
     y = ConvFn.apply(x, weight, bias, wq, tuple(stride), tuple(padding), tuple(dilation), act, stats, join)
     if stats is not None:
         y._rt_bn_stats = (stats, nrb)
