@@ -431,8 +431,7 @@ __global__ void __launch_bounds__(256) bn_bwd_stats_kernel(const GS gs, const T*
         const float a = (red[0][tid][j] + red[0][64 + tid][j]) + (red[0][128 + tid][j] + red[0][192 + tid][j]);
         const float b = (red[1][tid][j] + red[1][64 + tid][j]) + (red[1][128 + tid][j] + red[1][192 + tid][j]);
         if (ch0 + j < c) {
-          float* o = part + ((long)(ch0 + j) * gridDim.x + blockIdx.x) * 2;
-          o[0] = a; o[1] = b;
+          *(float2*)(part + ((long)(ch0 + j) * gridDim.x + blockIdx.x) * 2) = make_float2(a, b);
         }
       }
     }
@@ -450,8 +449,7 @@ __global__ void __launch_bounds__(256) bn_bwd_stats_kernel(const GS gs, const T*
         b += red[1][gi * L.tpr + cv][j];
       }
       if (ch0 + j < c) {
-        float* o = part + ((long)(ch0 + j) * gridDim.x + blockIdx.x) * 2;
-        o[0] = a; o[1] = b;
+        *(float2*)(part + ((long)(ch0 + j) * gridDim.x + blockIdx.x) * 2) = make_float2(a, b);
       }
     }
   }
@@ -471,7 +469,8 @@ __global__ void __launch_bounds__(256) bn_bwd_finalize_kernel(const float* __res
     for (int u = 0; u < 8; ++u) {
       const int b = min(b0 + 256 * u, nrb - 1);
       const bool ok = b0 + 256 * u < nrb;
-      const float g = part[((long)ch * nrb + b) * 2], gx = part[((long)ch * nrb + b) * 2 + 1];
+      const float2 pr = *(const float2*)(part + ((long)ch * nrb + b) * 2);
+      const float g = pr.x, gx = pr.y;
       pg[u] = ok ? g : 0.f;
       px[u] = ok ? gx : 0.f;
     }
