@@ -33,6 +33,9 @@ sys.path.insert(0, ROOT)
 
 MFMA_BF16_PEAK_TFLOPS = 2500.0   # MI355X dense bf16 (MI355X_MICROARCH.md)
 NC = 19
+# default timed steps per workload: >= ~2.4 s of timed work at the round-2 step times, so the
+# driver's own wall clock and GPU-busy sampler can corroborate the measured window
+DEFAULT_STEPS = {"bisenet-seg": 400, "bisenet-da": 160, "deeplab-seg": 70, "deeplab-da": 40}
 # workload -> (model, DA?, default per-GPU batch, H, W, conv GFLOP per unit, BASELINE config)
 WORKLOADS = {
     "bisenet-seg": ("bisenet", False, 8, 512, 1024, 151.6, "configs[1]: BiSeNet-R18 seg-only train step (train.py:65-113)"),
@@ -49,7 +52,8 @@ H, W = 512, 1024
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=None,
+                    help="timed steps (default: the workload's, >= 2 s of timed work)")
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", default="bisenet-seg", choices=sorted(WORKLOADS))
     ap.add_argument("--batch", type=int, default=None, help="per-GPU batch (default: the workload's)")
@@ -153,8 +157,30 @@ def build(args, dev, rank):
     return net, x, set_lr, core, [opt, dopt]
 
 
+def launch_ranks(args):
+    """``--gpus N`` (N > 1) without a torchrun environment: start N ranks (one process per
+    GPU) under torch.distributed.run as a CHILD process -- nothing here has touched the GPU
+    yet -- and exit with its status; rank 0 prints the JSON line."""
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
 def main():
     args = parse()
+    env_world = int(os.environ.get("WORLD_SIZE", "0"))
+    if env_world == 0 and args.gpus > 1:
+        sys.exit(launch_ranks(args))
+    if env_world and env_world != args.gpus:
+        print(f"bench: --gpus {args.gpus} but WORLD_SIZE={env_world}", file=sys.stderr)
+        sys.exit(2)
+    if args.steps is None:
+        args.steps = DEFAULT_STEPS[args.workload]
     from rtsds_amd import functional as F
     from rtsds_amd import optim, set_compute_dtype
     from rtsds_amd.utils import init_distributed
@@ -165,6 +191,11 @@ def main():
     rank, local, world = init_distributed()
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    if world > 1:  # the ranks the collective backend actually formed
+        world = dist.get_world_size()
+        backend = dist.get_backend()
+    else:
+        backend = None
     dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
     set_compute_dtype(dtype)
     optim.set_allreduce_dtype({"fp32": torch.float32, "fp16": torch.float16, "bf16": torch.bfloat16}[args.allreduce_dtype])
@@ -294,6 +325,8 @@ def main():
         "final_loss": round(final_loss, 4),
         "host_enqueue_ms_per_step": round(1000.0 * t_enqueue / args.steps, 3),
         "hip_graph": use_graph,
+        "timed_s": round(elapsed, 3),
+        **({"ranks": world, "backend": backend} if backend else {}),
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.workload == "bisenet-seg":
         out["cpu_baseline"] = cpu_baseline()

@@ -235,6 +235,15 @@ int rtsds_adam_step_dev(float* param, const float* grad, float* exp_avg, float* 
                         void* bf16_shadow, long n, const float* hyper, float beta1, float beta2,
                         float eps, float weight_decay, float grad_scale, void* stream);
 
+/* torch.optim.SGD step (main.py:118-120) over a flat fp32 arena: d = grad*grad_scale
+ * (+ weight_decay*param); with momentum, buf = d on the first step (first != 0), else
+ * buf = momentum*buf + (1-dampening)*d; d = nesterov ? d + momentum*buf : buf;
+ * param -= lr*d.  hyper (device fp32 {lr, first}, may be NULL) overrides lr / first for
+ * hipGraph replays.  bf16_shadow (may be NULL) receives bf16(param).                       */
+int rtsds_sgd_step(float* param, const float* grad, float* momentum_buf, void* bf16_shadow,
+                   long n, const float* hyper, float lr, float momentum, float dampening,
+                   float weight_decay, int nesterov, int first, float grad_scale, void* stream);
+
 /* ---------------------------------------------------------------- metrics
  * argmax over channels, first maximum wins (train.py:102-106,272-275; validation.py:51).
  * out (int64 [n*hw]) may be NULL; if target and correct are given, *correct += #matches.

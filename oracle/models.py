@@ -259,3 +259,14 @@ class _GRL(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g):
         return -ctx.alpha * g, None
+
+
+class UpSampler(nn.Module):
+    """x8 bilinear (align_corners=False) -> 1x1 conv with bias (model.py:19-28)."""
+
+    def __init__(self, num_classes):
+        super().__init__()
+        self.conv = nn.Conv2d(num_classes, num_classes, kernel_size=1)
+
+    def forward(self, x):
+        return self.conv(F.interpolate(x, scale_factor=8, mode="bilinear"))

@@ -75,6 +75,8 @@ SIGNATURES = {
     "rtsds_bce_fwd": (c_int, [P, P, P, c_int, P]),
     "rtsds_bce_bwd": (c_int, [P, P, P, P, c_int, P]),
     "rtsds_adam_step_dev": (c_int, [P, P, P, P, P, c_long, P, c_float, c_float, c_float, c_float, c_float, P]),
+    "rtsds_sgd_step": (c_int, [P, P, P, P, c_long, P, c_float, c_float, c_float, c_float, c_int, c_int,
+                               c_float, P]),
     "rtsds_adam_step": (c_int, [P, P, P, P, P, c_long, c_float, c_float, c_float, c_float, c_float,
                                 c_int, c_float, P]),
     "rtsds_argmax": (c_int, [P, c_long, c_long, c_long, P, P, P, c_int, c_long, c_int, c_int, P]),

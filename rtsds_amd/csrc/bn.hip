@@ -9,13 +9,7 @@
 #include "common.h"
 #include <algorithm>
 
-#ifndef RTSDS_BN_MAXRB
-#define RTSDS_BN_MAXRB 2048
-#endif
-#ifndef RTSDS_BN_RPT
-#define RTSDS_BN_RPT 8
-#endif
-static const int kBnMaxRB = RTSDS_BN_MAXRB;  // row blocks of the partial-statistics pass
+static const int kBnMaxRB = 2048;  // row blocks of the partial-statistics pass
 
 // Threads of a 256-block are laid out [row group][channel vector]; TPR = threads per row.
 template <int VEC> struct BnLayout {
@@ -371,10 +365,7 @@ __global__ void __launch_bounds__(256) bn_bwd_stats_kernel(const GS gs, const T*
   if (active) {
     bn_bwd_coef<VEC>(ch0, c, gamma, beta, mean, sinv, mu, sc, sh);
     const long step = (long)gridDim.x * L.rpi;
-#ifndef RTSDS_BN_U
-#define RTSDS_BN_U 2
-#endif
-    constexpr int U = RTSDS_BN_U;  // rows in flight per thread (loads issued before any use)
+    constexpr int U = 2;  // rows in flight per thread (loads issued before any use)
     for (long r = (long)blockIdx.x * L.rpi + rg; r < rows; r += U * step) {
       float g[U][VEC], xv[U][VEC], yv[HAS_Y ? U : 1][VEC];
 #pragma unroll
@@ -566,7 +557,7 @@ static long bn_need(long rows, int c, int vec) {
 static int bn_rb(long rows, int c, int vec) {
   const long need = bn_need(rows, c, vec);
   long rb = std::min<long>(need, kBnMaxRB);
-  rb = std::max<long>(1, std::min<long>(rb, (need + RTSDS_BN_RPT - 1) / RTSDS_BN_RPT));
+  rb = std::max<long>(1, std::min<long>(rb, (need + 7) / 8));
   return (int)rb;
 }
 // Row blocks of the elementwise passes: ~2 rows per thread.

@@ -144,7 +144,13 @@ RT_DEV bf16x8 rc_gl_frag(s16x4 t0, s16x4 t1) {
 // 16 zero bytes: the DMA source of padding / out-of-range gathers.
 __device__ __attribute__((aligned(16))) bf16 g_conv_zero[8];
 template <int N> RT_DEV void wait_vmcnt() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+// Workgroup barrier of the LDS-DMA pipelines.  The s_waitcnt lgkmcnt(0) is required: without
+// it the compiler may leave this wave's last ds_reads of an operand buffer outstanding across
+// the barrier (their consumers, the MFMAs, are free to sink past it), and another wave's DMA
+// refill of that buffer then races them -- measured as non-deterministic outputs on large
+// grids (tests/test_configs_gpu.py::test_bench_conv_shapes, tools/diag/det_conv.py).
 RT_DEV void gl_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
 }
@@ -766,16 +772,12 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(const ConvArgs P0) {
     gl_issue(kt0, 0);
     for (int kt = kt0; kt < kt1; ++kt) {
       const int buf = (kt - kt0) & 1;
-#ifndef RTSDS_CONV_MIDISSUE
       if (kt + 1 < kt1) {
         gl_issue(kt + 1, buf ^ 1);
         wait_vmcnt<NA + NB>();  // tile kt landed; tile kt+1 stays in flight across the barrier
       } else {
         wait_vmcnt<0>();
       }
-#else
-      wait_vmcnt<0>();
-#endif
       gl_barrier();
       const T* sa = smem + buf * (A_EL + B_EL);
       const T* sb = sa + A_EL;
@@ -805,20 +807,11 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(const ConvArgs P0) {
 #pragma unroll
           for (int j = 0; j < FN; ++j) fb[j] = frag_kc_gl((const bf16*)sb, wn0 + j * 16, ks, lane);
         }
-#ifdef RTSDS_CONV_PRIO
-        __builtin_amdgcn_s_setprio(1);
-#endif
 #pragma unroll
         for (int i = 0; i < FM; ++i)
 #pragma unroll
           for (int j = 0; j < FN; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
-#ifdef RTSDS_CONV_PRIO
-        __builtin_amdgcn_s_setprio(0);
-#endif
-#ifdef RTSDS_CONV_MIDISSUE
-        if (ks == 0 && kt + 1 < kt1) gl_issue(kt + 1, buf ^ 1);
-#endif
       }
       gl_barrier();  // every wave is done reading buf before it is refilled
     }
@@ -1265,35 +1258,16 @@ static void launch(const ConvArgs& p, int splits, hipStream_t st) {
   hipLaunchKernelGGL((conv_gemm_kernel<T, MODE, BM, BN, BK, WM, WN, ALA, ALB, GL>), grid, dim3(256), 0, st, p);
 }
 
-// LDS-DMA staging on (default) / off (RTSDS_CONV_GLDS=0, for A/B measurements).
-static bool glds_enabled() {
-  static const int on = [] {
-    const char* e = getenv("RTSDS_CONV_GLDS");
-    return (e && e[0] == '0') ? 0 : 1;
-  }();
-  return on != 0;
-}
-
 // Tile selection for FWD / DGRAD (occupancy-aware): the widest tile that still puts >= 256
 // workgroups on the 256 CUs.  bf16: 128x128 / 128x64 / 256x32 (19- and 1-channel outputs),
 // falling back to 64x64 / 128x32 for small-M layers (ResNet layer4, pooled vectors).
 static void pick_tile(long M, int N, bool b16, int& bm, int& bn) {
   auto blocks = [&](int a, int b) { return ((M + a - 1) / a) * (long)((N + b - 1) / b); };
   if (b16) {
-#ifdef RTSDS_N32_BM128
-    if (N <= 32) { bn = 32; bm = 128; }
-#else
     if (N <= 32) { bn = 32; bm = blocks(256, 32) >= 256 ? 256 : 128; }
-#endif
     else if (N <= 64) { bn = 64; bm = blocks(128, 64) >= 256 ? 128 : 64; }
-#ifndef RTSDS_T128_MIN
-#define RTSDS_T128_MIN 512
-#endif
-#ifndef RTSDS_T12864_MIN
-#define RTSDS_T12864_MIN 384
-#endif
-    else if (blocks(128, 128) >= RTSDS_T128_MIN) { bm = 128; bn = 128; }
-    else if (blocks(128, 64) >= RTSDS_T12864_MIN) { bm = 128; bn = 64; }
+    else if (blocks(128, 128) >= 512) { bm = 128; bn = 128; }
+    else if (blocks(128, 64) >= 384) { bm = 128; bn = 64; }
     else { bm = 64; bn = 64; }
   } else {
     if (N <= 32) { bm = 128; bn = 32; } else { bm = 64; bn = 64; }
@@ -1308,14 +1282,11 @@ static void launch_al(const ConvArgs& p, int cr, hipStream_t st, int splits = 1)
     // LDS-DMA path: every bf16 tile at BK = 64 (16-B chunks never straddle a tap: cr % 8 == 0)
     // (not for 3-channel images padded to 8: eight taps per K-tile gathered per chunk lose
     // to the register path there)
-    if (glds_enabled() && cr % 32 == 0 && p.K % 8 == 0) {
-#ifndef RTSDS_GLN
-#define RTSDS_GLN 2
-#endif
+    if (cr % 32 == 0 && p.K % 8 == 0) {
       // ALA 2 (buffer-offset DMA): DGRAD only at stride 1 or in the stride-2 parity phases
       const bool gb_ok = p.gbuf && (MODE != MODE_DGRAD || (p.sh == p.sw && (p.sh == 1 || (p.sh == 2 && p.psh == 2))));
-      if (cr % 64 == 0 && gb_ok) launch<T, MODE, BM, BN, 64, WM, WN, 2, 1, RTSDS_GLN>(p, splits, st);
-      else launch<T, MODE, BM, BN, 64, WM, WN, 1, 1, RTSDS_GLN>(p, splits, st);
+      if (cr % 64 == 0 && gb_ok) launch<T, MODE, BM, BN, 64, WM, WN, 2, 1, 2>(p, splits, st);
+      else launch<T, MODE, BM, BN, 64, WM, WN, 1, 1, 2>(p, splits, st);
       return;
     }
   }
@@ -1654,9 +1625,6 @@ struct DgradSplit {
 };
 static DgradSplit dgrad_split(const rtsds_conv_desc* d, int kp) {
   DgradSplit s = {1, 1 << 30, 0};
-#ifdef RTSDS_NO_DGRAD_SPLIT
-  return s;
-#endif
   if (d->dtype != RTSDS_BF16 || d->sh != 1 || d->sw != 1 || kp % 64 != 0 || d->c % 8 != 0) return s;
   const long M = (long)d->n * d->h * d->w;
   const int N = d->c, K = d->kh * d->kw * kp;
@@ -1702,6 +1670,11 @@ __global__ void __launch_bounds__(256) dgrad_split_reduce_kernel(const float* __
   }
 }
 
+// The DGRAD route of a descriptor: the halo direct conv for narrow-output 3x3 convs, else
+// the implicit GEMM (with split-K slabs when dgrad_split() asks).  One predicate for both the
+// workspace query and the launch.
+static bool dgrad_hconv(const rtsds_conv_desc* d, int kp) { return kp % 32 == 0 && hconv_dgrad_ok(d); }
+
 // DGRAD workspace: repacked (and Cout-padded) weights + a Cout-padded copy of dy if needed.
 extern "C" size_t rtsds_conv2d_dgrad_workspace(const rtsds_conv_desc* d) {
   if (pooled_1x1(d) || pw_ok(d)) return 0;
@@ -1709,6 +1682,7 @@ extern "C" size_t rtsds_conv2d_dgrad_workspace(const rtsds_conv_desc* d) {
   const size_t es = esize(d->dtype);
   size_t b = al256((size_t)kp * d->kh * d->kw * d->c * es);
   if (kp != d->k) b += al256((size_t)d->n * d->ho * d->wo * kp * es);
+  if (dgrad_hconv(d, kp)) return b;  // the halo conv needs no split-K slabs
   return b + dgrad_split(d, kp).slab_bytes;
 }
 
@@ -1761,7 +1735,7 @@ extern "C" int rtsds_conv2d_dgrad(const rtsds_conv_desc* d0, const void* dy, con
   }
   const int k_real = d.k;
   d.k = kp;
-  if (kp % 32 == 0 && hconv_dgrad_ok(d0)) {
+  if (dgrad_hconv(d0, kp)) {
     // narrow-output 3x3 conv: halo direct conv over dY with the flipped, transposed weights
     repack_launch(d.dtype, w, wt, k_real, kp, d.kh, d.kw, d.c, d.kh, d.kw, d.kh - 1, d.kw - 1, -1, st);
     hconv_dgrad(d0, dy, kp, wt, dx, accumulate, st);
@@ -1893,15 +1867,11 @@ template <typename T>
 static void wgrad_launch(const ConvArgs& p, int bm, int bn, int splits, hipStream_t st) {
   constexpr int BK = sizeof(T) == 2 ? 64 : 16;
   if constexpr (sizeof(T) == 2) {
-    if (glds_enabled()) {  // LDS-DMA staging (swizzled RC images)
-      if (bm == 64 && bn == 64) launch<T, MODE_WGRAD, 64, 64, BK, 2, 2, 1, 1, 2>(p, splits, st);
-      else if (bm == 64) launch<T, MODE_WGRAD, 64, 128, BK, 2, 2, 1, 1, 2>(p, splits, st);
-      else if (bn == 64) launch<T, MODE_WGRAD, 128, 64, BK, 2, 2, 1, 1, 2>(p, splits, st);
-      else launch<T, MODE_WGRAD, 128, 128, BK, 2, 2, 1, 1, 2>(p, splits, st);
-    } else if (bm == 64 && bn == 64) launch<T, MODE_WGRAD, 64, 64, BK, 2, 2, 1, 1>(p, splits, st);
-    else if (bm == 64) launch<T, MODE_WGRAD, 64, 128, BK, 2, 2, 1, 1>(p, splits, st);
-    else if (bn == 64) launch<T, MODE_WGRAD, 128, 64, BK, 2, 2, 1, 1>(p, splits, st);
-    else launch<T, MODE_WGRAD, 128, 128, BK, 2, 2, 1, 1>(p, splits, st);
+    // LDS-DMA staging (swizzled RC images)
+    if (bm == 64 && bn == 64) launch<T, MODE_WGRAD, 64, 64, BK, 2, 2, 1, 1, 2>(p, splits, st);
+    else if (bm == 64) launch<T, MODE_WGRAD, 64, 128, BK, 2, 2, 1, 1, 2>(p, splits, st);
+    else if (bn == 64) launch<T, MODE_WGRAD, 128, 64, BK, 2, 2, 1, 1, 2>(p, splits, st);
+    else launch<T, MODE_WGRAD, 128, 128, BK, 2, 2, 1, 1, 2>(p, splits, st);
   } else {
     launch<T, MODE_WGRAD, 64, 64, BK, 2, 2, 1, 1>(p, splits, st);
   }

@@ -1311,3 +1311,40 @@ extern "C" int rtsds_confusion(const int64_t* label, const int64_t* pred, unsign
   hipLaunchKernelGGL(confusion_kernel, dim3(ew_blocks(total, 256, 1024)), dim3(256), nc * nc * 4, (hipStream_t)stream, label, pred, hist, total, nc);
   RET_LAUNCH();
 }
+
+// ------------------------------------------------------------------ SGD (flat, fused)
+// torch.optim.SGD (main.py:118-120): d = g (+ wd p); with momentum, buf = d on a parameter's
+// first step, else buf = momentum buf + (1 - dampening) d; d = nesterov ? d + momentum buf :
+// buf; p -= lr d.  hyper (device, may be NULL) = {lr, first-step flag}: the hipGraph-replay
+// variant (runtime.GraphedStep) reads them per replay.
+__global__ void sgd_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ buf,
+                           bf16* __restrict__ shadow, long n, const float* __restrict__ hyper, float lr, float momentum,
+                           float dampening, float wd, int nesterov, int first, float gscale) {
+  if (hyper) {
+    lr = hyper[0];
+    first = hyper[1] != 0.f;
+  }
+  GRID_STRIDE(i, n) {
+    float pi = p[i];
+    float d = g[i] * gscale;
+    if (wd != 0.f) d = d + wd * pi;
+    if (momentum != 0.f) {
+      const float b = first ? d : buf[i] * momentum + (1.f - dampening) * d;
+      buf[i] = b;
+      d = nesterov ? d + momentum * b : b;
+    }
+    pi = pi + (-lr) * d;
+    p[i] = pi;
+    if (shadow) shadow[i] = (bf16)pi;
+  }
+}
+
+extern "C" int rtsds_sgd_step(float* param, const float* grad, float* momentum_buf, void* bf16_shadow, long n,
+                              const float* hyper, float lr, float momentum, float dampening, float weight_decay,
+                              int nesterov, int first, float grad_scale, void* stream) {
+  if (n <= 0 || (momentum != 0.f && !momentum_buf)) return RTSDS_ERR_SHAPE;
+  hipLaunchKernelGGL(sgd_kernel, dim3(ew_blocks(n, 256, 4096)), dim3(256), 0, (hipStream_t)stream, param, grad,
+                     momentum_buf, (bf16*)bf16_shadow, n, hyper, lr, momentum, dampening, weight_decay, nesterov, first,
+                     grad_scale);
+  RET_LAUNCH();
+}

@@ -136,7 +136,10 @@ __global__ void __launch_bounds__(256, 1) hconv_fwd_kernel(const HconvArgs P) {
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
     }
-    __builtin_amdgcn_s_barrier();  // every wave is done with this buffer before it is refilled
+    // every wave is done with this buffer before it is refilled: its ds_reads retired first
+    // (a raw s_barrier does not wait for them; see gl_barrier in conv.hip)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
   }
 
@@ -250,9 +253,6 @@ static bool hconv_geom(const rtsds_conv_desc* d) {
 // at 32 x 64: 34 / 40 us fwd / dgrad vs 38 / 44 us on the implicit GEMM; layer1 / layer2
 // (64 / 128 channels, 2-4 chunks) lose to the GEMM (59 vs 41 us, 42 vs 32 us fwd).
 static bool hconv_kc_ok(int k, int c) {
-#ifdef RTSDS_HCONV_NARROW_ONLY
-  return k <= 32;
-#endif
   return k <= 32 || (k % 32 == 0 && k <= 256 && c >= 256);
 }
 bool hconv_ok(const rtsds_conv_desc* d) {

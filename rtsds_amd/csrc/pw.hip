@@ -30,9 +30,6 @@ static int pw_kp(int k) { return k <= 20 ? 20 : 32; }
 static int pw_dgrad_v(int k, int c) { return c % 2 ? 1 : (pw_kp(k) == 20 && c % 4 == 0 ? 4 : 2); }
 
 bool pw_ok(const rtsds_conv_desc* d) {
-#ifdef RTSDS_NO_PW
-  return false;
-#endif
   return d->dtype == RTSDS_BF16 && d->kh == 1 && d->kw == 1 && d->sh == 1 && d->sw == 1 && d->ph == 0 && d->pw == 0 &&
          d->k <= kPwMaxK && d->c / pw_dgrad_v(d->k, d->c) <= 256 && (long)d->n * d->h * d->w >= 4096;
 }

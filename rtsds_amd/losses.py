@@ -4,7 +4,7 @@ import torch
 from torch import nn
 
 from . import functional as F
-from .runtime import dp_world
+from .runtime import collective, dp_world
 
 
 class CrossEntropyLoss(nn.Module):
@@ -30,6 +30,13 @@ class BCEWithLogitsLoss(nn.Module):
 
     def forward(self, input, target):
         loss = F.bce_with_logits(input, target)
-        w = dp_world()
-        # global-batch mean under data parallelism (see runtime.dp_world)
-        return loss if w == 1 else loss * (1.0 / w)
+        if dp_world() == 1:
+            return loss
+        # global-batch mean under data parallelism (see runtime.dp_world): this rank's mean
+        # weighted by its share of the all-reduced element count, so shards of unequal size
+        # still sum to the gathered-batch mean (a graph-segment break under capture)
+        import torch.distributed as dist
+        n = float(input.numel())
+        cnt = torch.full((1,), n, dtype=torch.float32, device=input.device)
+        collective(lambda: dist.all_reduce(cnt))
+        return loss * (n / cnt[0])

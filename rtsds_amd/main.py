@@ -30,12 +30,13 @@ from .validation import val, val_GTA5
 
 
 def optimzer_loss_loader(model, optimizer_config, loss_config):
-    """main.py:110-136 with the HIP-backed Adam and losses."""
+    """main.py:110-136 with the HIP-backed Adam / SGD and losses."""
     if optimizer_config["name"] == "Adam":
         optimizer = optim.Adam(model.parameters(), lr=optimizer_config["lr"],
                                weight_decay=optimizer_config.get("weight_decay", 0))
     elif optimizer_config["name"] == "SGD":
-        raise ValueError("SGD is not on the rtsds hot path (the reference config uses Adam)")
+        optimizer = optim.SGD(model.parameters(), lr=optimizer_config["lr"],
+                              momentum=optimizer_config["momentum"])
     else:
         raise ValueError("Invalid optimizer name. Please select Adam or SGD")
     if loss_config["name"] == "CrossEntropy":

@@ -1,4 +1,5 @@
-"""Fused Adam over a flat parameter arena (drop-in for torch.optim.Adam, main.py:116-117).
+"""Fused Adam / SGD over a flat parameter arena (drop-ins for torch.optim.Adam / SGD,
+main.py:114-120).
 
 On first use the optimizer moves every parameter of each group into one fp32 arena
 (``p.data`` becomes a view, same shape and strides, so modules and ``state_dict`` are
@@ -8,6 +9,10 @@ same pass, refreshes the bf16 weight shadows the bf16 convs read.  With
 ``torch.distributed`` initialised (world > 1) the flat gradients are all-reduced over RCCL
 (one collective per arena) before the update and scaled by 1/world inside the kernel --
 this replaces the reference's nn.DataParallel grad reduce (utils.py:104-105).
+
+SGD (momentum / dampening / nesterov / weight decay as torch.optim.SGD) shares the arena
+with its momentum buffer in the first-moment slot.  Checkpoints use torch.optim's
+state_dict format (interchangeable with the reference's optimizers both ways).
 
 Semantics match torch.optim.Adam(amsgrad=False, maximize=False): L2 weight decay added to the
 gradient, per-parameter step counts, parameters whose gradient was not produced in a step
@@ -56,14 +61,17 @@ def allreduce_flat(buffers):
 
 
 class _Arena:
-    def __init__(self, params):
+    """One parameter group's flat fp32 buffers: parameters, gradients, first moment (Adam's
+    exp_avg / SGD's momentum buffer), second moment (Adam only) and the bf16 shadow."""
+
+    def __init__(self, params, second=True):
         dev = params[0].device
         self.params = params
         self.offsets = []
         total = 0
         for p in params:
             if p.dtype != torch.float32 or not p.is_cuda:
-                raise RuntimeError("rtsds_amd.optim.Adam: fp32 HIP parameters required")
+                raise RuntimeError("rtsds_amd.optim: fp32 HIP parameters required")
             if not (p.is_contiguous() or p.is_contiguous(memory_format=torch.channels_last)):
                 p.data = p.data.contiguous()
             self.offsets.append(total)
@@ -72,7 +80,7 @@ class _Arena:
         self.flat = torch.zeros(total, dtype=torch.float32, device=dev)
         self.gflat = torch.zeros(total, dtype=torch.float32, device=dev)
         self.m = torch.zeros(total, dtype=torch.float32, device=dev)
-        self.v = torch.zeros(total, dtype=torch.float32, device=dev)
+        self.v = torch.zeros(total, dtype=torch.float32, device=dev) if second else None
         self.shadow = torch.empty(total, dtype=torch.bfloat16, device=dev)
         self.steps = [0] * len(params)
         self.touched = [False] * len(params)
@@ -120,27 +128,84 @@ class _Arena:
         p.grad = view
 
 
-class Adam(torch.optim.Optimizer):
-    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0, amsgrad=False):
-        if amsgrad:
-            raise NotImplementedError("rtsds_amd.optim.Adam: amsgrad")
-        super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
+class _FlatOptimizer(torch.optim.Optimizer):
+    """Flat-arena optimizer core shared by Adam and SGD: the arenas, gradient sinks,
+    zero_grad, the per-step runs of touched parameters, the data-parallel all-reduce, the
+    hipGraph hyperparameter buffer, and torch-format state_dict / load_state_dict.
+    Subclasses name their per-parameter state (``_STATE``: arena buffer -> torch key) and
+    launch the update kernel for one run (``_launch``) / fill its hyper slots (``_hyper3``)."""
+
+    _STATE = ()       # ((arena attribute, torch state key), ...)
+    _NAME = "optimizer"
+
+    def __init__(self, params, defaults):
+        super().__init__(params, defaults)
         self._arenas = None
         self._warned = False
-        # hipGraph mode (runtime.GraphedStep): lr and bias corrections come from a device buffer
-        self._graph = False      # launch rtsds_adam_step_dev
+        # hipGraph mode (runtime.GraphedStep): lr (and bias corrections) from a device buffer
+        self._graph = False      # launch the _dev kernel variant
         self._capturing = False  # inside stream capture: the hyper values are staged outside
         self._runs = None        # [(group, i, j)] of the last step
-        self._hyper = None       # device fp32 [runs][lr, bc1, sqrt(bc2)]
+        self._hyper = None       # device fp32 [runs][3]
 
     # ------------------------------------------------------------------ arena
     def _ensure(self):
         if self._arenas is None:
-            self._arenas = [_Arena(list(g["params"])) for g in self.param_groups]
+            self._arenas = [_Arena(list(g["params"]), second=len(self._STATE) > 1) for g in self.param_groups]
+            self._import_state()
         return self._arenas
 
     def arenas(self):
         return self._ensure()
+
+    # ------------------------------------------------------------------ checkpoints
+    # torch.optim's state_dict format ({"state": {index: {...}}, "param_groups": [...]}), so
+    # optimizer checkpoints interchange with the reference's torch.optim.Adam / SGD
+    # (main.py:116-120) in both directions.
+    def _view(self, a, i, attr):
+        p, off = a.params[i], a.offsets[i]
+        return getattr(a, attr)[off:off + p.numel()].as_strided(p.shape, p.stride())
+
+    def _import_state(self):
+        """Move per-parameter state loaded by load_state_dict into the flat arenas."""
+        if not self.state:
+            return
+        with torch.no_grad():
+            for a in self._arenas:
+                for i, p in enumerate(a.params):
+                    st = self.state.get(p)
+                    if not st:
+                        continue
+                    for attr, key in self._STATE:
+                        if st.get(key) is not None:
+                            self._view(a, i, attr).copy_(st[key])
+                    a.steps[i] = self._imported_steps(st)
+        self.state.clear()
+
+    def _imported_steps(self, st):
+        return int(float(st["step"]))
+
+    def _exported(self, a, i):
+        st = {key: self._view(a, i, attr).detach().clone() for attr, key in self._STATE}
+        st["step"] = torch.tensor(float(a.steps[i]))
+        return st
+
+    def state_dict(self):
+        if self._arenas is not None:
+            for a in self._arenas:
+                for i, p in enumerate(a.params):
+                    if a.steps[i] > 0:
+                        self.state[p] = self._exported(a, i)
+        try:
+            return super().state_dict()
+        finally:
+            if self._arenas is not None:
+                self.state.clear()
+
+    def load_state_dict(self, state_dict):
+        super().load_state_dict(state_dict)
+        if self._arenas is not None:
+            self._import_state()
 
     def zero_grad(self, set_to_none=True):
         for a in self._ensure():
@@ -160,7 +225,7 @@ class Adam(torch.optim.Optimizer):
             for i in range(len(a.params)):
                 if a.touched[i] and not a.grad_ptr_ok(i):
                     if not self._warned:
-                        warnings.warn("rtsds_amd.Adam: gradient left the arena; copying back")
+                        warnings.warn(f"rtsds_amd.{self._NAME}: gradient left the arena; copying back")
                         self._warned = True
                     a.rebind_grad(i)
         gscale = allreduce_flat([a.gflat for a in arenas])
@@ -179,24 +244,17 @@ class Adam(torch.optim.Optimizer):
                 i = j + 1
         if self._capturing:
             if runs != self._runs or self._hyper is None:
-                raise RuntimeError("rtsds_amd.Adam: step structure changed under graph capture")
+                raise RuntimeError(f"rtsds_amd.{self._NAME}: step structure changed under graph capture")
         else:
             self._runs = runs
             if self._graph:
                 self.stage_hyper()
         for r, (gi, i, j) in enumerate(runs):
             g, a = self.param_groups[gi], arenas[gi]
-            b1, b2 = g["betas"]
             lo = a.offsets[i]
             hi = a.offsets[j] + a.params[j].numel()
-            ptrs = (a.flat.data_ptr() + 4 * lo, a.gflat.data_ptr() + 4 * lo, a.m.data_ptr() + 4 * lo,
-                    a.v.data_ptr() + 4 * lo, a.shadow.data_ptr() + 2 * lo, hi - lo)
-            if self._graph:
-                lib.rtsds_adam_step_dev(*ptrs, self._hyper.data_ptr() + 12 * r, float(b1), float(b2),
-                                        float(g["eps"]), float(g["weight_decay"]), gscale, stream())
-            else:
-                lib.rtsds_adam_step(*ptrs, float(g["lr"]), float(b1), float(b2), float(g["eps"]),
-                                    float(g["weight_decay"]), a.steps[i] + 1, gscale, stream())
+            hyper = self._hyper.data_ptr() + 12 * r if self._graph else None
+            self._launch(g, a, lo, hi, a.steps[i] + 1, hyper, gscale)
             for k in range(i, j + 1):
                 a.steps[k] += 1
         return loss
@@ -206,23 +264,23 @@ class Adam(torch.optim.Optimizer):
         self._graph = bool(on)
 
     def stage_hyper(self):
-        """Write (lr, 1 - beta1^t, sqrt(1 - beta2^t)) of the NEXT step of every run of the last
-        step into the device hyper buffer (stream-ordered H2D copy from pinned memory)."""
+        """Write the hyperparameters of the NEXT step of every run of the last step into the
+        device hyper buffer (stream-ordered H2D copy from pinned memory)."""
         runs = self._runs or []
         arenas = self._ensure()
         vals = torch.empty(max(1, 3 * len(runs)), dtype=torch.float32, pin_memory=True)
         for r, (gi, i, _) in enumerate(runs):
-            g = self.param_groups[gi]
-            # betas rounded to fp32 first, exactly as rtsds_adam_step receives them (eager and
-            # replayed steps then update bit-identically)
-            b1, b2 = (float(torch.tensor(b, dtype=torch.float32)) for b in g["betas"])
-            t = arenas[gi].steps[i] + 1
-            vals[3 * r] = float(g["lr"])
-            vals[3 * r + 1] = 1.0 - b1 ** t
-            vals[3 * r + 2] = (1.0 - b2 ** t) ** 0.5
+            vals[3 * r:3 * r + 3] = torch.tensor(self._hyper3(self.param_groups[gi], arenas[gi].steps[i] + 1))
         if self._hyper is None or self._hyper.numel() < vals.numel():
             self._hyper = torch.empty(vals.numel(), dtype=torch.float32, device=arenas[0].flat.device)
         self._hyper[:vals.numel()].copy_(vals, non_blocking=True)
+
+    def steps_snapshot(self):
+        return [list(a.steps) for a in self._ensure()]
+
+    def restore_steps(self, snap):
+        for a, st in zip(self._ensure(), snap):
+            a.steps[:] = st
 
     def advance_steps(self, by=1):
         """Host step counters after a replayed step (the graph does not run Python)."""
@@ -230,3 +288,75 @@ class Adam(torch.optim.Optimizer):
         for gi, i, j in self._runs or []:
             for k in range(i, j + 1):
                 arenas[gi].steps[k] += by
+
+
+def _ptrs(a, lo, hi, *attrs):
+    return tuple(getattr(a, at).data_ptr() + 4 * lo for at in attrs)
+
+
+class Adam(_FlatOptimizer):
+    """torch.optim.Adam (main.py:116-117) as one rtsds_adam_step launch per run."""
+
+    _STATE = (("m", "exp_avg"), ("v", "exp_avg_sq"))
+    _NAME = "Adam"
+
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0, amsgrad=False):
+        if amsgrad:
+            raise NotImplementedError("rtsds_amd.optim.Adam: amsgrad")
+        super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
+
+    def _launch(self, g, a, lo, hi, t, hyper, gscale):
+        b1, b2 = g["betas"]
+        ptrs = _ptrs(a, lo, hi, "flat", "gflat", "m", "v") + (a.shadow.data_ptr() + 2 * lo, hi - lo)
+        if hyper is not None:
+            lib.rtsds_adam_step_dev(*ptrs, hyper, float(b1), float(b2), float(g["eps"]),
+                                    float(g["weight_decay"]), gscale, stream())
+        else:
+            lib.rtsds_adam_step(*ptrs, float(g["lr"]), float(b1), float(b2), float(g["eps"]),
+                                float(g["weight_decay"]), t, gscale, stream())
+
+    def _hyper3(self, g, t):
+        # betas rounded to fp32 first, exactly as rtsds_adam_step receives them (eager and
+        # replayed steps then update bit-identically)
+        b1, b2 = (float(torch.tensor(b, dtype=torch.float32)) for b in g["betas"])
+        return [float(g["lr"]), 1.0 - b1 ** t, (1.0 - b2 ** t) ** 0.5]
+
+
+class SGD(_FlatOptimizer):
+    """torch.optim.SGD (main.py:118-120: lr, momentum; weight_decay, dampening and nesterov
+    as torch) as one rtsds_sgd_step launch per run.  The momentum buffer is the arena's
+    first-moment buffer; a parameter's first step initialises it with the gradient (torch's
+    ``momentum_buffer is None`` branch)."""
+
+    _STATE = (("m", "momentum_buffer"),)
+    _NAME = "SGD"
+
+    def __init__(self, params, lr=1e-3, momentum=0, dampening=0, weight_decay=0, nesterov=False,
+                 maximize=False):
+        if maximize:
+            raise NotImplementedError("rtsds_amd.optim.SGD: maximize")
+        if nesterov and (momentum <= 0 or dampening != 0):
+            raise ValueError("Nesterov momentum requires a momentum and zero dampening")
+        super().__init__(params, dict(lr=lr, momentum=momentum, dampening=dampening,
+                                      weight_decay=weight_decay, nesterov=nesterov))
+
+    def _launch(self, g, a, lo, hi, t, hyper, gscale):
+        lib.rtsds_sgd_step(*_ptrs(a, lo, hi, "flat", "gflat", "m"), a.shadow.data_ptr() + 2 * lo, hi - lo,
+                           hyper, float(g["lr"]), float(g["momentum"]), float(g["dampening"]),
+                           float(g["weight_decay"]), int(bool(g["nesterov"])), int(t == 1), gscale, stream())
+
+    def _hyper3(self, g, t):
+        return [float(g["lr"]), 1.0 if t == 1 else 0.0, 0.0]
+
+    def _exported(self, a, i):
+        # torch.optim.SGD keeps no step count; momentum_buffer only when momentum != 0
+        st = {}
+        if self.param_groups[self._arenas.index(a)]["momentum"] != 0:
+            st["momentum_buffer"] = self._view(a, i, "m").detach().clone()
+        st["step"] = torch.tensor(float(a.steps[i]))  # extra key, ignored by torch.optim.SGD
+        return st
+
+    def _imported_steps(self, st):
+        if "step" in st:
+            return int(float(st["step"]))
+        return 1 if st.get("momentum_buffer") is not None else 0

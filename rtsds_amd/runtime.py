@@ -220,6 +220,9 @@ class GraphedStep:
         self.segments = []  # [(graph, collective run after it or None)]
         self._pool = torch.cuda.graph_pool_handle()
         cap_stream = torch.cuda.Stream(device=cur.device)
+        # the capture runs the optimizers' Python bookkeeping (step counters) without executing
+        # a step: their counters are restored afterwards, also when the capture fails part-way
+        saved = [o.steps_snapshot() for o in self.optimizers]
         for o in self.optimizers:
             o._capturing = True
         try:
@@ -234,13 +237,11 @@ class GraphedStep:
                     self._graph.capture_end()
                 self.segments.append((self._graph, None))
         finally:
-            for o in self.optimizers:
+            for o, st in zip(self.optimizers, saved):
                 o._capturing = False
+                o.restore_steps(st)
         cur.wait_stream(cap_stream)
         self.graph = self.segments[0][0]
-        # the capture ran the optimizers' Python bookkeeping once without executing a step
-        for o in self.optimizers:
-            o.advance_steps(-1)
 
     def _break(self, coll):
         self._graph.capture_end()

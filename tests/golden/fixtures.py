@@ -54,9 +54,15 @@ def check_tensor(arrays, meta, name, t, rtol, atol=0.0):
 
 
 def check_params(arrays, meta, name, tensors, rtol, atol=0.0):
+    """Every key of the fixture must be present in ``tensors`` and vice versa (a renamed or
+    dropped parameter fails); a fixture entry of None (the reference produced no gradient)
+    requires None or an all-zero tensor."""
+    missing = sorted(set(meta[name]) ^ set(tensors))
+    assert not missing, (name, "key sets differ", missing[:8])
     for key, t in tensors.items():
-        m = meta[name].get(key)
+        m = meta[name][key]
         if m is None:
+            assert t is None or float(t.detach().abs().max()) == 0.0, (name, key, "expected no gradient")
             continue
         got = samples_of(t, PSAMPLES, 1)
         ref = arrays[name + ":" + key].astype(np.float64)

@@ -112,6 +112,8 @@ def main():
     if only:
         if "da2" in only:
             make_da2(ref_train, BiSeNet, TinyDomainDiscriminator)
+        if "extras" in only:
+            make_extras(BiSeNet, DomainDiscriminator)
         return
 
     keys = {}
@@ -218,6 +220,58 @@ def main():
     with open(os.path.join(HERE, "state_dict_keys.json"), "w") as f:
         json.dump(keys, f)
     print("wrote state_dict_keys.json")
+    make_extras(BiSeNet, DomainDiscriminator)
+
+
+def make_extras(BiSeNet, DomainDiscriminator):
+    """API surface beyond the C1 captures: BiSeNet with the ResNet-101 context path
+    (build_contextpath.py:32-57), DomainDiscriminator(with_grl=True) (model.py:9-17, 61-62)
+    and UpSampler (model.py:19-28).  Keys of the R101 model go to state_dict_keys_r101.json."""
+    from models.domain_shift.adversarial.model import UpSampler
+    torch.manual_seed(42)
+    arrays, meta = {}, {}
+    g = apply_recipe(BiSeNet(19, "resnet101"), seed=4)
+    with open(os.path.join(HERE, "state_dict_keys_r101.json"), "w") as f:
+        json.dump([[k, list(v.shape)] for k, v in g.state_dict().items()], f)
+    x = synthetic_images(2, 64, 128, seed=49)
+    y = synthetic_labels(2, 64, 128, seed=50)
+    g.train()
+    out, a1, a2 = g(x)
+    ce = torch.nn.CrossEntropyLoss(ignore_index=19)
+    loss = ce(out, y) + ce(a1, y) + ce(a2, y)
+    loss.backward()
+    meta["r101_loss"] = float(loss)
+    for nm, t in (("r101_out", out), ("r101_aux1", a1), ("r101_aux2", a2)):
+        summarize(arrays, meta, nm, t.detach())
+    arrays["r101_out_argmax"] = out.detach().argmax(1).to(torch.uint8).numpy()
+    param_summary(arrays, meta, "r101_grad", {k: p.grad for k, p in g.named_parameters()})
+    g.eval()
+    with torch.no_grad():
+        summarize(arrays, meta, "r101_eval_out", g(x))
+
+    # gradient reversal: D(with_grl=True) has the same forward and the negated, lambda-scaled
+    # input gradient; its own parameter gradients are NOT reversed (the GRL sits after them)
+    z = torch.randn(2, 19, 64, 128, generator=torch.Generator().manual_seed(7))
+    D = apply_recipe(DomainDiscriminator(19, with_grl=True, lambda_=0.1), seed=2)
+    zi = z.clone().requires_grad_(True)
+    p = D(torch.softmax(zi, 1))
+    l = torch.nn.BCEWithLogitsLoss()(p, torch.ones_like(p))
+    l.backward()
+    arrays["grl_pred"] = p.detach().numpy()
+    meta["grl_loss"] = float(l)
+    summarize(arrays, meta, "grl_dz", zi.grad)
+    param_summary(arrays, meta, "grl_grad", {k: q.grad for k, q in D.named_parameters()})
+
+    # UpSampler: x8 bilinear (align_corners=False) then 1x1 conv with bias
+    up = apply_recipe(UpSampler(19), seed=5)
+    u = torch.randn(2, 19, 16, 32, generator=torch.Generator().manual_seed(8)).requires_grad_(True)
+    o = up(u)
+    w = torch.randn(o.shape, generator=torch.Generator().manual_seed(9))
+    (o * w).sum().backward()
+    summarize(arrays, meta, "up_out", o.detach())
+    summarize(arrays, meta, "up_du", u.grad)
+    param_summary(arrays, meta, "up_grad", {k: q.grad for k, q in up.named_parameters()})
+    save("extras", arrays, meta)
 
 
 def make_da2(ref_train, BiSeNet, TinyDomainDiscriminator):

@@ -106,3 +106,135 @@ def test_two_rank_seg_step_equals_gathered_batch(tmp_path):
     # gradients may flip a few of those moves
     assert worst <= 2.05 * lr, worst
     assert bad <= 1e-3 * n, (bad, n)
+
+
+# ----------------------------------------------------------------------------- DA iteration
+def _da_data():
+    from oracle.weights import synthetic_images, synthetic_labels
+    # unequal shards: rank 0 gets 2 source + 2 target images, rank 1 gets 3 + 3 (as the
+    # reference's DataParallel scatters an odd batch; BCE and CE must use the GLOBAL counts)
+    x = synthetic_images(5, 64, 128, seed=42)
+    y = synthetic_labels(5, 64, 128, seed=43)
+    y[:2][torch.rand(y[:2].shape, generator=torch.Generator().manual_seed(5)) < 0.5] = 19
+    xt = synthetic_images(5, 64, 128, seed=46)
+    return x, y, xt
+
+
+SHARDS = ((0, 2), (2, 5))
+
+
+def _models():
+    from oracle.weights import recipe_state_dict
+    from rtsds_amd.models.domain_shift.adversarial.model import TinyDomainDiscriminator
+    g = _model()
+    d = TinyDomainDiscriminator(19)
+    sd = d.state_dict()
+    d.load_state_dict(recipe_state_dict({k: tuple(v.shape) for k, v in sd.items()}, 2))
+    return g, d.to(DEV).train()
+
+
+def _da_worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    import torch.distributed as dist
+    import rtsds_amd
+    from rtsds_amd import losses, optim
+    from rtsds_amd.train import da_step
+    dist.init_process_group("gloo")
+    try:
+        x, y, xt = _da_data()
+        lo, hi = SHARDS[rank]
+        with rtsds_amd.precision(torch.float32):
+            g, d = _models()
+            og = optim.Adam(g.parameters(), lr=1e-4)
+            od = optim.Adam(d.parameters(), lr=1e-4, weight_decay=1e-4)
+            res = da_step(g, d, og, od, losses.CrossEntropyLoss(ignore_index=19), losses.BCEWithLogitsLoss(),
+                          x[lo:hi].to(DEV), y[lo:hi].to(DEV), xt[lo:hi].to(DEV), 0.1, 2)
+            t = torch.stack([v.double().reshape(()) for v in res])
+            dist.all_reduce(t)
+        if rank == 0:
+            torch.save({"logs": t.cpu(),
+                        "g": {k: v.detach().cpu() for k, v in g.named_parameters()},
+                        "d": {k: v.detach().cpu() for k, v in d.named_parameters()}}, out)
+    finally:
+        dist.destroy_process_group()
+
+
+def _gathered_da_step(g, d, og, od, x, y, xt, lam, it):
+    """adversarial_train's iteration (train.py:174-275) under nn.DataParallel on the gathered
+    batch: every module runs per replica on its shard (per-replica BatchNorm statistics), the
+    outputs are gathered and each loss is one mean over the whole batch."""
+    import rtsds_amd.functional as F
+    from rtsds_amd import losses
+    bce = losses.BCEWithLogitsLoss()
+    cat = lambda ts: torch.cat(ts).contiguous(memory_format=torch.channels_last)  # noqa: E731
+    og.zero_grad()
+    od.zero_grad()
+    for p in d.parameters():
+        p.requires_grad = False
+    correct = torch.zeros(1, dtype=torch.int64, device=DEV)
+    parts = [g.forward_lowres(x[lo:hi]) for lo, hi in SHARDS]
+    geo = parts[0][0][1]
+    heads = [cat([p[h][0] for p in parts]) for h in range(3)]
+    loss_seg = F.upsample_cross_entropy(heads, y, geo, 19, correct) / it
+    loss_seg.backward()
+    src = F.interpolate_geometry(heads[0].detach(), geo)
+    tparts = []
+    for lo, hi in SHARDS:
+        (t, tg), = g.forward_lowres(xt[lo:hi], main_only=True)
+        tparts.append(F.interpolate_geometry(t, tg))
+    pred_t = cat([d(F.softmax(t, dim=1)) for t in tparts])
+    loss_adv = lam * bce(pred_t, torch.ones(pred_t.shape, device=DEV)) / it
+    loss_adv.backward()
+    for p in d.parameters():
+        p.requires_grad = True
+    pred_s = cat([d(F.softmax(src[lo:hi], dim=1)) for lo, hi in SHARDS])
+    loss_ds = bce(pred_s, torch.ones(pred_s.shape, device=DEV)) / it
+    loss_ds.backward()
+    pred_t2 = cat([d(F.softmax(t.detach(), dim=1)) for t in tparts])
+    loss_dt = bce(pred_t2, torch.zeros(pred_t2.shape, device=DEV)) / it
+    loss_dt.backward()
+    og.step()
+    od.step()
+    return [float(v) for v in (loss_seg, loss_adv, loss_ds, loss_dt)] + [int(correct)]
+
+
+def test_two_rank_da_step_equals_gathered_batch(tmp_path):
+    """A sharded adversarial_train iteration (2 ranks, UNEQUAL shards of 2 and 3 source +
+    target images) equals the DataParallel iteration on the gathered batch: the four losses,
+    the pixel-accuracy count, and G and D after both Adam steps (D gradients summed over
+    ranks, BCE over the global element count, the frozen-D adversarial gradient into G)."""
+    out = str(tmp_path / "rank0_da.pt")
+    ctx = mp.get_context("spawn")
+    port = _port()
+    procs = [ctx.Process(target=_da_worker, args=(r, 2, port, out)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=300)
+        assert p.exitcode == 0
+    got = torch.load(out, weights_only=True)
+
+    import rtsds_amd
+    from rtsds_amd import optim
+    x, y, xt = _da_data()
+    with rtsds_amd.precision(torch.float32):
+        g, d = _models()
+        og = optim.Adam(g.parameters(), lr=1e-4)
+        od = optim.Adam(d.parameters(), lr=1e-4, weight_decay=1e-4)
+        want = _gathered_da_step(g, d, og, od, x.to(DEV), y.to(DEV), xt.to(DEV), 0.1, 2)
+    logs = got["logs"].tolist()
+    for i, nm in enumerate(("loss_seg", "loss_adv", "loss_dsrc", "loss_dtgt")):
+        assert abs(logs[i] - want[i]) <= 1e-5 * abs(want[i]) + 1e-9, (nm, logs[i], want[i])
+    assert int(logs[4]) == want[4]
+    lr = 1e-4
+    for name, mod in (("g", g), ("d", d)):
+        n = bad = 0
+        worst = 0.0
+        for k, p in mod.named_parameters():
+            dlt = (got[name][k] - p.detach().cpu()).abs()
+            n += dlt.numel()
+            bad += int((dlt > 1e-6).sum())
+            worst = max(worst, float(dlt.max()))
+        assert worst <= 2.05 * lr, (name, worst)
+        assert bad <= 1e-3 * n, (name, bad, n)

@@ -58,6 +58,7 @@ CONV_CASES = [
     (1, 64, 12, 64, 32, 3, 1, 1, 1, True),     # hconv with bias, Cout 32, edge tiles on 3 row-blocks
     (1, 256, 8, 64, 64, 3, 1, 1, 1, True),     # hconv N-tiled (Cin >= 256, Cout 2 x 32), fwd and dgrad
     (2, 512, 16, 32, 512, 3, 1, 1, 1, False),  # layer4-like: DGRAD split-K (128x128 tiles, fp32 slabs)
+    (2, 512, 16, 32, 512, 3, 1, 2, 2, False),  # dilated (DeepLab layer3-like, small M): DGRAD split-K
     (2, 512, 32, 64, 19, 1, 1, 0, 1, True),    # supervision 1x1 (pw.hip backward): 1 row group
     (2, 40, 32, 64, 32, 1, 1, 0, 1, True),     # pw.hip: Cout 32, 12 row groups
     (4, 19, 32, 32, 19, 1, 1, 0, 1, True),     # pw.hip: final 19->19, odd Cin (scalar lanes)
