@@ -369,10 +369,29 @@ def batch_norm(x, gamma, beta, running_mean, running_var, training, momentum, ep
 
 # ----------------------------------------------------------------------------- layout / dtype
 def pack_input(x, dtype):
-    """NCHW fp32 image batch (reference loaders) -> NHWC compute dtype.  No gradient."""
+    """NCHW fp32 batch (reference loaders, reference-layout activations) -> NHWC compute dtype.
+    Differentiable when ``x`` requires grad (discriminator / UpSampler inputs): the gradient
+    goes back as the NHWC tensor cast to x's dtype (same logical NCHW shape)."""
     require_hip(x)
     if x.dtype == dtype and x.dim() == 4 and x.is_contiguous(memory_format=CL) and x.shape[1] > 1:
         return x
+    if x.requires_grad and torch.is_grad_enabled():
+        return PackInputFn.apply(x, dtype)
+    return _pack(x, dtype)
+
+
+class PackInputFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, dtype):
+        ctx.xdtype = x.dtype
+        return _pack(x, dtype)
+
+    @staticmethod
+    def backward(ctx, dy):
+        return cast(nhwc(dy), ctx.xdtype), None
+
+
+def _pack(x, dtype):
     xf = x if x.dtype == torch.float32 else cast(x, torch.float32)
     xf = xf.contiguous()
     n, c, h, w = xf.shape

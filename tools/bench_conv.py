@@ -1,5 +1,5 @@
 """Micro-benchmark of one conv layer (fwd + dgrad + wgrad through the HIP ABI) for
-rocprofv3 counter runs.  usage: bench_conv.py N C H W K KH STRIDE PAD [iters]"""
+rocprofv3 counter runs.  usage: bench_conv.py N C H W K KH STRIDE PAD [iters] [dilation]"""
 import ctypes
 import os
 import sys
@@ -14,11 +14,12 @@ from rtsds_amd.runtime import workspace  # noqa: E402
 
 n, c, h, w, k, kh, s, p = [int(v) for v in sys.argv[1:9]]
 iters = int(sys.argv[9]) if len(sys.argv) > 9 else 20
+dil = int(sys.argv[10]) if len(sys.argv) > 10 else 1
 dev = "cuda"
 CL = torch.channels_last
 x = torch.randn(n, c, h, w, device=dev).to(torch.bfloat16).contiguous(memory_format=CL)
 wt = (torch.randn(k, c, kh, kh, device=dev) * 0.05).to(torch.bfloat16).contiguous(memory_format=CL)
-d = F._conv_desc(x, k, kh, kh, (s, s), (p, p), (1, 1))
+d = F._conv_desc(x, k, kh, kh, (s, s), (p, p), (dil, dil))
 y = torch.empty(n, k, d.ho, d.wo, device=dev, dtype=torch.bfloat16).contiguous(memory_format=CL)
 dy = torch.randn_like(y)
 dx = torch.empty_like(x)
@@ -41,4 +42,4 @@ for name, fn in (
         fn()
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / iters
-    print(f"{name:5s} {dt * 1e6:8.1f} us  {flop / dt / 1e12:7.1f} TF/s")
+    print(f"{' '.join(sys.argv[1:9])} d{dil} {name:5s} {dt * 1e6:8.1f} us  {flop / dt / 1e12:7.1f} TF/s", flush=True)
