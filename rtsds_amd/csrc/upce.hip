@@ -29,6 +29,7 @@
 #include <cmath>
 
 static const int kUpceCMax = 32;
+typedef float f2 __attribute__((ext_vector_type(2)));
 #ifndef UPCE_ROWS
 #define UPCE_ROWS 32.f  // full-res rows per tile (one wave walks them)
 #endif
@@ -121,16 +122,29 @@ __global__ void __launch_bounds__(256, 3) upce_fwd_kernel(UpceArgs a) {
   float* xm1 = xm0 + q.wmax;
   int* xs = (int*)(xm1 + q.wmax);
   int* xe = xs + TW1;
-  float* hbase = (float*)(xe + TW1);
+  // per-head buffers 16-B aligned (packed 8-B LDS accesses)
+  float* hbase = smem + ((TW1 * q.wmax + 4 * q.wmax + 2 * TW1 + 3) & ~3);
   const int per_head = ltile + 64 * CP;
   // labels of the tile's pixels as bytes (class, 254 = ignore_index, 253 = out of range),
   // staged once for all heads: the row loop then never waits on a global load
   unsigned char* lab = (unsigned char*)(hbase + a.nheads * per_head);
   const int Ht = min(y_hi - y_lo, q.hmax);
-  for (int e = tid; e < Ht * Wt; e += nthr) {
-    const int yy = e / Wt, xx = e - yy * Wt;
-    const long t = a.tgt[((long)img * q.H + y_lo + yy) * q.W + x_lo + xx];
-    lab[e] = t == a.ignore ? 254 : ((t >= 0 && t < C) ? (unsigned char)t : 253);
+  // 8 label loads in flight per thread before any LDS store (the loads are the prologue's
+  // latency, not its bandwidth)
+  for (int e0 = tid; e0 < Ht * Wt; e0 += 8 * nthr) {
+    long tv[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int e = e0 + u * nthr;
+      const int yy = e / Wt, xx = e - yy * Wt;
+      tv[u] = e < Ht * Wt ? a.tgt[((long)img * q.H + y_lo + yy) * q.W + x_lo + xx] : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int e = e0 + u * nthr;
+      const long t = tv[u];
+      if (e < Ht * Wt) lab[e] = t == a.ignore ? 254 : ((t >= 0 && t < C) ? (unsigned char)t : 253);
+    }
   }
 
   for (int xx = tid; xx < Wt; xx += nthr) {
@@ -159,12 +173,19 @@ __global__ void __launch_bounds__(256, 3) upce_fwd_kernel(UpceArgs a) {
   for (int hh = 0; hh < a.nheads; ++hh) {
     const T* X = (const T*)a.x[hh] + (long)img * q.hl * q.wl * C;
     float* lt = hbase + hh * per_head;
-    for (int e = tid; e < ltile; e += nthr) {
-      const int cc = e % CP, cell = e / CP;
-      const int il = cell / TW1, jl = cell - il * TW1;
-      float v = cc < C ? 0.f : -1e30f;
-      if (cc < C && il < rows_l && jl < cols_l) v = to_f(X[((long)(r0 + il) * q.wl + (c0 + jl)) * C + cc]);
-      lt[e] = v;
+    for (int e0 = tid; e0 < ltile; e0 += 8 * nthr) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int e = e0 + u * nthr;
+        const int cc = e % CP, cell = e / CP;
+        const int il = cell / TW1, jl = cell - il * TW1;
+        v[u] = cc < C ? 0.f : -1e30f;
+        if (e < ltile && cc < C && il < rows_l && jl < cols_l) v[u] = to_f(X[((long)(r0 + il) * q.wl + (c0 + jl)) * C + cc]);
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (e0 + u * nthr < ltile) lt[e0 + u * nthr] = v[u];
     }
   }
   __syncthreads();
@@ -174,6 +195,7 @@ __global__ void __launch_bounds__(256, 3) upce_fwd_kernel(UpceArgs a) {
   float* xrow = hbase + h * per_head + ltile;
   float* gdst = a.want_grad ? a.gpart[h] + (long)blockIdx.x * tile_el : nullptr;
   const float kL2E = 1.4426950408889634f, kLN2 = 0.6931471805599453f;
+  constexpr int CP2 = CP / 2;
   float lsum = 0.f, cnt = 0.f;
   unsigned long long corr = 0;
 
@@ -185,9 +207,9 @@ __global__ void __launch_bounds__(256, 3) upce_fwd_kernel(UpceArgs a) {
     const float m0 = xm0[xc], m1 = xm1[xc];
     const int xend = min(xb + 63, Wt - 1);
     const bool add = xb > 0;  // later column chunks add into the rows the first one wrote
-    float H0[CP], H1[CP], Rlo[CP], Rhi[CP];
+    f2 H0[CP2], H1[CP2], Rlo[CP2], Rhi[CP2];
 #pragma unroll
-    for (int k = 0; k < CP; ++k) { Rlo[k] = 0.f; Rhi[k] = 0.f; }
+    for (int k = 0; k < CP2; ++k) { Rlo[k] = (f2){0.f, 0.f}; Rhi[k] = (f2){0.f, 0.f}; }
     int pj[3], pc[3], plo[3], phi[3];  // this lane's x-fold pairs (low-res column, class)
 #pragma unroll
     for (int u = 0; u < 3; ++u) {
@@ -197,16 +219,17 @@ __global__ void __launch_bounds__(256, 3) upce_fwd_kernel(UpceArgs a) {
       plo[u] = max(xs[pj[u]], xb);
       phi[u] = min(xe[pj[u]], xend);
     }
-    auto hblend = [&](int li, float* H) {
-      const float* L = lt + li * rowp;
+    auto hblend = [&](int li, f2* H) {
+      const f2* L0 = (const f2*)(lt + li * rowp + j0 * CP);
+      const f2* L1 = (const f2*)(lt + li * rowp + j1 * CP);
 #pragma unroll
-      for (int k = 0; k < CP; ++k) H[k] = fmaf(m1, L[j1 * CP + k], m0 * L[j0 * CP + k]);
+      for (int k = 0; k < CP2; ++k) H[k] = __builtin_elementwise_fma((f2){m1, m1}, L1[k], (f2){m0, m0} * L0[k]);
     };
     // x-fold of finished low-res row il (all lanes of the wave take part)
-    auto emit = [&](int il, const float* R) {
+    auto emit = [&](int il, const f2* R) {
       if (xv) {
 #pragma unroll
-        for (int k = 0; k < CP; ++k) xrow[lane * CP + k] = R[k];
+        for (int k = 0; k < CP2; ++k) *(f2*)(xrow + lane * CP + 2 * k) = R[k];
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // LDS only: the row's global stores stay in flight
       __builtin_amdgcn_wave_barrier();
@@ -243,71 +266,78 @@ __global__ void __launch_bounds__(256, 3) upce_fwd_kernel(UpceArgs a) {
         float l0, l1;
         bil_src(y, q.sh, q.hl, i0, i1, l0, l1);
         if (!xv) continue;
-        float z[CP];
-#pragma unroll
-        for (int k = 0; k < CP; ++k) z[k] = fmaf(l1, H1[k], l0 * H0[k]);
-        // max as a 4-way interleaved tree (dependent-chain depth CP/4 + 2 instead of CP)
-        float mq[4] = {z[0], z[1], z[2], z[3]};
-#pragma unroll
-        for (int k = 4; k < CP; ++k) mq[k & 3] = fmaxf(mq[k & 3], z[k]);
-        const float mx = fmaxf(fmaxf(mq[0], mq[1]), fmaxf(mq[2], mq[3]));
         const bool in_range = tb < 253;
-        const int t = in_range ? tb : (tb == 254 ? a.ignore : -1);
-        // z[t] recomputed from the LDS tile with the same expression (no register indexing)
-        const int tq = in_range ? tb : 0;
-        const float h0 = fmaf(m1, L0[j1 * CP + tq], m0 * L0[j0 * CP + tq]);
-        const float h1 = fmaf(m1, L1[j1 * CP + tq], m0 * L1[j0 * CP + tq]);
-        const float zt = in_range ? fmaf(l1, h1, l0 * h0) : NAN;
         const bool valid = tb != 254;
-        // softmax with the hardware exp2 / log2 / rcp (v_exp_f32, v_log_f32, v_rcp_f32)
-        const float mxs = mx * kL2E;
-        int bi = 0;  // argmax before z is overwritten
+        // z[t] from the LDS tile with the same expression as z (no register indexing); its
+        // loads are issued first so their latency hides behind the logits
+        const int tq = in_range ? tb : 0;
+        const float a00 = L0[j1 * CP + tq], a01 = L0[j0 * CP + tq], a10 = L1[j1 * CP + tq], a11 = L1[j0 * CP + tq];
+        // logits, packed: z = l1 * H1 + l0 * H0 (the expression of rtsds_bilinear_fwd)
+        f2 z[CP2];
+#pragma unroll
+        for (int k = 0; k < CP2; ++k) z[k] = __builtin_elementwise_fma((f2){l1, l1}, H1[k], (f2){l0, l0} * H0[k]);
+        float mq[3] = {fmaxf(z[0].x, z[0].y), z[1].x, z[1].y};
+#pragma unroll
+        for (int k = 2; k < CP2; ++k) mq[k % 3] = fmaxf(mq[k % 3], fmaxf(z[k].x, z[k].y));
+        const float mx = fmaxf(fmaxf(mq[0], mq[1]), mq[2]);
+        int bi = 0;  // argmax (head 0) before z is overwritten
         if (h == 0 && a.correct) {
 #pragma unroll
-          for (int k = CP - 1; k >= 0; --k) bi = z[k] == mx ? k : bi;
+          for (int k = CP2 - 1; k >= 0; --k) {
+            bi = z[k].y == mx ? 2 * k + 1 : bi;
+            bi = z[k].x == mx ? 2 * k : bi;
+          }
         }
-        float sq[4] = {0.f, 0.f, 0.f, 0.f};
+        // softmax with the hardware exp2 / log2 / rcp (v_exp_f32, v_log_f32, v_rcp_f32)
+        const float mxs = mx * kL2E;
+        f2 sq = {0.f, 0.f};
 #pragma unroll
-        for (int k = 0; k < CP; ++k) {  // z -> exp(z - max) in place
-          z[k] = __builtin_amdgcn_exp2f(fmaf(z[k], kL2E, -mxs));
-          sq[k & 3] += z[k];
+        for (int k = 0; k < CP2; ++k) {  // z -> exp(z - max) in place
+          const f2 ar = __builtin_elementwise_fma(z[k], (f2){kL2E, kL2E}, (f2){-mxs, -mxs});
+          z[k] = (f2){__builtin_amdgcn_exp2f(ar.x), __builtin_amdgcn_exp2f(ar.y)};
+          sq += z[k];
         }
-        const float se = (sq[0] + sq[1]) + (sq[2] + sq[3]);
+        const float se = sq.x + sq.y;
         if (h == 0 && a.correct) {  // first maximum wins (torch argmax; a NaN logit wins)
           if (__builtin_amdgcn_ballot_w64(se != se)) {  // wave-uniform: only with NaN logits
-            float best = fmaf(l1, H1[0], l0 * H0[0]);
+            float best = fmaf(l1, H1[0].x, l0 * H0[0].x);
             int bn = 0;
             for (int k = 1; k < CP; ++k) {
-              const float zk = fmaf(l1, H1[k], l0 * H0[k]);
+              const float zk = fmaf(l1, ((const float*)H1)[k], l0 * ((const float*)H0)[k]);
               if (zk > best || (zk != zk && best == best)) { best = zk; bn = k; }
             }
             bi = se != se ? bn : bi;
           }
+          const int t = in_range ? tb : (tb == 254 ? a.ignore : -1);
           corr += (t == bi) ? 1ull : 0ull;  // t = ignore_index (or -1): never a class index < C
         }
+        const float h0 = fmaf(m1, a00, m0 * a01);
+        const float h1 = fmaf(m1, a10, m0 * a11);
+        const float zt = in_range ? fmaf(l1, h1, l0 * h0) : NAN;
         lsum += valid ? fmaf(__builtin_amdgcn_logf(se), kLN2, mx) - zt : 0.f;
         if (h == 0) cnt += valid ? 1.f : 0.f;
         if (a.want_grad) {
+          // g = softmax - onehot(t), folded vertically into the two low-res rows (packed FMAs)
           const float is = valid ? __builtin_amdgcn_rcpf(se) : 0.f;
           const int th1 = (valid && in_range) ? tb : -1;
+          const f2 isv = {is, is}, l0v = {l0, l0}, l1v = {l1, l1};
 #pragma unroll
-          for (int k = 0; k < CP; ++k) z[k] = fmaf(z[k], is, th1 == k ? -1.f : 0.f);  // g in place
-          if (same) {  // group-uniform
-#pragma unroll
-            for (int k = 0; k < CP; ++k) Rlo[k] = fmaf(l1, z[k], fmaf(l0, z[k], Rlo[k]));
-          } else {
-#pragma unroll
-            for (int k = 0; k < CP; ++k) {
-              Rlo[k] = fmaf(l0, z[k], Rlo[k]);
-              Rhi[k] = fmaf(l1, z[k], Rhi[k]);
-            }
+          for (int k = 0; k < CP2; ++k) {
+            const f2 oh = {th1 == 2 * k ? -1.f : 0.f, th1 == 2 * k + 1 ? -1.f : 0.f};
+            const f2 g = __builtin_elementwise_fma(z[k], isv, oh);
+            Rlo[k] = __builtin_elementwise_fma(l0v, g, Rlo[k]);
+            Rhi[k] = __builtin_elementwise_fma(l1v, g, Rhi[k]);
           }
         }
       }
       if (a.want_grad) {  // row li is complete
+        if (same) {
+#pragma unroll
+          for (int k = 0; k < CP2; ++k) { Rlo[k] += Rhi[k]; Rhi[k] = (f2){0.f, 0.f}; }
+        }
         emit(li, Rlo);
 #pragma unroll
-        for (int k = 0; k < CP; ++k) { Rlo[k] = Rhi[k]; Rhi[k] = 0.f; }
+        for (int k = 0; k < CP2; ++k) { Rlo[k] = Rhi[k]; Rhi[k] = (f2){0.f, 0.f}; }
       }
       ya = yb;
     }
@@ -431,8 +461,8 @@ static bool upce_plan(int n, int hl, int wl, int c, int H, int W, float sh, floa
 static int upce_cp(int c) { return (c + 3) / 4 * 4; }
 static size_t upce_lds(const UpceGeo& g, int nheads) {
   const size_t cp = upce_cp(g.c), tile_el = (size_t)(g.th + 1) * (g.tw + 1) * cp;
-  return ((size_t)(g.tw + 1) * g.wmax + 4 * (size_t)g.wmax + 2 * (size_t)(g.tw + 1) + nheads * (tile_el + 64 * cp)) * 4 +
-         (size_t)g.hmax * g.wmax;
+  const size_t head = (((size_t)(g.tw + 1) * g.wmax + 4 * (size_t)g.wmax + 2 * (size_t)(g.tw + 1) + 3) & ~(size_t)3);
+  return (head + nheads * (tile_el + 64 * cp)) * 4 + (size_t)g.hmax * g.wmax;
 }
 static size_t upce_tile_el(const UpceGeo& g) { return (size_t)(g.th + 1) * (g.tw + 1) * g.c; }
 // ws: stat[64] (count, per-head loss sums; offset 0, see the header) | [heads][nblocks][tile_el]
