@@ -282,6 +282,27 @@ int rtsds_upce_bwd(int nheads, const float* grad_loss, int grad_stride, void* co
                    int n, int hl, int wl, int c, int H, int W, float scale_h, float scale_w,
                    int dtype, const void* ws, size_t ws_bytes, void* stream);
 
+/* ---------------------------------------------------------------- input pipeline
+ * The reference's per-sample torchvision transforms (main.py:60-108; datasets/cityscapes.py:
+ * 56-68, datasets/gta5.py:69-118) on a decoded HWC image in device memory.
+ * rtsds_resize_aa: Resize((ho, wo), antialias=True) == F.interpolate(bilinear,
+ *   align_corners=False, antialias=True) of the float image, optionally of its horizontal
+ *   mirror (flip != 0: RandomHorizontalFlip applied before the resize), with the epilogue of
+ *   kind 0: f32 HWC, 1: bf16 HWC (both (v - mean[c]) / std[c] when mean/std are given:
+ *   Normalize on the 0-255 scale), 2: int64 label (round half-to-even, clamp to
+ *   [clamp_lo, clamp_hi] when clamp_lo <= clamp_hi: IntRangeTransformer).  src_u8 selects a
+ *   uint8 (else fp32) source.  dst is the image's slot in an NHWC batch.
+ * rtsds_gaussian_blur: GaussianBlur((kx, ky), sigma) of a HWC image (uint8 or fp32 source),
+ *   fp32 HWC out, reflect padding.
+ * rtsds_gta5_decode: RGB label (HWC uint8) -> train id 0..18 (unmatched colours -> 0).      */
+size_t rtsds_resize_aa_workspace(int c, int h, int w, int ho, int wo);
+int rtsds_resize_aa(const void* src, int src_u8, int c, int h, int w, void* dst, int kind, int ho, int wo,
+                    int flip, const float* mean, const float* std, int clamp_lo, int clamp_hi, void* ws,
+                    size_t ws_bytes, void* stream);
+int rtsds_gaussian_blur(const void* src, int src_u8, float* dst, int c, int h, int w, int kx, int ky,
+                        float sigma_x, float sigma_y, void* stream);
+int rtsds_gta5_decode(const uint8_t* rgb, int64_t* out, int h, int w, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -75,6 +75,11 @@ SIGNATURES = {
     "rtsds_bce_fwd": (c_int, [P, P, P, c_int, P]),
     "rtsds_bce_bwd": (c_int, [P, P, P, P, c_int, P]),
     "rtsds_adam_step_dev": (c_int, [P, P, P, P, P, c_long, P, c_float, c_float, c_float, c_float, c_float, P]),
+    "rtsds_resize_aa_workspace": (c_size_t, [c_int, c_int, c_int, c_int, c_int]),
+    "rtsds_resize_aa": (c_int, [P, c_int, c_int, c_int, c_int, P, c_int, c_int, c_int, c_int, P, P, c_int, c_int,
+                                P, c_size_t, P]),
+    "rtsds_gaussian_blur": (c_int, [P, c_int, P, c_int, c_int, c_int, c_int, c_int, c_float, c_float, P]),
+    "rtsds_gta5_decode": (c_int, [P, P, c_int, c_int, P]),
     "rtsds_sgd_step": (c_int, [P, P, P, P, c_long, P, c_float, c_float, c_float, c_float, c_int, c_int,
                                c_float, P]),
     "rtsds_adam_step": (c_int, [P, P, P, P, P, c_long, c_float, c_float, c_float, c_float, c_float,

@@ -5,10 +5,11 @@ config.yaml, factories main.py:110-231, dispatch main.py:272-374) on the HIP pat
                              [--model bisenet|deeplab] [--dataset cityscapes|gta5] [--seed 42]
     torchrun --nproc-per-node 8 --master-addr 127.0.0.1 -m rtsds_amd.main --domain_adaptation
 
-Dataset readers (PNG decode, resize, augmentation; datasets/*, main.py:46-108) are outside
-the hot path: when the configured dataset directories do not exist, synthetic loaders of the
-configured shapes are used (ImageNet-normalised 0-255 images, labels 0..19 with 19 = ignore),
-sharded per rank.  Deviations from the reference (documented in DESIGN.md): DA accepts a
+Datasets (main.py:46-108): when the configured directories exist, the reference's readers
+(rtsds_amd.datasets) feed the device-side transforms (rtsds_amd.transforms: antialiased
+resize, normalize, augmentation, label clamp as HIP kernels); otherwise synthetic loaders of
+the configured shapes are used (ImageNet-normalised 0-255 images, labels 0..19 with
+19 = ignore), sharded per rank.  Deviations from the reference (documented in DESIGN.md): DA accepts a
 DeepLab generator; validation accepts class_names / detailed_report.
 """
 import argparse
@@ -102,13 +103,44 @@ class SyntheticLoader:
         return iter(self.data)
 
 
+def real_datasets_loader(config, is_augmented, device="cuda"):
+    """main.py:60-108 on the device pipeline: the reference's readers (PNG decode on CPU
+    DataLoader workers) deliver raw uint8 samples, batches go to HBM and through the
+    torchvision-equivalent HIP transforms (rtsds_amd.transforms); under data parallelism each
+    rank reads a disjoint shard (DistributedSampler)."""
+    from torch.utils.data import DataLoader
+    from torch.utils.data.distributed import DistributedSampler
+
+    from . import transforms as T
+    from .datasets import GTA5, CityScapes
+    cs, gta = config.data["cityscapes"], config.data["gta5_modified"]
+    cs_size, gta_size = T.parse_size(cs["image_size"]), T.parse_size(gta["image_size"])
+    rank, _, world = dist_env()
+
+    def loader(ds, bs, workers, shuffle):
+        sampler = DistributedSampler(ds, num_replicas=world, rank=rank, shuffle=shuffle) if world > 1 else None
+        return DataLoader(ds, batch_size=bs, shuffle=shuffle and sampler is None, sampler=sampler, pin_memory=False,
+                          num_workers=workers, collate_fn=T.collate_raw)
+
+    city_img = T.ImagePipeline(cs_size)
+    city_lbl = T.LabelPipeline(cs_size, clamp=(0, cs["num_classes"]))
+    gta_img = T.ImagePipeline(gta_size, augment=T.augmentation_loader(config, 0.5) if is_augmented else None)
+    gta_lbl = T.LabelPipeline(gta_size)
+    train_ds = CityScapes(cs["segmentation_train_dir"], cs["images_train_dir"])
+    val_ds = CityScapes(cs["segmentation_val_dir"], cs["images_val_dir"])
+    gta_ds = GTA5(gta["images_dir"], gta["segmentation_dir"], None, None)
+    return (T.DeviceLoader(loader(train_ds, cs["batch_size"], cs["num_workers"], True), city_img, city_lbl, device),
+            T.DeviceLoader(loader(val_ds, cs["batch_size"], cs["num_workers"], False), city_img, city_lbl, device),
+            T.DeviceLoader(loader(gta_ds, gta["batch_size"], gta["num_workers"], True), gta_img, gta_lbl, device))
+
+
 def datasets_loader(config, is_augmented):
-    """Real datasets are out of the hot path's scope; synthetic loaders when absent."""
+    """main.py:60-108: the dataset directories of config.yaml through the device pipeline when
+    they exist, else synthetic loaders of the configured shapes."""
     cs, gta = config.data["cityscapes"], config.data["gta5_modified"]
     present = os.path.isdir(cs["images_train_dir"]) and os.path.isdir(gta["images_dir"])
     if present:
-        raise NotImplementedError("PNG dataset readers are outside the rtsds hot path "
-                                  "(datasets/*); feed tensors through the same loaders API")
+        return real_datasets_loader(config, is_augmented, config.device)
     rank = dist_env()[0]
     nb = config.data.get("synthetic_batches", 4)
     size = lambda s: [int(v) for v in str(s).split(",")]  # noqa: E731

@@ -60,6 +60,44 @@ def allreduce_flat(buffers):
     return 1.0
 
 
+_OVERLAP = {"on": True}
+
+
+def set_overlap_allreduce(on):
+    """Early (overlapped) gradient all-reduce in the DA iteration on (default) / off (serial,
+    inside step())."""
+    _OVERLAP["on"] = bool(on)
+
+
+def allreduce_start(buffers):
+    """Start the SUM all-reduce of flat gradient buffers now, asynchronously (RCCL on its own
+    stream, overlapping whatever the caller enqueues next), and return a finisher that makes
+    the current stream wait for them (and casts reduced-precision wire copies back); None
+    when there is nothing to reduce.  Under runtime.GraphedStep capture the start and the wait
+    are graph-segment breaks re-issued between replays, so a replayed iteration overlaps the
+    same way (DA iteration: G's all-reduce runs beside the discriminator phase)."""
+    if not (dist.is_available() and dist.is_initialized()) or dp_world() <= 1:
+        return None
+    wire = _ALLREDUCE["dtype"]
+    pending, pairs = [], []
+    for b in buffers:
+        t = b if wire == torch.float32 else b.to(wire)
+        pairs.append((b, t))
+        collective(lambda t=t: pending.append(dist.all_reduce(t, async_op=True)))
+
+    def wait_all():
+        for h in pending:
+            h.wait()
+        pending.clear()
+
+    def finish():
+        collective(wait_all)
+        for b, t in pairs:
+            if t is not b:
+                b.copy_(t)
+    return finish
+
+
 class _Arena:
     """One parameter group's flat fp32 buffers: parameters, gradients, first moment (Adam's
     exp_avg / SGD's momentum buffer), second moment (Adam only) and the bf16 shadow."""
@@ -147,6 +185,7 @@ class _FlatOptimizer(torch.optim.Optimizer):
         self._capturing = False  # inside stream capture: the hyper values are staged outside
         self._runs = None        # [(group, i, j)] of the last step
         self._hyper = None       # device fp32 [runs][3]
+        self._finish = None      # pending early gradient all-reduce (start_grad_allreduce)
 
     # ------------------------------------------------------------------ arena
     def _ensure(self):
@@ -217,10 +256,7 @@ class _FlatOptimizer(torch.optim.Optimizer):
                     a.gflat[a.offsets[i]:a.offsets[i] + a.params[i].numel()].zero_()
 
     # ------------------------------------------------------------------ step
-    @torch.no_grad()
-    def step(self, closure=None):
-        loss = closure() if closure is not None else None
-        arenas = self._ensure()
+    def _fix_grads(self, arenas):
         for a in arenas:
             for i in range(len(a.params)):
                 if a.touched[i] and not a.grad_ptr_ok(i):
@@ -228,7 +264,27 @@ class _FlatOptimizer(torch.optim.Optimizer):
                         warnings.warn(f"rtsds_amd.{self._NAME}: gradient left the arena; copying back")
                         self._warned = True
                     a.rebind_grad(i)
-        gscale = allreduce_flat([a.gflat for a in arenas])
+
+    @torch.no_grad()
+    def start_grad_allreduce(self):
+        """Data parallelism: the gradients are final now -- start their all-reduce so it overlaps
+        the work enqueued before step(), which then only waits for it.  No-op at world 1."""
+        if self._finish is None and _OVERLAP["on"]:
+            arenas = self._ensure()
+            self._fix_grads(arenas)
+            self._finish = allreduce_start([a.gflat for a in arenas])
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = closure() if closure is not None else None
+        arenas = self._ensure()
+        if self._finish is not None:
+            self._finish()
+            self._finish = None
+            gscale = 1.0
+        else:
+            self._fix_grads(arenas)
+            gscale = allreduce_flat([a.gflat for a in arenas])
         # contiguous runs of touched parameters with equal step counts -> one launch each
         runs = []
         for gi, a in enumerate(arenas):

@@ -152,6 +152,11 @@ def _seg_loss(model, criterion, x, label, correct):
     return loss, outs[0], None
 
 
+def _start_allreduce(optimizer):
+    if dp_world() > 1 and hasattr(optimizer, "start_grad_allreduce"):
+        optimizer.start_grad_allreduce()
+
+
 def _full(t, geo):
     return F.interpolate_geometry(t, geo) if geo is not None else t
 
@@ -180,6 +185,8 @@ def da_step(generator, discriminator, generator_optimizer, discriminator_optimiz
     ones = torch.ones(pred_t.size(), device=pred_t.device)
     loss_adv = lambda_ * discriminator_loss(pred_t, ones) / iterations
     loss_adv.backward()
+    # G's gradients are final: under data parallelism their all-reduce overlaps the D phase
+    _start_allreduce(generator_optimizer)
 
     for p in discriminator.parameters():
         p.requires_grad = True
@@ -190,6 +197,7 @@ def da_step(generator, discriminator, generator_optimizer, discriminator_optimiz
     pred_t2 = discriminator(F.softmax(target_feature, dim=1))
     loss_dtgt = discriminator_loss(pred_t2, torch.zeros(pred_t2.size(), device=pred_t2.device)) / iterations
     loss_dtgt.backward()
+    _start_allreduce(discriminator_optimizer)  # overlaps G's optimizer step
 
     generator_optimizer.step()
     discriminator_optimizer.step()

@@ -35,6 +35,40 @@ def _worker(rank, world, port, q, wire="fp32"):
     dist.destroy_process_group()
 
 
+def _async_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    from rtsds_amd.utils import init_distributed
+    init_distributed("gloo")
+    from rtsds_amd.optim import allreduce_start
+    a = torch.arange(6, dtype=torch.float32) * (rank + 1)
+    b = torch.ones(3) * (rank + 10)
+    finish = allreduce_start([a, b])
+    finish()
+    q.put((rank, a.tolist(), b.tolist(), finish is not None))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_async_allreduce_start_finish():
+    """optim.allreduce_start (the DA iteration's early, overlapped gradient all-reduce):
+    after finish() every buffer holds the SUM over ranks, exactly as the serial path."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_async_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(2)]
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    for rank, a, b, started in res:
+        assert started
+        assert a == [float(3 * i) for i in range(6)]
+        assert b == [21.0] * 3
+
+
 @pytest.mark.parametrize("wire", ["fp32", "fp16"])
 @pytest.mark.parametrize("world", [2])
 def test_gloo_flat_allreduce(world, wire):

@@ -430,26 +430,35 @@ def test_side_stream_wgrad_equals_serial(da):
             assert torch.equal(states[0][k], s[k]), k
 
 
-@pytest.mark.parametrize("da", [False, True])
-def test_graphed_step_with_collectives(da, monkeypatch):
-    """Data-parallel iterations under runtime.GraphedStep: every collective (the losses'
-    global valid-pixel counts, the gradient all-reduce) is a break between captured graph
-    segments and is re-issued eagerly between their replays.  A one-rank RCCL group with the
-    data-parallel code paths forced on (dp_world patched to 2; all_reduce over one rank is the
-    identity) must leave parameters, optimizer state and BN buffers bit-identical to the same
-    iterations run eagerly."""
+@pytest.fixture(scope="module")
+def one_rank_rccl():
+    """A one-rank RCCL process group for the module (created once: the collectives tests'
+    parameters share it rather than re-initialising RCCL in one process)."""
     import socket
 
     import torch.distributed as dist
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+    yield
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("da", [False, True])
+def test_graphed_step_with_collectives(da, monkeypatch, one_rank_rccl):
+    """Data-parallel iterations under runtime.GraphedStep: every collective (the losses'
+    global valid-pixel counts, the gradient all-reduce -- started early and awaited in step()
+    in the DA iteration) is a break between captured graph segments and is re-issued eagerly
+    between their replays.  A one-rank RCCL group with the
+    data-parallel code paths forced on (dp_world patched to 2; all_reduce over one rank is the
+    identity) must leave parameters, optimizer state and BN buffers bit-identical to the same
+    iterations run eagerly."""
     from rtsds_amd import functional as rf
     from rtsds_amd import losses as rl
     from rtsds_amd import runtime
     from rtsds_amd.runtime import GraphedStep
 
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        port = s.getsockname()[1]
-    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
     try:
         for mod in (rf, optim, rl, rtrain):
             monkeypatch.setattr(mod, "dp_world", lambda: 2)
@@ -460,7 +469,10 @@ def test_graphed_step_with_collectives(da, monkeypatch):
         ce, bce = losses.CrossEntropyLoss(ignore_index=19), losses.BCEWithLogitsLoss()
         states, nseg = [], None
         with rtsds_amd.precision(torch.bfloat16):
-            for graphed in (False, True):
+            # serial all-reduce (inside step()), the DA iteration's early overlapped all-reduce
+            # (optim.start_grad_allreduce) eager, and the same replayed as graph segments
+            for overlap, graphed in ((False, False), (True, False), (True, True)):
+                optim.set_overlap_allreduce(overlap)
                 torch.manual_seed(3)
                 net = BiSeNet(19, "resnet18").to(DEV).train()
                 disc = TinyDomainDiscriminator(19).to(DEV).train()
@@ -482,10 +494,11 @@ def test_graphed_step_with_collectives(da, monkeypatch):
                 states.append({k: v.detach().float().cpu().clone() for k, v in
                                list(net.state_dict().items()) + list(disc.state_dict().items())})
         assert nseg is not None and nseg >= 3, nseg  # count all-reduce(s) + gradient all-reduce
-        for k in states[0]:
-            assert torch.equal(states[0][k], states[1][k]), k
+        for st in states[1:]:
+            for k in states[0]:
+                assert torch.equal(states[0][k], st[k]), k
     finally:
-        dist.destroy_process_group()
+        optim.set_overlap_allreduce(True)
         assert runtime._capture["step"] is None
 
 
