@@ -34,6 +34,10 @@ enum {
 };
 enum { RTSDS_ACT_NONE = 0, RTSDS_ACT_RELU = 1, RTSDS_ACT_LEAKY = 2, RTSDS_ACT_SIGMOID = 3 };
 #define RTSDS_ACCUMULATE 0x100 /* conv fwd flag: y += conv(...) (ASPP sum, deeplabv2.py:62-66) */
+/* conv fwd (act) / wgrad (accumulate) flag: x is already stored with the padded channel pitch
+ * the GEMM gathers (19 -> 32 for the discriminator's class-probability input, written by
+ * rtsds_upsoftmax_fwd) and zero in channels c..pitch-1: the internal pad pass is skipped.   */
+#define RTSDS_INPUT_PADDED 0x400
 
 typedef struct {
   int n, h, w, c;   /* input  [n][h][w][c]                                     */
@@ -281,6 +285,19 @@ int rtsds_upce_finish(int nheads, const void* ws, float* loss, float* loss_sum, 
 int rtsds_upce_bwd(int nheads, const float* grad_loss, int grad_stride, void* const* dlogits,
                    int n, int hl, int wl, int c, int H, int W, float scale_h, float scale_w,
                    int dtype, const void* ws, size_t ws_bytes, void* stream);
+
+/* ---------------------------------------------------------------- discriminator input
+ * softmax(interpolate_bilinear(x)) over classes (train.py:225,245,256) in one pass: x NHWC
+ * [n][hi][wi][c], y NHWC [n][ho][wo][y_ld] with channels c..y_ld-1 zero (the padded input of
+ * the discriminator's first conv, RTSDS_INPUT_PADDED).  Bit-identical to rtsds_bilinear_fwd
+ * followed by the channel softmax.  rtsds_upsoftmax_bwd: dx = resize_adjoint(softmax_bwd(dy,
+ * y)) (dy with row pitch dy_ld), bit-identical to the unfused backward chain.  c <= 32.      */
+int rtsds_upsoftmax_fwd(const void* x, void* y, int n, int hi, int wi, int c, int ho, int wo,
+                        float scale_h, float scale_w, int y_ld, int dtype, void* stream);
+size_t rtsds_upsoftmax_bwd_workspace(int n, int hi, int wi, int c, int ho, int wo);
+int rtsds_upsoftmax_bwd(const void* dy, int dy_ld, const void* y, int y_ld, void* dx, int n, int hi,
+                        int wi, int c, int ho, int wo, float scale_h, float scale_w, int dtype,
+                        void* ws, size_t ws_bytes, void* stream);
 
 /* ---------------------------------------------------------------- input pipeline
  * The reference's per-sample torchvision transforms (main.py:60-108; datasets/cityscapes.py:

@@ -17,6 +17,7 @@ LIB_PATH = os.environ.get("RTSDS_LIB") or os.path.join(_HERE, "librtsds_hip.so")
 F32, BF16 = 0, 1
 ACT_NONE, ACT_RELU, ACT_LEAKY, ACT_SIGMOID = 0, 1, 2, 3
 ACCUMULATE = 0x100
+INPUT_PADDED = 0x400
 ERRORS = {1: "bad shape", 2: "unsupported configuration", 3: "HIP launch failure", 4: "workspace too small"}
 
 c_int, c_long, c_float, c_size_t, c_void_p = (ctypes.c_int, ctypes.c_long, ctypes.c_float,
@@ -75,6 +76,10 @@ SIGNATURES = {
     "rtsds_bce_fwd": (c_int, [P, P, P, c_int, P]),
     "rtsds_bce_bwd": (c_int, [P, P, P, P, c_int, P]),
     "rtsds_adam_step_dev": (c_int, [P, P, P, P, P, c_long, P, c_float, c_float, c_float, c_float, c_float, P]),
+    "rtsds_upsoftmax_fwd": (c_int, [P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_float, c_int, c_int, P]),
+    "rtsds_upsoftmax_bwd_workspace": (c_size_t, [c_int, c_int, c_int, c_int, c_int, c_int]),
+    "rtsds_upsoftmax_bwd": (c_int, [P, c_int, P, c_int, P, c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_float,
+                                    c_int, P, c_size_t, P]),
     "rtsds_resize_aa_workspace": (c_size_t, [c_int, c_int, c_int, c_int, c_int]),
     "rtsds_resize_aa": (c_int, [P, c_int, c_int, c_int, c_int, P, c_int, c_int, c_int, c_int, P, P, c_int, c_int,
                                 P, c_size_t, P]),

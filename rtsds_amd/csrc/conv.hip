@@ -1527,7 +1527,7 @@ extern "C" size_t rtsds_conv2d_fwd_workspace(const rtsds_conv_desc* d) {
 // Operands of the forward GEMM: the superpixel view of 3-channel stride-2 convs, or
 // channel-padded copies when Cin is not a vector multiple (workspace), else x / w as given.
 static void fwd_prepare(const rtsds_conv_desc* d0, const void*& x, const void*& w, void* ws, rtsds_conv_desc& d,
-                        hipStream_t st) {
+                        hipStream_t st, bool x_padded = false) {
   d = *d0;
   if (sp_path(d0)) {
     void* x4 = ws;
@@ -1546,9 +1546,11 @@ static void fwd_prepare(const rtsds_conv_desc* d0, const void*& x, const void*& 
     const size_t es = esize(d.dtype);
     void* xp = ws;
     void* wp = (char*)ws + al256((size_t)d.n * d.h * d.w * cp * es);
-    pad_any(d.dtype, x, xp, (long)d.n * d.h * d.w, d.c, cp, st);
+    if (!x_padded) {
+      pad_any(d.dtype, x, xp, (long)d.n * d.h * d.w, d.c, cp, st);
+      x = xp;
+    }
     pad_any(d.dtype, w, wp, (long)d.k * d.kh * d.kw, d.c, cp, st);
-    x = xp;
     w = wp;
     d.c = cp;
   }
@@ -1567,13 +1569,15 @@ extern "C" int rtsds_conv2d_fwd(const rtsds_conv_desc* d0, const void* x, const 
     else pooled_fwd_launch<float>(d0, x, w, bias, y, act & 0xff, accum, bn_stats, st);
     return hipGetLastError() == hipSuccess ? RTSDS_OK : RTSDS_ERR_LAUNCH;
   }
+  const bool x_padded = (act & RTSDS_INPUT_PADDED) != 0;
+  if (x_padded && (sp_path(d0) || hconv_ok(d0) || pad_c(d0->c, d0->dtype) == d0->c)) return RTSDS_ERR_UNSUPPORTED;
   if (hconv_ok(d0) && !(act & RTSDS_ACCUMULATE)) {
     if (bn_stats && (act & 0xff)) return RTSDS_ERR_UNSUPPORTED;
     hconv_fwd(d0, x, w, bias, nullptr, y, act & 0xff, bn_stats, st);
     return hipGetLastError() == hipSuccess ? RTSDS_OK : RTSDS_ERR_LAUNCH;
   }
   rtsds_conv_desc d;
-  fwd_prepare(d0, x, w, ws, d, st);
+  fwd_prepare(d0, x, w, ws, d, st, x_padded);
   ConvArgs p = make_args(&d);
   p.a = x; p.b = w; p.bias = bias; p.out = y;
   p.act = act & 0xff;
@@ -1881,6 +1885,9 @@ extern "C" int rtsds_conv2d_wgrad(const rtsds_conv_desc* d0, const void* x, cons
                                   float* dbias, int accumulate, void* ws, size_t ws_bytes, void* stream) {
   int e = check_desc(d0);
   if (e) return e;
+  const bool x_padded = (accumulate & RTSDS_INPUT_PADDED) != 0;
+  accumulate &= ~RTSDS_INPUT_PADDED;
+  if (x_padded && (sp_path(d0) || pooled_1x1(d0) || pad_c(d0->c, d0->dtype) == d0->c)) return RTSDS_ERR_UNSUPPORTED;
   if (ws_bytes < rtsds_conv2d_wgrad_workspace(d0)) return RTSDS_ERR_WORKSPACE;
   hipStream_t st = (hipStream_t)stream;
   if (pooled_1x1(d0)) {
@@ -1911,8 +1918,10 @@ extern "C" int rtsds_conv2d_wgrad(const rtsds_conv_desc* d0, const void* x, cons
     d.k = pl.kp;
   }
   if (!sp && pl.cp != d.c) {
-    pad_any(d.dtype, x, xp, (long)d.n * d.h * d.w, d.c, pl.cp, st);
-    x = xp;
+    if (!x_padded) {  // RTSDS_INPUT_PADDED: x already has the padded channel pitch
+      pad_any(d.dtype, x, xp, (long)d.n * d.h * d.w, d.c, pl.cp, st);
+      x = xp;
+    }
     d.c = pl.cp;
   }
   ConvArgs p = make_args(&d);

@@ -10,7 +10,7 @@ import ctypes
 import numpy as np
 import torch
 
-from ._lib import ACT_RELU, ACT_SIGMOID, ConvDesc, lib
+from ._lib import ACT_RELU, ACT_SIGMOID, INPUT_PADDED, ConvDesc, lib
 from .runtime import (CL, collective, dcode, dp_world, empty_nhwc, nhwc, require_hip, side_enabled, side_fork,
                       stream, workspace)
 
@@ -79,6 +79,22 @@ def _conv_desc(x, k, kh, kw, stride, padding, dilation):
     return d
 
 
+def is_padded_input(x):
+    """A class-probability tensor written with the padded channel pitch the conv gathers
+    (upsample_softmax): [N, C, H, W] view of an NHWC [N, H, W, Cp] buffer, zero in C..Cp-1."""
+    cp = getattr(x, "_rt_cpad", None)
+    return cp is not None and x.dim() == 4 and x.stride(1) == 1 and x.stride(3) == cp and \
+        x.stride(2) == cp * x.shape[3] and x.stride(0) == cp * x.shape[2] * x.shape[3]
+
+
+def detach_padded(x):
+    """x.detach() keeping the padded-input marker (tensor attributes do not survive detach)."""
+    y = x.detach()
+    if getattr(x, "_rt_cpad", None) is not None:
+        y._rt_cpad = x._rt_cpad
+    return y
+
+
 class GradJoin:
     """Gradient of a tensor read by ``n`` rtsds Functions -- a residual block's input, read by
     conv1 and by the identity (BatchNorm residual) or downsample branch
@@ -121,14 +137,18 @@ class ConvFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, wq, stride, padding, dilation, act, stats, join=None):
         require_hip(x, weight)
-        x = nhwc(x)
+        padded = is_padded_input(x)
+        if not padded:
+            x = nhwc(x)
         k, _, kh, kw = weight.shape
         d = _conv_desc(x, k, kh, kw, stride, padding, dilation)
         y = empty_nhwc(d.n, k, d.ho, d.wo, x.dtype, x.device)
         ws = workspace(lib.rtsds_conv2d_fwd_workspace(ctypes.byref(d)), x.device)
+        flag = INPUT_PADDED if padded else 0
         with _Timed(d, "fwd"):
-            lib.rtsds_conv2d_fwd(ctypes.byref(d), _P(x), _P(wq), _P(bias), _P(y), act, _P(stats), _P(ws),
-                                 ws.numel(), stream())
+            lib.rtsds_conv2d_fwd(ctypes.byref(d), _P(x), _P(wq), _P(bias), _P(y), act | flag, _P(stats), _P(ws),
+                                        ws.numel(), stream())
+        ctx.xflag = flag
         ctx.d, ctx.act, ctx.has_bias = d, act, bias is not None
         ctx.params = (weight, bias)
         ctx.join = join
@@ -157,7 +177,7 @@ class ConvFn(torch.autograd.Function):
             if sinks is not None:
                 ws = workspace(lib.rtsds_conv2d_wgrad_workspace(ctypes.byref(d)), x.device)
                 side = side_fork(x, g, ws)
-                lib.rtsds_conv2d_wgrad(ctypes.byref(d), _P(x), _P(g), _P(sinks[0]), _P(sinks[1]), 1,
+                lib.rtsds_conv2d_wgrad(ctypes.byref(d), _P(x), _P(g), _P(sinks[0]), _P(sinks[1]), 1 | ctx.xflag,
                                        _P(ws), ws.numel(), side.cuda_stream)
                 wg_side = True
         if ctx.needs_input_grad[0]:
@@ -176,8 +196,8 @@ class ConvFn(torch.autograd.Function):
             ws = workspace(lib.rtsds_conv2d_wgrad_workspace(ctypes.byref(d)), x.device)
             if sinks is not None:
                 with _Timed(d, "wgrad"):
-                    lib.rtsds_conv2d_wgrad(ctypes.byref(d), _P(x), _P(g), _P(sinks[0]), _P(sinks[1]), 1,
-                                           _P(ws), ws.numel(), stream())
+                    lib.rtsds_conv2d_wgrad(ctypes.byref(d), _P(x), _P(g), _P(sinks[0]), _P(sinks[1]), 1 | ctx.xflag,
+                                                  _P(ws), ws.numel(), stream())
                 dw = None
                 db = None
             else:
@@ -185,8 +205,8 @@ class ConvFn(torch.autograd.Function):
                                  memory_format=CL)
                 db = torch.empty(d.k, dtype=torch.float32, device=x.device) if ctx.has_bias else None
                 with _Timed(d, "wgrad"):
-                    lib.rtsds_conv2d_wgrad(ctypes.byref(d), _P(x), _P(g), _P(dw), _P(db), 0, _P(ws),
-                                           ws.numel(), stream())
+                    lib.rtsds_conv2d_wgrad(ctypes.byref(d), _P(x), _P(g), _P(dw), _P(db), ctx.xflag, _P(ws),
+                                                  ws.numel(), stream())
                 if not ctx.needs_input_grad[1]:
                     dw = None
         return dx, dw, db, None, None, None, None, None, None, None
@@ -923,6 +943,48 @@ def upsample_cross_entropy(heads, target, geo, ignore_index=-100, correct=None):
     fn = UpsampleCrossEntropyFn
     total = fn.apply(t, full, int(ignore_index), correct, *heads)
     return total
+
+
+class UpsampleSoftmaxFn(torch.autograd.Function):
+    """softmax(interpolate_bilinear(x, geo), dim=1) in one pass (rtsds_upsoftmax_fwd), written
+    zero-padded to 32 channels so the discriminator's first conv reads it directly
+    (RTSDS_INPUT_PADDED); backward = softmax backward + resize adjoint in one pass plus the
+    vertical adjoint (rtsds_upsoftmax_bwd).  Bit-identical to interpolate -> softmax."""
+
+    @staticmethod
+    def forward(ctx, x, geo):
+        require_hip(x)
+        x = nhwc(x)
+        n, c, hi, wi = x.shape
+        ho, wo, sh, sw = geo
+        cp = 32
+        buf = torch.empty((n, ho, wo, cp), dtype=x.dtype, device=x.device)
+        lib.rtsds_upsoftmax_fwd(_P(x), _P(buf), n, hi, wi, c, ho, wo, sh, sw, cp, dcode(x), stream())
+        ctx.geo, ctx.shape, ctx.cp = geo, (n, c, hi, wi), cp
+        ctx.save_for_backward(buf)
+        return buf.permute(0, 3, 1, 2)[:, :c]
+
+    @staticmethod
+    def backward(ctx, dy):
+        buf, = ctx.saved_tensors
+        n, c, hi, wi = ctx.shape
+        ho, wo, sh, sw = ctx.geo
+        dy = nhwc(dy)
+        if dy.dtype != buf.dtype:
+            dy = cast(dy, buf.dtype)
+        dx = empty_nhwc(n, c, hi, wi, buf.dtype, buf.device)
+        ws = workspace(lib.rtsds_upsoftmax_bwd_workspace(n, hi, wi, c, ho, wo), buf.device)
+        lib.rtsds_upsoftmax_bwd(_P(dy), c, _P(buf), ctx.cp, _P(dx), n, hi, wi, c, ho, wo, sh, sw, dcode(buf),
+                                       _P(ws), ws.numel(), stream())
+        return dx, None
+
+
+def upsample_softmax(x, geo):
+    """softmax over classes of the resized head (train.py:225,245,256), as the discriminator's
+    zero-padded input (functional.is_padded_input)."""
+    y = UpsampleSoftmaxFn.apply(x, geo)
+    y._rt_cpad = 32
+    return y
 
 
 class BCEWithLogitsFn(torch.autograd.Function):

@@ -38,7 +38,11 @@ class UpSampler(nn.Module):
 
 
 def _nhwc_input(x):
-    """Accept either an rtsds NHWC activation or a reference-layout NCHW fp32 tensor."""
+    """Accept an rtsds NHWC activation, the zero-padded class probabilities of
+    functional.upsample_softmax (read in place by conv1), or a reference-layout NCHW fp32
+    tensor."""
+    if F.is_padded_input(x):
+        return x
     if x.dim() == 4 and x.is_contiguous(memory_format=torch.channels_last) and x.shape[1] > 1:
         return x
     return to_input(x)
@@ -46,6 +50,8 @@ def _nhwc_input(x):
 
 class DomainDiscriminator(nn.Module):
     """model.py:30-64: 19->64->128->256->512->1, k4 s2 p1, LeakyReLU(0.2), GAP, optional GRL."""
+
+    accepts_padded_probs = True  # conv1 reads functional.upsample_softmax's padded output
 
     def __init__(self, num_classes=19, with_grl=False, lambda_: float = 0.1) -> None:
         super(DomainDiscriminator, self).__init__()
@@ -71,6 +77,8 @@ class DomainDiscriminator(nn.Module):
 
 class TinyDomainDiscriminator(nn.Module):
     """model.py:67-83: conv 19->64 k4s2p1 + LeakyReLU(0.2) -> conv 64->1 k4s2p1 -> GAP."""
+
+    accepts_padded_probs = True
 
     def __init__(self, num_classes=19) -> None:
         super(TinyDomainDiscriminator, self).__init__()

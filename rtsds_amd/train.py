@@ -177,6 +177,11 @@ def da_step(generator, discriminator, generator_optimizer, discriminator_optimiz
     loss_seg, main, geo = _seg_loss(generator, generator_loss, source_image, source_label, correct)
     loss_seg = loss_seg / iterations
     loss_seg.backward()
+    if geo is not None and getattr(discriminator, "accepts_padded_probs", False) and \
+            hasattr(generator, "forward_lowres") and main.shape[1] <= 32:
+        return _da_step_fused(generator, discriminator, generator_optimizer, discriminator_optimizer,
+                              discriminator_loss, main, geo, target_image, lambda_, iterations, loss_seg,
+                              correct)
     with torch.no_grad():
         source_features = _full(main.detach(), geo)
 
@@ -198,6 +203,39 @@ def da_step(generator, discriminator, generator_optimizer, discriminator_optimiz
     loss_dtgt = discriminator_loss(pred_t2, torch.zeros(pred_t2.size(), device=pred_t2.device)) / iterations
     loss_dtgt.backward()
     _start_allreduce(discriminator_optimizer)  # overlaps G's optimizer step
+
+    generator_optimizer.step()
+    discriminator_optimizer.step()
+    return loss_seg.detach(), loss_adv.detach(), loss_dsrc.detach(), loss_dtgt.detach(), correct
+
+
+def _da_step_fused(generator, discriminator, generator_optimizer, discriminator_optimizer,
+                   discriminator_loss, main, geo, target_image, lambda_, iterations, loss_seg, correct):
+    """da_step's discriminator phases with the full-resolution resize and softmax of each
+    head fused into one pass that writes the discriminator's padded input
+    (functional.upsample_softmax): identical values to softmax(interpolate(head)) -- the
+    reference's D(softmax(G(x))) at train.py:225,245,256 -- without the full-resolution logits,
+    the separate softmax pass or the conv's channel-pad pass.  softmax(target_feature.detach())
+    (train.py:256) equals the G-phase target probabilities, so they are computed once."""
+    with torch.no_grad():
+        source_probs = F.upsample_softmax(main.detach(), geo)
+    (t_low, t_geo), = generator.forward_lowres(target_image, main_only=True)
+    target_probs = F.upsample_softmax(t_low, t_geo)
+    pred_t = discriminator(target_probs)
+    ones = torch.ones(pred_t.size(), device=pred_t.device)
+    loss_adv = lambda_ * discriminator_loss(pred_t, ones) / iterations
+    loss_adv.backward()
+    _start_allreduce(generator_optimizer)
+
+    for p in discriminator.parameters():
+        p.requires_grad = True
+    pred_s = discriminator(source_probs)
+    loss_dsrc = discriminator_loss(pred_s, torch.ones(pred_s.size(), device=pred_s.device)) / iterations
+    loss_dsrc.backward()
+    pred_t2 = discriminator(F.detach_padded(target_probs))
+    loss_dtgt = discriminator_loss(pred_t2, torch.zeros(pred_t2.size(), device=pred_t2.device)) / iterations
+    loss_dtgt.backward()
+    _start_allreduce(discriminator_optimizer)
 
     generator_optimizer.step()
     discriminator_optimizer.step()

@@ -585,3 +585,40 @@ def test_upsampler(golden):
     check_tensor(arrays, meta, "up_out", o.float().cpu(), rtol=1e-4)
     check_tensor(arrays, meta, "up_du", ui.grad.float().cpu(), rtol=1e-4)
     check_params(arrays, meta, "up_grad", {k: q.grad.cpu() for k, q in up.named_parameters()}, rtol=1e-4)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_da_step_fused_discriminator_input_equals_unfused(dt):
+    """da_step's fused discriminator input (functional.upsample_softmax: resize + softmax +
+    channel padding in one pass, read in place by D's first conv; backward fused the same
+    way; target probabilities shared by the G and D phases) leaves losses, parameters,
+    optimizer state and BN buffers bit-identical to the unfused chain (interpolate, softmax,
+    the conv's internal pad) after two iterations."""
+    g = torch.Generator().manual_seed(21)
+    x = torch.randn(2, 3, 64, 128, generator=g).to(DEV)
+    xt = torch.randn(2, 3, 64, 128, generator=g).to(DEV)
+    y = torch.randint(0, 20, (2, 64, 128), generator=g).to(DEV)
+    ce, bce = losses.CrossEntropyLoss(ignore_index=19), losses.BCEWithLogitsLoss()
+    runs = []
+    with rtsds_amd.precision(dt):
+        for fused in (False, True):
+            for cls in (TinyDomainDiscriminator, DomainDiscriminator):
+                torch.manual_seed(3)
+                net = BiSeNet(19, "resnet18").to(DEV).train()
+                disc = cls(19).to(DEV).train()
+                if not fused:
+                    disc.accepts_padded_probs = False
+                opt = optim.Adam(net.parameters(), lr=1e-3)
+                dopt = optim.Adam(disc.parameters(), lr=1e-3, weight_decay=1e-4)
+                logs = []
+                for _ in range(2):
+                    logs.append([float(v) for v in rtrain.da_step(net, disc, opt, dopt, ce, bce, x, y, xt, 0.1, 2)])
+                torch.cuda.synchronize()
+                st = {k: v.detach().float().cpu().clone() for k, v in
+                      list(net.state_dict().items()) + list(disc.state_dict().items())}
+                st.update({f"m{i}": a.m.cpu() for i, a in enumerate(opt.arenas() + dopt.arenas())})
+                runs.append((cls.__name__, logs, st))
+    for (n0, l0, s0), (n1, l1, s1) in zip(runs[:2], runs[2:]):
+        assert n0 == n1 and l0 == l1, (n0, l0, l1)
+        for k in s0:
+            assert torch.equal(s0[k], s1[k]), (n0, k)

@@ -683,3 +683,35 @@ def test_conv_bn_stats_epilogue(shape):
     _close(y, yr, torch.bfloat16, "y")
     rm_ref = 0.1 * TF.conv2d(x, wr, None, 1, 1).mean(dim=(0, 2, 3))
     _close(bn.running_mean, rm_ref, torch.bfloat16, "running_mean")
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("geo", [((2, 19, 16, 32), (128, 256)), ((1, 19, 13, 17), (97, 129))])
+def test_upsample_softmax_fused(dt, geo):
+    """functional.upsample_softmax (rtsds_upsoftmax_fwd / _bwd): forward and input gradient vs
+    torch fp64 (interpolate bilinear + softmax), bit-identical to the unfused HIP chain
+    (interpolate_geometry -> softmax), and zero in the padding channels."""
+    (n, c, h, w), (ho, wo) = geo
+    g = torch.Generator().manual_seed(n * 7 + h)
+    x = torch.randn(n, c, h, w, generator=g, dtype=torch.float64) * 3
+    gy = torch.randn(n, c, ho, wo, generator=g, dtype=torch.float64)
+    if dt == torch.bfloat16:
+        x, gy = x.bfloat16().double(), gy.bfloat16().double()
+    xr = x.clone().requires_grad_()
+    yr = torch.softmax(TF.interpolate(xr, size=(ho, wo), mode="bilinear", align_corners=False), dim=1)
+    yr.backward(gy)
+    xd = _dev(x, dt).requires_grad_()
+    geo_ = F.upsample_geometry(xd, size=(ho, wo))
+    y = F.upsample_softmax(xd, geo_)
+    assert F.is_padded_input(y)
+    y.backward(_dev(gy, dt))
+    pad = y.as_strided((n, ho, wo, 32), (ho * wo * 32, wo * 32, 32, 1))[..., c:]
+    assert float(pad.abs().max()) == 0.0
+    _close(y, yr, dt, "y")
+    _close(xd.grad, xr.grad, dt, "dx", tol=2e-4 if dt == torch.float32 else 5e-2)
+    # the unfused chain on the same input
+    x2 = _dev(x, dt).requires_grad_()
+    y2 = F.softmax(F.interpolate_geometry(x2, geo_), dim=1)
+    y2.backward(_dev(gy, dt))
+    assert torch.equal(y.detach().float(), y2.detach().float())
+    assert torch.equal(xd.grad, x2.grad)
