@@ -63,6 +63,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-infer", action="store_true")
     ap.add_argument("--conv-report", action="store_true")
+    ap.add_argument("--da-unfused", action="store_true",
+                    help="A/B: discriminator input through interpolate + softmax (no fused upsample_softmax)")
     ap.add_argument("--no-conv-profile", action="store_true", help="skip the event-timed roofline step")
     ap.add_argument("--graph", default="auto", choices=["auto", "on", "off"],
                     help="replay the iteration as hipGraph segments (auto = on; under data parallelism "
@@ -143,6 +145,8 @@ def build(args, dev, rank):
         return net, x, set_lr, core, [opt]
     from rtsds_amd.models.domain_shift.adversarial.model import TinyDomainDiscriminator
     disc = TinyDomainDiscriminator(NC).to(dev).train()
+    if args.da_unfused:
+        disc.accepts_padded_probs = False
     dopt = optim.Adam(disc.parameters(), lr=1e-4, weight_decay=1e-4)
     bce = losses.BCEWithLogitsLoss()
     xt, _ = synthetic_batch(args.batch, 43 + 2 * rank, dev, h, w)

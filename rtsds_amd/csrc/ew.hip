@@ -4,6 +4,7 @@
 // All activations are NHWC; per-pixel channel vectors are contiguous.
 #include "common.h"
 #include <algorithm>
+#include <climits>
 
 static inline int ew_blocks(long work, int per_block = 256, int cap = 8192) {
   return (int)std::max<long>(1, std::min<long>(cap, (work + per_block - 1) / per_block));
@@ -802,116 +803,6 @@ extern "C" int rtsds_bilinear_bwd(const void* dy, void* dx, int n, int hi, int w
 }
 
 
-// ------------------------------------------------------------------ fused resize + softmax
-// The discriminator input of the DA iteration (train.py:225,245,256): softmax over classes of
-// the bilinearly resized head, zero-padded to y_ld channels so the discriminator's first conv
-// reads it without a separate pad pass.  The logits are the bilinear_fwd values rounded to T
-// and the softmax is softmax_fwd_staged's arithmetic (two expf passes, sequential sum), so the
-// probabilities are bit-identical to the unfused resize -> softmax -> pad chain; the resized
-// logits and the unpadded probabilities never exist in memory.  One thread per output pixel,
-// the four source rows of 19 classes from L2 (the low-res head is a few MB).
-static const int kUpsmMaxC = 32;
-template <typename T>
-__global__ void upsoftmax_fwd_kernel(const T* __restrict__ x, T* __restrict__ y, int n, int hi, int wi, int c, int ho, int wo,
-                                     float sh, float sw, int yld) {
-  const long total = (long)n * ho * wo;
-  GRID_STRIDE(p, total) {
-    const int ow = (int)(p % wo);
-    const long q = p / wo;
-    const int oh = (int)(q % ho), img = (int)(q / ho);
-    int h0, h1, w0, w1;
-    float lh0, lh1, lw0, lw1;
-    bil_src(oh, sh, hi, h0, h1, lh0, lh1);
-    bil_src(ow, sw, wi, w0, w1, lw0, lw1);
-    const T* b = x + (long)img * hi * wi * c;
-    const T* p00 = b + ((long)h0 * wi + w0) * c;
-    const T* p01 = b + ((long)h0 * wi + w1) * c;
-    const T* p10 = b + ((long)h1 * wi + w0) * c;
-    const T* p11 = b + ((long)h1 * wi + w1) * c;
-    float z[kUpsmMaxC];
-    float m = -INFINITY;
-#pragma unroll
-    for (int k = 0; k < kUpsmMaxC; ++k) {
-      if (k < c) {
-        z[k] = to_f(from_f<T>(bil_mix(to_f(p00[k]), to_f(p01[k]), to_f(p10[k]), to_f(p11[k]), lh0, lh1, lw0, lw1)));
-        m = fmaxf(m, z[k]);
-      }
-    }
-    float sum = 0.f;
-#pragma unroll
-    for (int k = 0; k < kUpsmMaxC; ++k)
-      if (k < c) sum += expf(z[k] - m);
-    const float iz = 1.f / sum;
-    T* o = y + p * yld;
-#pragma unroll
-    for (int k = 0; k < kUpsmMaxC; ++k)
-      if (k < yld) o[k] = from_f<T>(k < c ? expf(z[k] - m) * iz : 0.f);
-  }
-}
-// Backward, first (width) pass of the resize adjoint with the softmax backward fused in:
-// tmp[img][oh][iw][k] = sum_ow w(ow->iw) T(p_k (dp_k - sum_j p_j dp_j)) at (oh, ow) -- the
-// softmax_bwd_staged value rounded to T, accumulated in bilinear_bwd_w_kernel's order, so the
-// result is bit-identical to softmax backward followed by the resize backward; the vertical
-// pass is bilinear_bwd_h_kernel.  One thread per (oh, iw), all classes.
-template <typename T>
-__global__ void upsoftmax_bwd_w_kernel(const T* __restrict__ dy, int dyld, const T* __restrict__ y, int yld,
-                                       float* __restrict__ tmp, int n, int wi, int c, int ho, int wo, float sw) {
-  const long total = (long)n * ho * wi;
-  GRID_STRIDE(i, total) {
-    const int iw = (int)(i % wi);
-    const long row = i / wi;  // img * ho + oh
-    int lo, hi;
-    bil_wsum_range(iw, sw, wi, wo, lo, hi);
-    float acc[kUpsmMaxC];
-#pragma unroll
-    for (int k = 0; k < kUpsmMaxC; ++k) acc[k] = 0.f;
-    for (int ow = lo; ow <= hi; ++ow) {
-      const float wt = bil_weight(ow, iw, sw, wi);
-      if (wt == 0.f) continue;
-      const T* g = dy + (row * wo + ow) * dyld;
-      const T* pr = y + (row * wo + ow) * yld;
-      float dot = 0.f;
-#pragma unroll
-      for (int k = 0; k < kUpsmMaxC; ++k)
-        if (k < c) dot = fmaf(to_f(g[k]), to_f(pr[k]), dot);
-#pragma unroll
-      for (int k = 0; k < kUpsmMaxC; ++k)
-        if (k < c) acc[k] = fmaf(wt, to_f(from_f<T>(to_f(pr[k]) * (to_f(g[k]) - dot))), acc[k]);
-    }
-    float* o = tmp + i * c;
-#pragma unroll
-    for (int k = 0; k < kUpsmMaxC; ++k)
-      if (k < c) o[k] = acc[k];
-  }
-}
-extern "C" int rtsds_upsoftmax_fwd(const void* x, void* y, int n, int hi, int wi, int c, int ho, int wo, float scale_h,
-                                   float scale_w, int y_ld, int dtype, void* stream) {
-  const long total = (long)n * ho * wo;
-  if (total <= 0 || hi <= 0 || wi <= 0 || c <= 0 || c > kUpsmMaxC || y_ld < c || y_ld > kUpsmMaxC) return RTSDS_ERR_SHAPE;
-  DISPATCH_T(dtype, hipLaunchKernelGGL(upsoftmax_fwd_kernel<T>, dim3(ew_blocks(total)), dim3(256), 0, (hipStream_t)stream,
-                                       (const T*)x, (T*)y, n, hi, wi, c, ho, wo, scale_h, scale_w, y_ld));
-  RET_LAUNCH();
-}
-extern "C" size_t rtsds_upsoftmax_bwd_workspace(int n, int hi, int wi, int c, int ho, int wo) {
-  return rtsds_bilinear_bwd_workspace(n, hi, wi, c, ho, wo);
-}
-extern "C" int rtsds_upsoftmax_bwd(const void* dy, int dy_ld, const void* y, int y_ld, void* dx, int n, int hi, int wi, int c,
-                                   int ho, int wo, float scale_h, float scale_w, int dtype, void* ws, size_t ws_bytes,
-                                   void* stream) {
-  const long total = (long)n * hi * wi * c;
-  if (total <= 0 || ho <= 0 || wo <= 0 || c > kUpsmMaxC || dy_ld < c || y_ld < c) return RTSDS_ERR_SHAPE;
-  if (ws_bytes < rtsds_upsoftmax_bwd_workspace(n, hi, wi, c, ho, wo)) return RTSDS_ERR_WORKSPACE;
-  hipStream_t st = (hipStream_t)stream;
-  float* tmp = (float*)ws;
-  DISPATCH_T(dtype, {
-    hipLaunchKernelGGL(upsoftmax_bwd_w_kernel<T>, dim3(ew_blocks((long)n * ho * wi)), dim3(256), 0, st, (const T*)dy, dy_ld,
-                       (const T*)y, y_ld, tmp, n, wi, c, ho, wo, scale_w);
-    hipLaunchKernelGGL(bilinear_bwd_h_kernel<T>, dim3(ew_blocks(total)), dim3(256), 0, st, (const float*)tmp, (T*)dx, n, hi,
-                       wi, c, ho, scale_h);
-  });
-  RET_LAUNCH();
-}
-
 // ------------------------------------------------------------------ LDS-staged per-pixel kernels
 // The per-pixel channel loops (C = 19 classes) read/write rows of C*sizeof(T) bytes (38 B for
 // bf16) that are not 16-B aligned per pixel.  These variants move a block's 256 pixels
@@ -944,6 +835,165 @@ RT_DEV void stage_out(T* __restrict__ g, const T* s, int nel) {
     for (int i = threadIdx.x; i < nel; i += blockDim.x) g[i] = s[i];
   }
 }
+// ------------------------------------------------------------------ fused resize + softmax
+// The discriminator input of the DA iteration (train.py:225,245,256): softmax over classes of
+// the bilinearly resized head, zero-padded to y_ld channels so the discriminator's first conv
+// reads it without a separate pad pass.  The logits are the bilinear_fwd values rounded to T
+// and the softmax is softmax_fwd_staged's arithmetic (two expf passes, sequential sum), so the
+// probabilities are bit-identical to the unfused resize -> softmax -> pad chain; the resized
+// logits and the unpadded probabilities never exist in memory.
+//   forward:  one block per 256 output pixels of a row; thread per pixel, the 4 taps from L2
+//             (neighbouring lanes share source pixels), the padded result staged in LDS and
+//             written with 16-B stores (the row segment is contiguous).
+//   backward: one block per (row, tile of kUpsmTW input columns): the output-pixel segment the
+//             tile's width adjoint reads is staged (dy and p, coalesced) in LDS, the softmax
+//             backward T(p_k (dp_k - sum_j p_j dp_j)) is formed in place, then thread per
+//             (input column, class) accumulates the width adjoint in bilinear_bwd_w_kernel's
+//             order; the vertical pass is bilinear_bwd_h_kernel.
+static const int kUpsmMaxC = 32;
+static const int kUpsmPix = 256;
+static const int kUpsmLds = 48 * 1024;
+template <typename T>
+__global__ void __launch_bounds__(256) upsoftmax_fwd_kernel(const T* __restrict__ x, T* __restrict__ y, int hi, int wi, int c,
+                                                            int ho, int wo, float sh, float sw, int yld, int tiles) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  T* buf = (T*)smem_raw;
+  const int tile = blockIdx.x % tiles;
+  const long row = blockIdx.x / tiles;  // img * ho + oh
+  const int oh = (int)(row % ho), img = (int)(row / ho);
+  const int ow0 = tile * kUpsmPix, np = min(kUpsmPix, wo - ow0);
+  const int ow = ow0 + (int)threadIdx.x;
+  if ((int)threadIdx.x < np) {
+    int h0, h1, w0, w1;
+    float lh0, lh1, lw0, lw1;
+    bil_src(oh, sh, hi, h0, h1, lh0, lh1);
+    bil_src(ow, sw, wi, w0, w1, lw0, lw1);
+    const T* b = x + (long)img * hi * wi * c;
+    const T* p00 = b + ((long)h0 * wi + w0) * c;
+    const T* p01 = b + ((long)h0 * wi + w1) * c;
+    const T* p10 = b + ((long)h1 * wi + w0) * c;
+    const T* p11 = b + ((long)h1 * wi + w1) * c;
+    float z[kUpsmMaxC];
+    float m = -INFINITY;
+#pragma unroll
+    for (int k = 0; k < kUpsmMaxC; ++k) {
+      if (k < c) {
+        z[k] = to_f(from_f<T>(bil_mix(to_f(p00[k]), to_f(p01[k]), to_f(p10[k]), to_f(p11[k]), lh0, lh1, lw0, lw1)));
+        m = fmaxf(m, z[k]);
+      }
+    }
+    float sum = 0.f;
+#pragma unroll
+    for (int k = 0; k < kUpsmMaxC; ++k)
+      if (k < c) sum += expf(z[k] - m);
+    const float iz = 1.f / sum;
+    T* o = buf + threadIdx.x * yld;
+#pragma unroll
+    for (int k = 0; k < kUpsmMaxC; ++k)
+      if (k < yld) o[k] = from_f<T>(k < c ? expf(z[k] - m) * iz : 0.f);
+  }
+  __syncthreads();
+  stage_out(y + (row * wo + ow0) * yld, buf, np * yld);
+}
+// exact output-pixel span [lo, hi] read by input columns [iw0, iw1] (bil_wsum_range bounds)
+__host__ __device__ inline void upsm_span(int iw0, int iw1, float sw, int wi, int wo, int& lo, int& hi) {
+  lo = (int)floorf(((float)iw0 - 0.5f) / sw - 0.5f) - 1;
+  hi = (int)ceilf(((float)iw1 + 1.5f) / sw - 0.5f) + 1;
+  lo = lo < 0 ? 0 : lo;
+  hi = hi > wo - 1 ? wo - 1 : hi;
+}
+template <typename T>
+__global__ void __launch_bounds__(256) upsoftmax_bwd_w_kernel(const T* __restrict__ dy, int dyld, const T* __restrict__ y,
+                                                              int yld, float* __restrict__ tmp, int wi, int c, int wo, float sw,
+                                                              int tw, int tiles, int cap) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  T* sg = (T*)smem_raw;
+  T* sy = sg + cap * c;
+  const int tile = blockIdx.x % tiles;
+  const long row = blockIdx.x / tiles;  // img * ho + oh
+  const int iw0 = tile * tw, iw1 = min(wi, iw0 + tw) - 1;
+  int olo, ohi;
+  upsm_span(iw0, iw1, sw, wi, wo, olo, ohi);
+  const int cnt = ohi - olo + 1;  // <= cap (host: exact maximum over the tiles)
+  const T* gr = dy + (row * wo + olo) * dyld;
+  const T* yr = y + (row * wo + olo) * yld;
+  for (int e = threadIdx.x; e < cnt * c; e += blockDim.x) {
+    const int q = e / c, k = e - q * c;
+    sg[e] = gr[(long)q * dyld + k];
+    sy[e] = yr[(long)q * yld + k];
+  }
+  __syncthreads();
+  for (int q = threadIdx.x; q < cnt; q += blockDim.x) {
+    T* g = sg + q * c;
+    const T* pr = sy + q * c;
+    float dot = 0.f;
+    for (int k = 0; k < c; ++k) dot = fmaf(to_f(g[k]), to_f(pr[k]), dot);
+    for (int k = 0; k < c; ++k) g[k] = from_f<T>(to_f(pr[k]) * (to_f(g[k]) - dot));
+  }
+  __syncthreads();
+  const int nw = iw1 - iw0 + 1;
+  for (int e = threadIdx.x; e < nw * c; e += blockDim.x) {
+    const int iw = iw0 + e / c, k = e % c;
+    int lo, hi;
+    bil_wsum_range(iw, sw, wi, wo, lo, hi);
+    float acc = 0.f;
+    for (int ow = lo; ow <= hi; ++ow) {
+      const float wt = bil_weight(ow, iw, sw, wi);
+      if (wt != 0.f) acc = fmaf(wt, to_f(sg[(ow - olo) * c + k]), acc);
+    }
+    tmp[(row * wi + iw) * c + k] = acc;
+  }
+}
+extern "C" int rtsds_upsoftmax_fwd(const void* x, void* y, int n, int hi, int wi, int c, int ho, int wo, float scale_h,
+                                   float scale_w, int y_ld, int dtype, void* stream) {
+  if (n <= 0 || ho <= 0 || wo <= 0 || hi <= 0 || wi <= 0 || c <= 0 || c > kUpsmMaxC || y_ld < c || y_ld > kUpsmMaxC)
+    return RTSDS_ERR_SHAPE;
+  const int tiles = rt_cdiv(wo, kUpsmPix);
+  const long blocks = (long)n * ho * tiles;
+  if (blocks > INT_MAX) return RTSDS_ERR_UNSUPPORTED;
+  DISPATCH_T(dtype, hipLaunchKernelGGL(upsoftmax_fwd_kernel<T>, dim3((unsigned)blocks), dim3(256), kUpsmPix * y_ld * sizeof(T),
+                                       (hipStream_t)stream, (const T*)x, (T*)y, hi, wi, c, ho, wo, scale_h, scale_w, y_ld, tiles));
+  RET_LAUNCH();
+}
+extern "C" size_t rtsds_upsoftmax_bwd_workspace(int n, int hi, int wi, int c, int ho, int wo) {
+  return rtsds_bilinear_bwd_workspace(n, hi, wi, c, ho, wo);
+}
+// widest tile (<= 64 input columns) whose staged dy / p segment fits kUpsmLds; cap = its
+// exact largest segment
+static bool upsm_tiling(int wi, int wo, int c, float sw, size_t esz, int& tw, int& cap) {
+  for (tw = 64; tw >= 1; tw /= 2) {
+    cap = 0;
+    for (int iw0 = 0; iw0 < wi; iw0 += tw) {
+      int lo, hi;
+      upsm_span(iw0, std::min(wi, iw0 + tw) - 1, sw, wi, wo, lo, hi);
+      cap = std::max(cap, hi - lo + 1);
+    }
+    if ((size_t)cap * c * 2 * esz <= (size_t)kUpsmLds) return true;
+  }
+  return false;
+}
+extern "C" int rtsds_upsoftmax_bwd(const void* dy, int dy_ld, const void* y, int y_ld, void* dx, int n, int hi, int wi, int c,
+                                   int ho, int wo, float scale_h, float scale_w, int dtype, void* ws, size_t ws_bytes,
+                                   void* stream) {
+  const long total = (long)n * hi * wi * c;
+  if (total <= 0 || ho <= 0 || wo <= 0 || c > kUpsmMaxC || dy_ld < c || y_ld < c) return RTSDS_ERR_SHAPE;
+  if (ws_bytes < rtsds_upsoftmax_bwd_workspace(n, hi, wi, c, ho, wo)) return RTSDS_ERR_WORKSPACE;
+  hipStream_t st = (hipStream_t)stream;
+  float* tmp = (float*)ws;
+  DISPATCH_T(dtype, {
+    int tw, cap;
+    if (!upsm_tiling(wi, wo, c, scale_w, sizeof(T), tw, cap)) return RTSDS_ERR_UNSUPPORTED;
+    const int tiles = rt_cdiv(wi, tw);
+    const long blocks = (long)n * ho * tiles;
+    if (blocks > INT_MAX) return RTSDS_ERR_UNSUPPORTED;
+    hipLaunchKernelGGL(upsoftmax_bwd_w_kernel<T>, dim3((unsigned)blocks), dim3(256), (size_t)cap * c * 2 * sizeof(T), st,
+                       (const T*)dy, dy_ld, (const T*)y, y_ld, tmp, wi, c, wo, scale_w, tw, tiles, cap);
+    hipLaunchKernelGGL(bilinear_bwd_h_kernel<T>, dim3(ew_blocks(total)), dim3(256), 0, st, (const float*)tmp, (T*)dx, n, hi,
+                       wi, c, ho, scale_h);
+  });
+  RET_LAUNCH();
+}
+
 // Staged variants need NHWC-contiguous logits with c <= kStageMaxC.
 static const int kStageMaxC = 64;
 static inline bool stage_ok(long sn, long sc, long shw, long hw, int c) {

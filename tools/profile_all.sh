@@ -6,6 +6,10 @@
 set -e
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 tag=$1; shift
+# heartbeat: PMC passes print nothing for minutes on the larger workloads
+( while sleep 50; do date >> gpurun_out/prof_${tag}_heartbeat; done ) &
+hb=$!
+trap "kill $hb" EXIT
 wls=${@:-bisenet-seg bisenet-da deeplab-seg deeplab-da}
 for wl in $wls; do
   o=gpurun_out/prof_${tag}_$wl; mkdir -p $o
