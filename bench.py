@@ -111,12 +111,16 @@ def cpu_baseline(seconds=15.0):
 
 
 def conv_traffic(args, dtype):
-    """HBM bytes per step of the conv kernels, from the committed rocprofv3 --pmc passes of this
-    same bench command (tools/pmc_bench.sh + tools/pmc_traffic.py; gfx950 FETCH_SIZE x2)."""
-    path = os.path.join(ROOT, "profiles", "conv_traffic.json")
-    if args.workload != "bisenet-seg" or args.batch != 8 or dtype != torch.bfloat16 or not os.path.exists(path):
+    """HBM bytes per step of the conv kernels, from the newest committed rocprofv3 --pmc
+    FETCH_SIZE / WRITE_SIZE passes of this same workload at its default batch in bf16
+    (tools/profile_all.sh -> profiles/r<NN>_<workload>_pmc_traffic.json; gfx950 FETCH_SIZE x2)."""
+    import glob
+    if args.batch != WORKLOADS[args.workload][2] or dtype != torch.bfloat16:
         return None
-    with open(path) as f:
+    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{args.workload}_pmc_traffic.json")))
+    if not paths:
+        return None
+    with open(paths[-1]) as f:
         return json.load(f)["conv_gemm_kernel_bytes_per_step"]
 
 
