@@ -842,58 +842,118 @@ RT_DEV void stage_out(T* __restrict__ g, const T* s, int nel) {
 // and the softmax is softmax_fwd_staged's arithmetic (two expf passes, sequential sum), so the
 // probabilities are bit-identical to the unfused resize -> softmax -> pad chain; the resized
 // logits and the unpadded probabilities never exist in memory.
-//   forward:  one block per 256 output pixels of a row; thread per pixel, the 4 taps from L2
-//             (neighbouring lanes share source pixels), the padded result staged in LDS and
-//             written with 16-B stores (the row segment is contiguous).
-//   backward: one block per (row, tile of kUpsmTW input columns): the output-pixel segment the
-//             tile's width adjoint reads is staged (dy and p, coalesced) in LDS, the softmax
-//             backward T(p_k (dp_k - sum_j p_j dp_j)) is formed in place, then thread per
-//             (input column, class) accumulates the width adjoint in bilinear_bwd_w_kernel's
-//             order; the vertical pass is bilinear_bwd_h_kernel.
+//   forward:  one block per 256 output pixels of a row.  The two low-res source rows the tile
+//             reads (a few dozen pixels for x8) are staged once in LDS as fp32 (coalesced), each
+//             thread blends its pixel's 4 taps from LDS, and the tile's padded rows leave through
+//             LDS as lane-consecutive 16-B chunks (HBM-bound on the padded output).
+//   backward: one block per (row, tile of up to 64 input columns): the dy segment the tile's
+//             width adjoint reads is staged in LDS (coalesced), then thread per output pixel
+//             forms the softmax backward T(p_k (dp_k - sum_j p_j dp_j)) in place (its p row by
+//             16-B loads); the tile's bilinear
+//             weights are tabulated once in LDS; thread per (input column, class) accumulates
+//             the width adjoint in bilinear_bwd_w_kernel's order (ascending output column,
+//             zero weights skipped).  The vertical pass is bilinear_bwd_h_kernel.
 static const int kUpsmMaxC = 32;
 static const int kUpsmPix = 256;
 static const int kUpsmLds = 48 * 1024;
-template <typename T>
-__global__ void __launch_bounds__(256) upsoftmax_fwd_kernel(const T* __restrict__ x, T* __restrict__ y, int hi, int wi, int c,
+// one output pixel of upsoftmax_fwd_kernel: blend, softmax, padded row into the LDS tile
+template <typename T, bool STAGED, int CC>
+RT_DEV void upsm_pixel(const T* __restrict__ r0, const T* __restrict__ r1, const float* src, T* o, int wlo, int n1, int c_, int ow,
+                       float sw, int wi, float lh0, float lh1, int yld) {
+  const int c = CC > 0 ? CC : c_;
+  int w0, w1;
+  float lw0, lw1;
+  bil_src(ow, sw, wi, w0, w1, lw0, lw1);
+  float z[kUpsmMaxC];
+  float m = -INFINITY;
+#pragma unroll
+  for (int k = 0; k < kUpsmMaxC; ++k) {
+    if (k < c) {
+      float p00, p01, p10, p11;
+      if (STAGED) {
+        p00 = src[(w0 - wlo) * c + k];
+        p01 = src[(w1 - wlo) * c + k];
+        p10 = src[n1 + (w0 - wlo) * c + k];
+        p11 = src[n1 + (w1 - wlo) * c + k];
+      } else {
+        p00 = to_f(r0[(long)w0 * c + k]);
+        p01 = to_f(r0[(long)w1 * c + k]);
+        p10 = to_f(r1[(long)w0 * c + k]);
+        p11 = to_f(r1[(long)w1 * c + k]);
+      }
+      z[k] = to_f(from_f<T>(bil_mix(p00, p01, p10, p11, lh0, lh1, lw0, lw1)));
+      m = fmaxf(m, z[k]);
+    }
+  }
+  float sum = 0.f;  // exp(z - m) evaluated once per class (softmax_fwd_staged evaluates the same
+                    // expf twice: identical values)
+#pragma unroll
+  for (int k = 0; k < kUpsmMaxC; ++k)
+    if (k < c) {
+      z[k] = expf(z[k] - m);
+      sum += z[k];
+    }
+  const float iz = 1.f / sum;
+  // the padded row goes through LDS so the tile leaves as lane-consecutive 16-B chunks (the
+  // tile's rows are contiguous in y): full-line writes instead of 64-B-strided partial ones
+  if (sizeof(T) == 2 && yld == 32) {  // 4 x 16-B LDS writes, chunk q at slot q ^ (pixel & 3)
+    typedef typename VecT<T>::v16 V16;
+    const int sw4 = ow & 3;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      V16 v;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = from_f<T>(q * 8 + j < c ? z[q * 8 + j] * iz : 0.f);
+      *(V16*)(o + (q ^ sw4) * 8) = v;
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < kUpsmMaxC; ++k)
+      if (k < yld) o[k] = from_f<T>(k < c ? z[k] * iz : 0.f);
+  }
+}
+template <typename T, bool STAGED, int CC>  // CC > 0: compile-time class count (19), 0: runtime c
+__global__ void __launch_bounds__(256) upsoftmax_fwd_kernel(const T* __restrict__ x, T* __restrict__ y, int hi, int wi, int c_,
                                                             int ho, int wo, float sh, float sw, int yld, int tiles) {
-  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-  T* buf = (T*)smem_raw;
+  const int c = CC > 0 ? CC : c_;
+  extern __shared__ __attribute__((aligned(16))) float src[];  // STAGED: [2][ncols][c]
   const int tile = blockIdx.x % tiles;
   const long row = blockIdx.x / tiles;  // img * ho + oh
   const int oh = (int)(row % ho), img = (int)(row / ho);
   const int ow0 = tile * kUpsmPix, np = min(kUpsmPix, wo - ow0);
-  const int ow = ow0 + (int)threadIdx.x;
-  if ((int)threadIdx.x < np) {
-    int h0, h1, w0, w1;
-    float lh0, lh1, lw0, lw1;
-    bil_src(oh, sh, hi, h0, h1, lh0, lh1);
-    bil_src(ow, sw, wi, w0, w1, lw0, lw1);
-    const T* b = x + (long)img * hi * wi * c;
-    const T* p00 = b + ((long)h0 * wi + w0) * c;
-    const T* p01 = b + ((long)h0 * wi + w1) * c;
-    const T* p10 = b + ((long)h1 * wi + w0) * c;
-    const T* p11 = b + ((long)h1 * wi + w1) * c;
-    float z[kUpsmMaxC];
-    float m = -INFINITY;
-#pragma unroll
-    for (int k = 0; k < kUpsmMaxC; ++k) {
-      if (k < c) {
-        z[k] = to_f(from_f<T>(bil_mix(to_f(p00[k]), to_f(p01[k]), to_f(p10[k]), to_f(p11[k]), lh0, lh1, lw0, lw1)));
-        m = fmaxf(m, z[k]);
-      }
+  const int tid = threadIdx.x;
+  int h0, h1;
+  float lh0, lh1;
+  bil_src(oh, sh, hi, h0, h1, lh0, lh1);
+  const T* r0 = x + ((long)img * hi + h0) * wi * c;
+  const T* r1 = x + ((long)img * hi + h1) * wi * c;
+  int wlo = 0, n1 = 0;
+  if (STAGED) {  // taps are monotone in ow: columns [w0(ow0), w1(last)] cover the tile
+    int a0, a1, b0, b1;
+    float t0, t1;
+    bil_src(ow0, sw, wi, a0, a1, t0, t1);
+    bil_src(ow0 + np - 1, sw, wi, b0, b1, t0, t1);
+    wlo = a0;
+    n1 = (b1 - a0 + 1) * c;
+    for (int e = tid; e < n1; e += 256) {
+      src[e] = to_f(r0[(long)wlo * c + e]);
+      src[n1 + e] = to_f(r1[(long)wlo * c + e]);
     }
-    float sum = 0.f;
-#pragma unroll
-    for (int k = 0; k < kUpsmMaxC; ++k)
-      if (k < c) sum += expf(z[k] - m);
-    const float iz = 1.f / sum;
-    T* o = buf + threadIdx.x * yld;
-#pragma unroll
-    for (int k = 0; k < kUpsmMaxC; ++k)
-      if (k < yld) o[k] = from_f<T>(k < c ? expf(z[k] - m) * iz : 0.f);
+    __syncthreads();
   }
-  __syncthreads();
-  stage_out(y + (row * wo + ow0) * yld, buf, np * yld);
+  T* outbuf = (T*)(src + ((2 * n1 + 3) & ~3));  // [256][yld], 16-B aligned
+  if (tid < np) upsm_pixel<T, STAGED, CC>(r0, r1, src, outbuf + tid * yld, wlo, n1, c, ow0 + tid, sw, wi, lh0, lh1, yld);
+  __syncthreads();  // every lane reaches the same barrier (no early exit)
+  T* dst = y + (row * wo + ow0) * yld;
+  if (sizeof(T) == 2 && yld == 32) {  // un-swizzle: LDS read linear, global chunk q = slot ^ (pixel & 3)
+    typedef typename VecT<T>::v16 V16;
+    for (int i = tid; i < np * 4; i += 256) {
+      const int t = i >> 2, q = (i & 3) ^ ((ow0 + t) & 3);
+      *(V16*)(dst + t * 32 + q * 8) = *(const V16*)(outbuf + i * 8);
+    }
+  } else {
+    stage_out(dst, outbuf, np * yld);
+  }
 }
 // exact output-pixel span [lo, hi] read by input columns [iw0, iw1] (bil_wsum_range bounds)
 __host__ __device__ inline void upsm_span(int iw0, int iw1, float sw, int wi, int wo, int& lo, int& hi) {
@@ -902,47 +962,97 @@ __host__ __device__ inline void upsm_span(int iw0, int iw1, float sw, int wi, in
   lo = lo < 0 ? 0 : lo;
   hi = hi > wo - 1 ? wo - 1 : hi;
 }
-template <typename T>
+template <typename T, int CC>  // CC > 0: compile-time class count (19), 0: runtime c
 __global__ void __launch_bounds__(256) upsoftmax_bwd_w_kernel(const T* __restrict__ dy, int dyld, const T* __restrict__ y,
-                                                              int yld, float* __restrict__ tmp, int wi, int c, int wo, float sw,
-                                                              int tw, int tiles, int cap) {
-  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-  T* sg = (T*)smem_raw;
-  T* sy = sg + cap * c;
+                                                              int yld, float* __restrict__ tmp, int wi, int c_, int wo, float sw,
+                                                              int tw, int tiles, int cap, int maxw) {
+  const int c = CC > 0 ? CC : c_;
+  extern __shared__ __attribute__((aligned(16))) float smf[];
+  float* wt = smf;                       // [tw][maxw]: weights of output columns lo(iw) + j
+  int* wlo = (int*)(wt + tw * maxw);     // [tw]
+  T* sgt = (T*)(wlo + tw);               // [cap][c]: dy, then the softmax backward in place
+  const int tid = threadIdx.x;
   const int tile = blockIdx.x % tiles;
   const long row = blockIdx.x / tiles;  // img * ho + oh
-  const int iw0 = tile * tw, iw1 = min(wi, iw0 + tw) - 1;
+  const int iw0 = tile * tw, iw1 = min(wi, iw0 + tw) - 1, nw = iw1 - iw0 + 1;
   int olo, ohi;
   upsm_span(iw0, iw1, sw, wi, wo, olo, ohi);
   const int cnt = ohi - olo + 1;  // <= cap (host: exact maximum over the tiles)
-  const T* gr = dy + (row * wo + olo) * dyld;
-  const T* yr = y + (row * wo + olo) * yld;
-  for (int e = threadIdx.x; e < cnt * c; e += blockDim.x) {
-    const int q = e / c, k = e - q * c;
-    sg[e] = gr[(long)q * dyld + k];
-    sy[e] = yr[(long)q * yld + k];
+  // dy segment -> LDS as T, coalesced (rows of pitch c; contiguous in memory when dyld == c)
+  const T* gseg = dy + (row * wo + olo) * dyld;
+  if (dyld == c) {
+    for (int e = tid; e < cnt * c; e += 256) sgt[e] = gseg[e];
+  } else {
+    for (int e = tid; e < cnt * c; e += 256) {
+      const int q = e / c;
+      sgt[e] = gseg[(long)q * dyld + (e - q * c)];
+    }
   }
   __syncthreads();
-  for (int q = threadIdx.x; q < cnt; q += blockDim.x) {
-    T* g = sg + q * c;
-    const T* pr = sy + q * c;
+  // thread per output pixel: p row (16-B vectors when the pitch allows), softmax backward in place
+  for (int q = tid; q < cnt; q += 256) {
+    const T* pr = y + (row * wo + olo + q) * yld;
+    float pv[kUpsmMaxC];
+    if (sizeof(T) == 2 && (yld & 7) == 0) {
+      typedef typename VecT<T>::v16 V16;
+#pragma unroll
+      for (int v = 0; v < kUpsmMaxC / 8; ++v)
+        if (v * 8 < c) {
+          const V16 t = *(const V16*)(pr + v * 8);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) pv[v * 8 + j] = to_f(t[j]);
+        }
+    } else {
+#pragma unroll
+      for (int k = 0; k < kUpsmMaxC; ++k)
+        if (k < c) pv[k] = to_f(pr[k]);
+    }
+    T* g = sgt + q * c;
+    float gv[kUpsmMaxC];
     float dot = 0.f;
-    for (int k = 0; k < c; ++k) dot = fmaf(to_f(g[k]), to_f(pr[k]), dot);
-    for (int k = 0; k < c; ++k) g[k] = from_f<T>(to_f(pr[k]) * (to_f(g[k]) - dot));
+#pragma unroll
+    for (int k = 0; k < kUpsmMaxC; ++k)
+      if (k < c) {
+        gv[k] = to_f(g[k]);
+        dot = fmaf(gv[k], pv[k], dot);
+      }
+#pragma unroll
+    for (int k = 0; k < kUpsmMaxC; ++k)
+      if (k < c) g[k] = from_f<T>(pv[k] * (gv[k] - dot));
   }
-  __syncthreads();
-  const int nw = iw1 - iw0 + 1;
-  for (int e = threadIdx.x; e < nw * c; e += blockDim.x) {
-    const int iw = iw0 + e / c, k = e % c;
+  for (int e = tid; e < nw * maxw; e += 256) {
+    const int il = e / maxw, j = e - il * maxw, iw = iw0 + il;
     int lo, hi;
     bil_wsum_range(iw, sw, wi, wo, lo, hi);
-    float acc = 0.f;
-    for (int ow = lo; ow <= hi; ++ow) {
-      const float wt = bil_weight(ow, iw, sw, wi);
-      if (wt != 0.f) acc = fmaf(wt, to_f(sg[(ow - olo) * c + k]), acc);
-    }
-    tmp[(row * wi + iw) * c + k] = acc;
+    wt[e] = lo + j <= hi ? bil_weight(lo + j, iw, sw, wi) : 0.f;
+    if (j == 0) wlo[il] = lo - olo;
   }
+  __syncthreads();
+  for (int e = tid; e < nw * c; e += 256) {  // (input column, class) items, classes inner
+    const int il = e / c, k = e - il * c;
+    const float* w = wt + il * maxw;
+    const T* s = sgt + wlo[il] * c + k;
+    float acc = 0.f;
+    for (int j = 0; j < maxw; ++j) {
+      const float wv = w[j];
+      if (wv != 0.f) acc = fmaf(wv, to_f(s[j * c]), acc);
+    }
+    tmp[(row * wi + iw0) * c + e] = acc;
+  }
+}
+// columns of the low-res rows one forward tile stages (taps monotone in ow)
+static int upsm_fwd_cols(int wi, int wo, float sw) {
+  int cols = 0;
+  for (int ow0 = 0; ow0 < wo; ow0 += kUpsmPix) {
+    const int ow1 = std::min(wo, ow0 + kUpsmPix) - 1;
+    float src0 = sw * ((float)ow0 + 0.5f) - 0.5f, src1 = sw * ((float)ow1 + 0.5f) - 0.5f;
+    int a = src0 < 0.f ? 0 : (int)src0, b = src1 < 0.f ? 0 : (int)src1;
+    a = std::min(a, wi - 1);
+    b = std::min(b, wi - 1);
+    b = b + (b < wi - 1 ? 1 : 0);
+    cols = std::max(cols, b - a + 1);
+  }
+  return cols + 2;  // margin: the device computes the tap columns with its own float rounding
 }
 extern "C" int rtsds_upsoftmax_fwd(const void* x, void* y, int n, int hi, int wi, int c, int ho, int wo, float scale_h,
                                    float scale_w, int y_ld, int dtype, void* stream) {
@@ -951,16 +1061,36 @@ extern "C" int rtsds_upsoftmax_fwd(const void* x, void* y, int n, int hi, int wi
   const int tiles = rt_cdiv(wo, kUpsmPix);
   const long blocks = (long)n * ho * tiles;
   if (blocks > INT_MAX) return RTSDS_ERR_UNSUPPORTED;
-  DISPATCH_T(dtype, hipLaunchKernelGGL(upsoftmax_fwd_kernel<T>, dim3((unsigned)blocks), dim3(256), kUpsmPix * y_ld * sizeof(T),
-                                       (hipStream_t)stream, (const T*)x, (T*)y, hi, wi, c, ho, wo, scale_h, scale_w, y_ld, tiles));
+  const size_t taps = (size_t)2 * upsm_fwd_cols(wi, wo, scale_w) * c * sizeof(float);
+  const bool staged = taps <= (size_t)kUpsmLds;
+  const size_t outb = (size_t)kUpsmPix * y_ld * (dtype == RTSDS_BF16 ? 2 : 4);
+  const size_t lds = (staged ? taps + 16 : 0) + outb;
+  hipStream_t st = (hipStream_t)stream;
+  DISPATCH_T(dtype, {
+    if (staged && c == 19)
+      hipLaunchKernelGGL((upsoftmax_fwd_kernel<T, true, 19>), dim3((unsigned)blocks), dim3(256), lds, st, (const T*)x, (T*)y, hi,
+                         wi, c, ho, wo, scale_h, scale_w, y_ld, tiles);
+    else if (staged)
+      hipLaunchKernelGGL((upsoftmax_fwd_kernel<T, true, 0>), dim3((unsigned)blocks), dim3(256), lds, st, (const T*)x, (T*)y, hi,
+                         wi, c, ho, wo, scale_h, scale_w, y_ld, tiles);
+    else
+      hipLaunchKernelGGL((upsoftmax_fwd_kernel<T, false, 0>), dim3((unsigned)blocks), dim3(256), lds, st, (const T*)x, (T*)y, hi,
+                         wi, c, ho, wo, scale_h, scale_w, y_ld, tiles);
+  });
   RET_LAUNCH();
 }
 extern "C" size_t rtsds_upsoftmax_bwd_workspace(int n, int hi, int wi, int c, int ho, int wo) {
   return rtsds_bilinear_bwd_workspace(n, hi, wi, c, ho, wo);
 }
-// widest tile (<= 64 input columns) whose staged dy / p segment fits kUpsmLds; cap = its
-// exact largest segment
-static bool upsm_tiling(int wi, int wo, int c, float sw, size_t esz, int& tw, int& cap) {
+// widest tile (<= 64 input columns) whose staged segment + weight table fit kUpsmLds; cap =
+// its exact largest segment, maxw = the most output columns any input column reads
+static bool upsm_tiling(int wi, int wo, int c, float sw, size_t esz, int& tw, int& cap, int& maxw) {
+  maxw = 0;
+  for (int iw = 0; iw < wi; ++iw) {
+    int lo, hi;
+    upsm_span(iw, iw, sw, wi, wo, lo, hi);
+    maxw = std::max(maxw, hi - lo + 1);
+  }
   for (tw = 64; tw >= 1; tw /= 2) {
     cap = 0;
     for (int iw0 = 0; iw0 < wi; iw0 += tw) {
@@ -968,7 +1098,7 @@ static bool upsm_tiling(int wi, int wo, int c, float sw, size_t esz, int& tw, in
       upsm_span(iw0, std::min(wi, iw0 + tw) - 1, sw, wi, wo, lo, hi);
       cap = std::max(cap, hi - lo + 1);
     }
-    if ((size_t)cap * c * 2 * esz <= (size_t)kUpsmLds) return true;
+    if ((size_t)cap * c * esz + (size_t)tw * (maxw + 1) * 4 <= (size_t)kUpsmLds) return true;
   }
   return false;
 }
@@ -981,13 +1111,18 @@ extern "C" int rtsds_upsoftmax_bwd(const void* dy, int dy_ld, const void* y, int
   hipStream_t st = (hipStream_t)stream;
   float* tmp = (float*)ws;
   DISPATCH_T(dtype, {
-    int tw, cap;
-    if (!upsm_tiling(wi, wo, c, scale_w, sizeof(T), tw, cap)) return RTSDS_ERR_UNSUPPORTED;
+    int tw, cap, maxw;
+    if (!upsm_tiling(wi, wo, c, scale_w, sizeof(T), tw, cap, maxw)) return RTSDS_ERR_UNSUPPORTED;
     const int tiles = rt_cdiv(wi, tw);
     const long blocks = (long)n * ho * tiles;
     if (blocks > INT_MAX) return RTSDS_ERR_UNSUPPORTED;
-    hipLaunchKernelGGL(upsoftmax_bwd_w_kernel<T>, dim3((unsigned)blocks), dim3(256), (size_t)cap * c * 2 * sizeof(T), st,
-                       (const T*)dy, dy_ld, (const T*)y, y_ld, tmp, wi, c, wo, scale_w, tw, tiles, cap);
+    const size_t lds = (size_t)tw * (maxw + 1) * 4 + (size_t)cap * c * sizeof(T);
+    if (c == 19)
+      hipLaunchKernelGGL((upsoftmax_bwd_w_kernel<T, 19>), dim3((unsigned)blocks), dim3(256), lds, st, (const T*)dy, dy_ld,
+                         (const T*)y, y_ld, tmp, wi, c, wo, scale_w, tw, tiles, cap, maxw);
+    else
+      hipLaunchKernelGGL((upsoftmax_bwd_w_kernel<T, 0>), dim3((unsigned)blocks), dim3(256), lds, st, (const T*)dy, dy_ld,
+                         (const T*)y, y_ld, tmp, wi, c, wo, scale_w, tw, tiles, cap, maxw);
     hipLaunchKernelGGL(bilinear_bwd_h_kernel<T>, dim3(ew_blocks(total)), dim3(256), 0, st, (const float*)tmp, (T*)dx, n, hi,
                        wi, c, ho, scale_h);
   });

@@ -686,7 +686,7 @@ def test_conv_bn_stats_epilogue(shape):
 
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("geo", [((2, 19, 16, 32), (128, 256)), ((1, 19, 13, 17), (97, 129))])
+@pytest.mark.parametrize("geo", [((2, 19, 16, 32), (128, 256)), ((1, 19, 13, 17), (97, 129)), ((2, 7, 9, 40), (64, 96))])
 def test_upsample_softmax_fused(dt, geo):
     """functional.upsample_softmax (rtsds_upsoftmax_fwd / _bwd): forward and input gradient vs
     torch fp64 (interpolate bilinear + softmax), bit-identical to the unfused HIP chain
