@@ -76,6 +76,13 @@ int rtsds_conv2d_fwd_bn(const rtsds_conv_desc* d, const void* x, const void* w, 
 size_t rtsds_conv2d_dgrad_workspace(const rtsds_conv_desc* d);
 int rtsds_conv2d_dgrad(const rtsds_conv_desc* d, const void* dy, const void* w, void* dx,
                        int accumulate, void* ws, size_t ws_bytes, void* stream);
+/* dx = conv_transpose(dy, w) * act'(x_act): the data gradient of this conv followed by the
+ * backward of the ReLU (act 1) / LeakyReLU(0.2) (act 2) that produced its input x_act (NHWC
+ * [n][h][w][c], the activation's output) -- the discriminator's conv -> LeakyReLU -> conv
+ * chains (model.py:54-58,69-70), applied in the GEMM epilogue (else as a second pass).
+ * Values equal rtsds_conv2d_dgrad followed by rtsds_act_bwd.  Same workspace as dgrad.   */
+int rtsds_conv2d_dgrad_act(const rtsds_conv_desc* d, const void* dy, const void* w, void* dx, const void* x_act,
+                           int act, void* ws, size_t ws_bytes, void* stream);
 /* dw (fp32 [k][kh][kw][c]) = sum_pixels dy (x) patch(x); dbias (fp32 [k], may be NULL) =
  * sum_pixels dy.  accumulate != 0 adds into dw / dbias instead of overwriting (gradients go
  * straight into the optimizer's flat gradient arena, replacing autograd's AccumulateGrad).  */

@@ -38,6 +38,7 @@ SIGNATURES = {
     "rtsds_conv2d_fwd_bn": (c_int, [ctypes.POINTER(ConvDesc), P, P, P, P, P, P, c_int, P, c_size_t, P]),
     "rtsds_conv2d_dgrad_workspace": (c_size_t, [ctypes.POINTER(ConvDesc)]),
     "rtsds_conv2d_dgrad": (c_int, [ctypes.POINTER(ConvDesc), P, P, P, c_int, P, c_size_t, P]),
+    "rtsds_conv2d_dgrad_act": (c_int, [ctypes.POINTER(ConvDesc), P, P, P, P, c_int, P, c_size_t, P]),
     "rtsds_conv2d_wgrad_workspace": (c_size_t, [ctypes.POINTER(ConvDesc)]),
     "rtsds_conv2d_wgrad": (c_int, [ctypes.POINTER(ConvDesc), P, P, P, P, c_int, P, c_size_t, P]),
     "rtsds_bn_workspace": (c_size_t, [c_long, c_int]),

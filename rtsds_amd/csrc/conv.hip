@@ -37,6 +37,10 @@ struct ConvArgs {
   FastDiv f_tkw;
   int act;
   int accum;          // FWD/DGRAD: y += result
+  // DGRAD: dx = result * act'(mask) -- the backward of the activation (ReLU / LeakyReLU) that
+  // produced this conv's input (mask = that input, NHWC like dx), fused into the epilogue
+  const void* mask;
+  int mask_act;
   float* stats;       // FWD: per-M-tile BatchNorm partials [N][mtile][count, mean, M2, 0] (or null)
   long split_stride;  // elements between WGRAD split slabs (and DGRAD split-K slabs)
   float* slab;        // DGRAD split-K: fp32 partials [split][M][N] instead of the bf16 epilogue
@@ -903,6 +907,10 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(const ConvArgs P0) {
       return gm;
     };
     const bool has_res = MODE == MODE_FWD && P.res != nullptr;
+    const bool has_mask = MODE == MODE_DGRAD && P.mask != nullptr;
+    auto mask_f = [&](float g, float xv) {  // act_bwd_kernel's expression
+      return xv > 0.f ? g : (P.mask_act == RTSDS_ACT_LEAKY ? 0.2f * g : 0.f);
+    };
     bool stored = false;
     if constexpr (sizeof(T) == 2) {
       if (P.N % V == 0) {
@@ -914,7 +922,7 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(const ConvArgs P0) {
         constexpr int CP = BN + 8, CPR = BN / V;
         static_assert(BM * CP <= NBUF * (A_EL + B_EL), "epilogue staging fits the operand LDS");
         T* cs = smem;
-        const bool post = has_res || P.accum;
+        const bool post = has_res || P.accum || has_mask;
         __syncthreads();
 #pragma unroll
         for (int j = 0; j < FN; ++j) {
@@ -947,6 +955,11 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(const ConvArgs P0) {
 #pragma unroll
                 for (int q = 0; q < V; ++q) f[q] += to_f(r[q]);
               }
+              if (has_mask) {  // (accumulate is refused together with a mask)
+                const V16 r = *(const V16*)((const T*)P.mask + o);
+#pragma unroll
+                for (int q = 0; q < V; ++q) f[q] = mask_f(f[q], to_f(r[q]));
+              }
               if (P.accum) {
                 const V16 r = *(const V16*)(out + o);
 #pragma unroll
@@ -976,6 +989,7 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(const ConvArgs P0) {
             if (gm >= P.M) continue;
             const long orow = out_row(gm);
             float v = fmaf(acc[i][j][e], sv, bv);
+            if (has_mask) v = mask_f(to_f(from_f<T>(v)), to_f(((const T*)P.mask)[orow * P.N + gn]));
             if (has_res) v += to_f(((const T*)P.res)[orow * P.N + gn]);
             if (P.accum) v += to_f(out[orow * P.N + gn]);
             out[orow * P.N + gn] = from_f<T>(act_f(v));
@@ -1712,8 +1726,27 @@ static void phase_taps(int a, int pad, int dil, int ksz, int size, int& off, int
   else { r0 = 0; rstep = 1; tk = a == 0 ? ksz : 0; }
 }
 
+// mask: see ConvArgs::mask.  Paths whose epilogue does not apply it (pooled, narrow 1x1, halo,
+// split-K) report false and the caller masks dx in place afterwards.
+static int dgrad_impl(const rtsds_conv_desc* d0, const void* dy, const void* w, void* dx, int accumulate, const void* mask,
+                      int mask_act, bool& masked, void* ws, size_t ws_bytes, void* stream);
 extern "C" int rtsds_conv2d_dgrad(const rtsds_conv_desc* d0, const void* dy, const void* w, void* dx,
                                   int accumulate, void* ws, size_t ws_bytes, void* stream) {
+  bool masked = false;
+  return dgrad_impl(d0, dy, w, dx, accumulate, nullptr, 0, masked, ws, ws_bytes, stream);
+}
+extern "C" int rtsds_act_bwd(const void* dy, const void* y, void* dx, long n, int act, float alpha, int dtype, void* stream);
+extern "C" int rtsds_conv2d_dgrad_act(const rtsds_conv_desc* d0, const void* dy, const void* w, void* dx, const void* x_act,
+                                      int act, void* ws, size_t ws_bytes, void* stream) {
+  if (!x_act || (act != RTSDS_ACT_RELU && act != RTSDS_ACT_LEAKY)) return RTSDS_ERR_UNSUPPORTED;
+  bool masked = false;
+  const int e = dgrad_impl(d0, dy, w, dx, 0, x_act, act, masked, ws, ws_bytes, stream);
+  if (e || masked) return e;
+  return rtsds_act_bwd(dx, x_act, dx, (long)d0->n * d0->h * d0->w * d0->c, act, 1.f, d0->dtype, stream);
+}
+static int dgrad_impl(const rtsds_conv_desc* d0, const void* dy, const void* w, void* dx, int accumulate, const void* mask,
+                      int mask_act, bool& masked, void* ws, size_t ws_bytes, void* stream) {
+  masked = false;
   int e = check_desc(d0);
   if (e) return e;
   if (d0->sh > 2 || d0->sw > 2) return RTSDS_ERR_UNSUPPORTED;
@@ -1751,6 +1784,9 @@ extern "C" int rtsds_conv2d_dgrad(const rtsds_conv_desc* d0, const void* dy, con
     ConvArgs p = make_args(&d);
     p.a = dy; p.b = wt; p.bias = nullptr; p.out = dx; p.act = 0;
     p.accum = accumulate ? 1 : 0;
+    p.mask = mask;
+    p.mask_act = mask_act;
+    masked = mask != nullptr;
     p.psh = 2;
     p.N = d.c;
     RepackPhases rp = {};
@@ -1802,6 +1838,8 @@ extern "C" int rtsds_conv2d_dgrad(const rtsds_conv_desc* d0, const void* dy, con
     ConvArgs p = make_args(&d);
     p.a = dy; p.b = wt; p.bias = nullptr; p.out = dx; p.act = 0;
     p.accum = accumulate ? 1 : 0;
+    p.mask = mask;
+    p.mask_act = mask_act;
     p.M = d.n * d.h * d.w;
     p.N = d.c;
     p.K = d.kh * d.kw * kp;
@@ -1814,12 +1852,16 @@ extern "C" int rtsds_conv2d_dgrad(const rtsds_conv_desc* d0, const void* dy, con
       p.split_stride = (long)p.M * p.N;
       p.tiles_per_split = sk.tps;
       p.accum = 0;
+      p.mask = nullptr;  // the split reduce writes dx: masked afterwards by the caller
       launch_al<bf16, MODE_DGRAD, 128, 128, 64, 2, 2>(p, kp, st, sk.splits);
       const long nv8 = (long)p.M * p.N / 8;
       hipLaunchKernelGGL(dgrad_split_reduce_kernel, dim3((int)std::min<long>(8192, (nv8 + 255) / 256)), dim3(256), 0, st,
                          (const float*)p.slab, (bf16*)dx, nv8, p.split_stride, sk.splits, accumulate ? 1 : 0);
-    } else if (d.dtype == RTSDS_BF16) dispatch_align<bf16, MODE_DGRAD>(p, kp, st);
-    else dispatch_align<float, MODE_DGRAD>(p, kp, st);
+    } else {
+      masked = mask != nullptr;
+      if (d.dtype == RTSDS_BF16) dispatch_align<bf16, MODE_DGRAD>(p, kp, st);
+      else dispatch_align<float, MODE_DGRAD>(p, kp, st);
+    }
   }
   return hipGetLastError() == hipSuccess ? RTSDS_OK : RTSDS_ERR_LAUNCH;
 }

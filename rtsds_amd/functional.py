@@ -135,7 +135,12 @@ class ConvFn(torch.autograd.Function):
     parameter itself or its bf16 shadow); gradients are returned for ``weight``."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, wq, stride, padding, dilation, act, stats, join=None):
+    def forward(ctx, x, weight, bias, wq, stride, padding, dilation, act, stats, join=None, fold=(0, False)):
+        """``fold = (in_act, out_folded)``: ``in_act`` -- x is the output of a ReLU / LeakyReLU
+        whose backward this conv's data gradient applies in its epilogue
+        (rtsds_conv2d_dgrad_act); ``out_folded`` -- the single consumer of y does that for this
+        conv's own ``act``, so the backward takes dy as the pre-activation gradient.  Set only
+        by modules whose intermediate activations have exactly one reader (discriminators)."""
         require_hip(x, weight)
         padded = is_padded_input(x)
         if not padded:
@@ -149,6 +154,9 @@ class ConvFn(torch.autograd.Function):
             lib.rtsds_conv2d_fwd(ctypes.byref(d), _P(x), _P(wq), _P(bias), _P(y), act | flag, _P(stats), _P(ws),
                                         ws.numel(), stream())
         ctx.xflag = flag
+        ctx.in_act, ctx.out_folded = fold
+        if ctx.in_act and join is not None:
+            raise RuntimeError("rtsds_amd: a conv whose input gradient is masked cannot join other readers")
         ctx.d, ctx.act, ctx.has_bias = d, act, bias is not None
         ctx.params = (weight, bias)
         ctx.join = join
@@ -162,11 +170,11 @@ class ConvFn(torch.autograd.Function):
         dy = nhwc(dy)
         if dy.dtype != x.dtype:
             dy = cast(dy, x.dtype)
-        if ctx.act:
+        if ctx.act and not ctx.out_folded:
             g = torch.empty_like(dy)
             lib.rtsds_act_bwd(_P(dy), _P(y), _P(g), dy.numel(), ctx.act, 1.0, dcode(dy), stream())
         else:
-            g = dy
+            g = dy  # (out_folded: the consumer's dgrad already applied act')
         dx = dw = db = None
         # weight gradient into the optimizer's arena: on the side stream, overlapping the
         # data-gradient chain (runtime.side_fork); forked before the dgrad launch
@@ -186,8 +194,12 @@ class ConvFn(torch.autograd.Function):
             dx = join.buf if acc else empty_nhwc(d.n, d.c, d.h, d.w, x.dtype, x.device)
             ws = workspace(lib.rtsds_conv2d_dgrad_workspace(ctypes.byref(d)), x.device)
             with _Timed(d, "dgrad"):
-                lib.rtsds_conv2d_dgrad(ctypes.byref(d), _P(g), _P(wq), _P(dx), 1 if acc else 0, _P(ws),
-                                       ws.numel(), stream())
+                if ctx.in_act:
+                    lib.rtsds_conv2d_dgrad_act(ctypes.byref(d), _P(g), _P(wq), _P(dx), _P(x), ctx.in_act, _P(ws),
+                                               ws.numel(), stream())
+                else:
+                    lib.rtsds_conv2d_dgrad(ctypes.byref(d), _P(g), _P(wq), _P(dx), 1 if acc else 0, _P(ws),
+                                           ws.numel(), stream())
             if join is not None:
                 dx = join.put(dx)
         if (ctx.needs_input_grad[1] or ctx.needs_input_grad[2]) and not wg_side:
@@ -209,11 +221,11 @@ class ConvFn(torch.autograd.Function):
                                                   ws.numel(), stream())
                 if not ctx.needs_input_grad[1]:
                     dw = None
-        return dx, dw, db, None, None, None, None, None, None, None
+        return dx, dw, db, None, None, None, None, None, None, None, None
 
 
 def conv2d(x, weight, bias, wq, stride=(1, 1), padding=(0, 0), dilation=(1, 1), act=0, bn_stats=False,
-           join=None):
+           join=None, in_act=0, fold_out=False):
     """bn_stats=True: the conv epilogue also emits the following BatchNorm's per-tile batch
     statistics, attached to the output as ``_rt_bn_stats`` and consumed by batch_norm().
     ``join``: GradJoin shared with the other readers of ``x``."""
@@ -224,7 +236,8 @@ def conv2d(x, weight, bias, wq, stride=(1, 1), padding=(0, 0), dilation=(1, 1), 
         d = _conv_desc(x, k, kh, kw, stride, padding, dilation)
         nrb = lib.rtsds_conv2d_fwd_stats_tiles(ctypes.byref(d))
         stats = torch.empty(nrb * k * 4, dtype=torch.float32, device=x.device)  # [k][nrb][4]
-    y = ConvFn.apply(x, weight, bias, wq, tuple(stride), tuple(padding), tuple(dilation), act, stats, join)
+    y = ConvFn.apply(x, weight, bias, wq, tuple(stride), tuple(padding), tuple(dilation), act, stats, join,
+                     (in_act, bool(fold_out and act in (1, 2))))
     if stats is not None:
         y._rt_bn_stats = (stats, nrb)
     return y

@@ -1,8 +1,9 @@
 """Output-space discriminators on the MI355X kernels -- drop-in for the reference's
 models/domain_shift/adversarial/model.py.
 
-k4 s2 p1 convolutions with bias; the LeakyReLU(0.2) is fused into each conv's epilogue and
-its backward recovers the mask from the output sign.  The head is conv -> global average
+k4 s2 p1 convolutions with bias; the LeakyReLU(0.2) is fused into each conv's epilogue, and
+its backward into the next conv's data-gradient epilogue (mask from the sign of that conv's
+input: rtsds_conv2d_dgrad_act), so the activation gradient is never a separate pass.  The head is conv -> global average
 pool -> [N, 1, 1, 1] logit, as in the reference.
 """
 import torch
@@ -65,11 +66,16 @@ class DomainDiscriminator(nn.Module):
         self.leaky_relu = LeakyReLU(0.2)
         self.avgpool = AdaptiveAvgPool2d((1, 1))
 
+    fold_act = True  # LeakyReLU backward of conv_i applied by conv_{i+1}'s data gradient
+
     def forward(self, x):
         x = _nhwc_input(x)
+        f = self.fold_act
+        prev = None
         for conv in (self.conv1, self.conv2, self.conv3, self.conv4):
-            x = conv(x, act="leaky")
-        x = self.avgpool(self.classifier(x))
+            x = conv(x, act="leaky", in_act=prev, fold_out=f)
+            prev = "leaky" if f else None
+        x = self.avgpool(self.classifier(x, in_act=prev))
         if self.with_grl:
             x = F.GradReverseFn.apply(x, self.lambda_)
         return x
@@ -87,6 +93,10 @@ class TinyDomainDiscriminator(nn.Module):
         self.leaky_relu = LeakyReLU(0.2)
         self.avgpool = AdaptiveAvgPool2d((1, 1))
 
+    fold_act = True  # conv1's LeakyReLU backward applied by the classifier's data gradient
+
     def forward(self, x):
         x = _nhwc_input(x)
-        return self.avgpool(self.classifier(self.conv1(x, act="leaky")))
+        f = self.fold_act
+        h = self.conv1(x, act="leaky", fold_out=f)
+        return self.avgpool(self.classifier(h, in_act="leaky" if f else None))

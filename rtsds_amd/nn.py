@@ -48,13 +48,14 @@ class Conv2d(nn.Conv2d):
             self.weight.data = self.weight.data.contiguous(memory_format=CL)
         return out
 
-    def forward(self, x, act=None, bn_stats=False, join=None):
+    def forward(self, x, act=None, bn_stats=False, join=None, in_act=None, fold_out=False):
         """``bn_stats``: also emit the batch statistics of a directly following train-mode
         BatchNorm from the conv epilogue (see functional.conv2d).  ``join``: a
-        functional.GradJoin shared with the other readers of ``x``."""
+        functional.GradJoin shared with the other readers of ``x``.  ``in_act`` / ``fold_out``:
+        activation-backward folding between chained convs (functional.ConvFn)."""
         wq = _shadow(self.weight, x.dtype)
         return F.conv2d(x, self.weight, self.bias, wq, self.stride, self.padding, self.dilation,
-                        ACT[act], bn_stats, join)
+                        ACT[act], bn_stats, join, ACT[in_act], fold_out)
 
 
 class BatchNorm2d(nn.BatchNorm2d):

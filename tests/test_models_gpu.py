@@ -622,3 +622,31 @@ def test_da_step_fused_discriminator_input_equals_unfused(dt):
         assert n0 == n1 and l0 == l1, (n0, l0, l1)
         for k in s0:
             assert torch.equal(s0[k], s1[k]), (n0, k)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("cls", [TinyDomainDiscriminator, DomainDiscriminator])
+def test_discriminator_activation_fold_bit_identical(dt, cls):
+    """fold_act (each LeakyReLU backward applied by the next conv's data-gradient epilogue,
+    rtsds_conv2d_dgrad_act) gives bit-identical outputs, input gradients and parameter
+    gradients to the unfolded chain (conv dgrad -> rtsds_act_bwd)."""
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(2, 19, 64, 128, generator=g)
+    gy = torch.randn(2, 1, 1, 1, generator=g)
+    res = []
+    with rtsds_amd.precision(dt):
+        for fold in (False, True):
+            torch.manual_seed(9)
+            d = cls(19).to(DEV).train()
+            d.fold_act = fold
+            xi = x.to(DEV).requires_grad_()
+            y = d(xi)
+            y.backward(gy.to(DEV))
+            torch.cuda.synchronize()
+            res.append((y.detach().float().cpu(), xi.grad.float().cpu(),
+                        {k: p.grad.detach().float().cpu().clone() for k, p in d.named_parameters()}))
+    (y0, gx0, p0), (y1, gx1, p1) = res
+    assert torch.equal(y0, y1)
+    assert torch.equal(gx0, gx1)
+    for k in p0:
+        assert torch.equal(p0[k], p1[k]), k
