@@ -1273,14 +1273,23 @@ static void launch(const ConvArgs& p, int splits, hipStream_t st) {
 }
 
 // Tile selection for FWD / DGRAD (occupancy-aware): the widest tile that still puts >= 256
-// workgroups on the 256 CUs.  bf16: 128x128 / 128x64 / 256x32 (19- and 1-channel outputs),
-// falling back to 64x64 / 128x32 for small-M layers (ResNet layer4, pooled vectors).
-static void pick_tile(long M, int N, bool b16, int& bm, int& bn) {
+// workgroups on the 256 CUs.  bf16: 128x128 (or 160x128, see below) / 128x64 / 256x32 (19- and
+// 1-channel outputs), falling back to 64x64 / 128x32 for small-M layers (ResNet layer4, pooled
+// vectors).
+static void pick_tile(long M, int N, bool b16, int& bm, int& bn, bool fwd = false) {
   auto blocks = [&](int a, int b) { return ((M + a - 1) / a) * (long)((N + b - 1) / b); };
   if (b16) {
     if (N <= 32) { bn = 32; bm = blocks(256, 32) >= 256 ? 256 : 128; }
     else if (N <= 64) { bn = 64; bm = blocks(128, 64) >= 256 ? 128 : 64; }
-    else if (blocks(128, 128) >= 512) { bm = 128; bn = 128; }
+    else if (blocks(128, 128) >= 512) {
+      // tail quantisation: 2 workgroups per CU = 512 slots per round.  A 160-row tile (still 2
+      // per CU in FWD: 113 VGPRs; the DGRAD instantiation needs 181 and would run 1 per CU)
+      // when it needs fewer row-weighted rounds -- DeepLab's M = 33,540 rows: 526 tiles of
+      // 128 (2 rounds, the second 3 % full) vs 420 of 160 (1 round)
+      bn = 128;
+      const long r128 = (blocks(128, 128) + 511) / 512, r160 = (blocks(160, 128) + 511) / 512;
+      bm = fwd && r160 * 160 < r128 * 128 ? 160 : 128;
+    }
     else if (blocks(128, 64) >= 384) { bm = 128; bn = 64; }
     else { bm = 64; bn = 64; }
   } else {
@@ -1311,12 +1320,13 @@ static void launch_al(const ConvArgs& p, int cr, hipStream_t st, int splits = 1)
 template <typename T, int MODE>
 static void dispatch_align(const ConvArgs& p, int cr, hipStream_t st) {
   int bm, bn;
-  pick_tile(p.M, p.N, sizeof(T) == 2, bm, bn);
+  pick_tile(p.M, p.N, sizeof(T) == 2, bm, bn, MODE == MODE_FWD);
   if constexpr (sizeof(T) == 2) {
     if (bn == 32 && bm == 256) launch_al<T, MODE, 256, 32, 32, 4, 1>(p, cr, st);
     else if (bn == 32) launch_al<T, MODE, 128, 32, 32, 4, 1>(p, cr, st);
     else if (bn == 64 && bm == 128) launch_al<T, MODE, 128, 64, 32, 2, 2>(p, cr, st);
     else if (bn == 64) launch_al<T, MODE, 64, 64, 64, 2, 2>(p, cr, st);
+    else if (MODE == MODE_FWD && bm == 160) launch_al<T, MODE_FWD, 160, 128, 64, 2, 2>(p, cr, st);
     else launch_al<T, MODE, 128, 128, 64, 2, 2>(p, cr, st);
   } else {
     if (bn == 32) launch_al<T, MODE, 128, 32, 16, 4, 1>(p, cr, st);
@@ -1524,7 +1534,7 @@ extern "C" int rtsds_conv2d_fwd_stats_tiles(const rtsds_conv_desc* d) {
   if (hconv_ok(d)) return hconv_tiles(d);
   int bm, bn;
   const long M = (long)d->n * d->ho * d->wo;
-  pick_tile(M, d->k, d->dtype == RTSDS_BF16, bm, bn);
+  pick_tile(M, d->k, d->dtype == RTSDS_BF16, bm, bn, true);
   return (int)((M + bm - 1) / bm);
 }
 
