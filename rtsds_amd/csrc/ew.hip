@@ -5,6 +5,7 @@
 #include "common.h"
 #include <algorithm>
 #include <climits>
+#include <cmath>
 
 static inline int ew_blocks(long work, int per_block = 256, int cap = 8192) {
   return (int)std::max<long>(1, std::min<long>(cap, (work + per_block - 1) / per_block));
@@ -765,6 +766,95 @@ __global__ void bilinear_bwd_h_kernel(const float* __restrict__ tmp, T* __restri
     dx[i] = from_f<T>(acc);
   }
 }
+// Table-driven variants of the two passes: the weights of one axis (per input index i: lo(i)
+// and w(lo + j -> i), zero past hi(i)) are tabulated once per block in LDS instead of being
+// re-derived (two bil_src evaluations) for every element and tap; same taps, same order, same
+// zero skipping, so the sums are bit-identical to the kernels above.
+static const int kBilTabLds = 48 * 1024;
+RT_DEV void bil_table_build(float* tab, int* tlo, int in, int out, float s, int maxw) {
+  for (int e = threadIdx.x; e < in * maxw; e += blockDim.x) {
+    const int i = e / maxw, j = e - i * maxw;
+    int lo, hi;
+    bil_wsum_range(i, s, in, out, lo, hi);
+    tab[e] = lo + j <= hi ? bil_weight(lo + j, i, s, in) : 0.f;
+    if (j == 0) tlo[i] = lo;
+  }
+  __syncthreads();
+}
+template <typename T>
+__global__ void bilinear_bwd_w_tab_kernel(const T* __restrict__ dy, float* __restrict__ tmp, int n, int wi, int c, int ho, int wo,
+                                          float sw, int dyld, int dyoff, int maxw, FastDiv f_c, FastDiv f_wi) {
+  extern __shared__ float tab[];
+  int* tlo = (int*)(tab + wi * maxw);
+  bil_table_build(tab, tlo, wi, wo, sw, maxw);
+  const long total = (long)n * ho * wi * c;  // < 2^31 (host)
+  GRID_STRIDE(i, total) {
+    const uint32_t q = fdiv((uint32_t)i, f_c), row = fdiv(q, f_wi);
+    const int ch = (int)((uint32_t)i - q * c), iw = (int)(q - row * wi);
+    const float* w = tab + iw * maxw;
+    const T* src = dy + ((long)row * wo + tlo[iw]) * dyld + dyoff + ch;
+    float acc = 0.f;
+    for (int j = 0; j < maxw; ++j) {
+      const float wt = w[j];
+      if (wt != 0.f) acc = fmaf(wt, to_f(src[(long)j * dyld]), acc);
+    }
+    tmp[i] = acc;
+  }
+}
+template <typename T>
+__global__ void bilinear_bwd_h_tab_kernel(const float* __restrict__ tmp, T* __restrict__ dx, int n, int hi, int wi, int c, int ho,
+                                          float sh, int maxh, FastDiv f_plane, FastDiv f_hi) {
+  extern __shared__ float tab[];
+  int* tlo = (int*)(tab + hi * maxh);
+  bil_table_build(tab, tlo, hi, ho, sh, maxh);
+  const uint32_t plane = (uint32_t)wi * c;
+  const long total = (long)n * hi * plane;  // < 2^31 (host)
+  GRID_STRIDE(i, total) {
+    const uint32_t q = fdiv((uint32_t)i, f_plane), img = fdiv(q, f_hi);
+    const uint32_t inner = (uint32_t)i - q * plane;
+    const int ih = (int)(q - img * hi);
+    const float* w = tab + ih * maxh;
+    const float* src = tmp + ((long)img * ho + tlo[ih]) * plane + inner;
+    float acc = 0.f;
+    for (int j = 0; j < maxh; ++j) {
+      const float wt = w[j];
+      if (wt != 0.f) acc = fmaf(wt, src[(long)j * plane], acc);
+    }
+    dx[i] = from_f<T>(acc);
+  }
+}
+// most outputs any input index of an axis receives from (bil_wsum_range, host float math)
+static int bil_maxw(int in, int out, float s) {
+  int m = 0;
+  for (int i = 0; i < in; ++i) {
+    int lo = (int)std::floor(((float)i - 0.5f) / s - 0.5f) - 1;
+    int hi = (int)std::ceil(((float)i + 1.5f) / s - 0.5f) + 1;
+    lo = std::max(lo, 0);
+    hi = std::min(hi, out - 1);
+    m = std::max(m, hi - lo + 1);
+  }
+  return m + 1;  // margin for the device's own rounding of the same range (zero entries)
+}
+static size_t bil_tab_bytes(int in, int maxw) { return ((size_t)in * maxw + in) * 4; }
+// launch both passes table-driven when the tables fit and the index math fits 32 bits, else the
+// per-element kernels; w pass reads dy with row pitch dyld at channel offset dyoff
+template <typename T>
+static void bilinear_bwd_launch(const T* dy, float* tmp, T* dx, int n, int hi, int wi, int c, int ho, int wo, float sh, float sw,
+                                int dyld, int dyoff, hipStream_t st) {
+  const long tw = (long)n * ho * wi * c, th = (long)n * hi * wi * c;
+  const int mw = bil_maxw(wi, wo, sw), mh = bil_maxw(hi, ho, sh);
+  const size_t bw = bil_tab_bytes(wi, mw), bh = bil_tab_bytes(hi, mh);
+  if (tw < (1L << 31) && bw <= (size_t)kBilTabLds)
+    hipLaunchKernelGGL(bilinear_bwd_w_tab_kernel<T>, dim3(ew_blocks(tw)), dim3(256), bw, st, dy, tmp, n, wi, c, ho, wo, sw, dyld,
+                       dyoff, mw, fastdiv_make(c), fastdiv_make(wi));
+  else
+    hipLaunchKernelGGL(bilinear_bwd_w_kernel<T>, dim3(ew_blocks(tw)), dim3(256), 0, st, dy, tmp, n, wi, c, ho, wo, sw, dyld, dyoff);
+  if (th < (1L << 31) && bh <= (size_t)kBilTabLds)
+    hipLaunchKernelGGL(bilinear_bwd_h_tab_kernel<T>, dim3(ew_blocks(th)), dim3(256), bh, st, (const float*)tmp, dx, n, hi, wi, c, ho,
+                       sh, mh, fastdiv_make((uint32_t)wi * c), fastdiv_make(hi));
+  else
+    hipLaunchKernelGGL(bilinear_bwd_h_kernel<T>, dim3(ew_blocks(th)), dim3(256), 0, st, (const float*)tmp, dx, n, hi, wi, c, ho, sh);
+}
 extern "C" int rtsds_bilinear_fwd(const void* x, void* y, int n, int hi, int wi, int c, int ho, int wo, float scale_h, float scale_w,
                                   int y_ld, int y_off, int dtype, void* stream) {
   const long total = (long)n * ho * wo * c;
@@ -795,10 +885,7 @@ extern "C" int rtsds_bilinear_bwd(const void* dy, void* dx, int n, int hi, int w
   if (dy_ld <= 0) dy_ld = c;
   hipStream_t st = (hipStream_t)stream;
   float* tmp = (float*)ws;
-  DISPATCH_T(dtype, {
-    hipLaunchKernelGGL(bilinear_bwd_w_kernel<T>, dim3(ew_blocks((long)n * ho * wi * c)), dim3(256), 0, st, (const T*)dy, tmp, n, wi, c, ho, wo, scale_w, dy_ld, dy_off);
-    hipLaunchKernelGGL(bilinear_bwd_h_kernel<T>, dim3(ew_blocks(total)), dim3(256), 0, st, (const float*)tmp, (T*)dx, n, hi, wi, c, ho, scale_h);
-  });
+  DISPATCH_T(dtype, bilinear_bwd_launch<T>((const T*)dy, tmp, (T*)dx, n, hi, wi, c, ho, wo, scale_h, scale_w, dy_ld, dy_off, st));
   RET_LAUNCH();
 }
 
@@ -1123,8 +1210,14 @@ extern "C" int rtsds_upsoftmax_bwd(const void* dy, int dy_ld, const void* y, int
     else
       hipLaunchKernelGGL((upsoftmax_bwd_w_kernel<T, 0>), dim3((unsigned)blocks), dim3(256), lds, st, (const T*)dy, dy_ld,
                          (const T*)y, y_ld, tmp, wi, c, wo, scale_w, tw, tiles, cap, maxw);
-    hipLaunchKernelGGL(bilinear_bwd_h_kernel<T>, dim3(ew_blocks(total)), dim3(256), 0, st, (const float*)tmp, (T*)dx, n, hi,
-                       wi, c, ho, scale_h);
+    const int mh = bil_maxw(hi, ho, scale_h);
+    const size_t bh = bil_tab_bytes(hi, mh);
+    if (total < (1L << 31) && bh <= (size_t)kBilTabLds)
+      hipLaunchKernelGGL(bilinear_bwd_h_tab_kernel<T>, dim3(ew_blocks(total)), dim3(256), bh, st, (const float*)tmp, (T*)dx, n,
+                         hi, wi, c, ho, scale_h, mh, fastdiv_make((uint32_t)wi * c), fastdiv_make(hi));
+    else
+      hipLaunchKernelGGL(bilinear_bwd_h_kernel<T>, dim3(ew_blocks(total)), dim3(256), 0, st, (const float*)tmp, (T*)dx, n, hi,
+                         wi, c, ho, scale_h);
   });
   RET_LAUNCH();
 }
