@@ -83,6 +83,18 @@ int rtsds_conv2d_dgrad(const rtsds_conv_desc* d, const void* dy, const void* w, 
  * Values equal rtsds_conv2d_dgrad followed by rtsds_act_bwd.  Same workspace as dgrad.   */
 int rtsds_conv2d_dgrad_act(const rtsds_conv_desc* d, const void* dy, const void* w, void* dx, const void* x_act,
                            int act, void* ws, size_t ws_bytes, void* stream);
+/* dx = conv_transpose(dy, w), plus -- from the stored dx values -- the backward statistics of
+ * the train-mode BatchNorm (+ ReLU / LeakyReLU, act) whose output is this conv's input
+ * (ResNet BasicBlock bn1 -> conv2, Bottleneck bn1 -> conv2, bn2 -> conv3): per M tile t and
+ * channel ch, part[(ch * tiles + t) * 2 + {0, 1}] = (sum g, sum g (bn_x - mean)),
+ * g = dx * act'(bn_x * gamma * invstd + beta - mean * gamma * invstd) -- what rtsds_bn_bwd's
+ * first pass computes, handed to rtsds_bn_bwd_part (the BatchNorm backward then skips it).
+ * tiles = rtsds_conv2d_dgrad_bnstats_tiles(d); 0 = route not available (bf16, stride 1 and
+ * the plain GEMM route only): call rtsds_conv2d_dgrad instead.                             */
+int rtsds_conv2d_dgrad_bnstats_tiles(const rtsds_conv_desc* d);
+int rtsds_conv2d_dgrad_bnstats(const rtsds_conv_desc* d, const void* dy, const void* w, void* dx, const void* bn_x,
+                               const float* gamma, const float* beta, const float* save_mean, const float* save_invstd,
+                               int act, float* part, void* ws, size_t ws_bytes, void* stream);
 /* dw (fp32 [k][kh][kw][c]) = sum_pixels dy (x) patch(x); dbias (fp32 [k], may be NULL) =
  * sum_pixels dy.  accumulate != 0 adds into dw / dbias instead of overwriting (gradients go
  * straight into the optimizer's flat gradient arena, replacing autograd's AccumulateGrad).  */
@@ -123,6 +135,12 @@ int rtsds_bn_bwd(const void* dy, const void* x, const void* y, void* dx, void* d
                  float* dgamma, float* dbeta, long rows, int c, const float* gamma,
                  const float* beta, const float* save_mean, const float* save_invstd, int training, int act,
                  int accumulate_params, int dtype, void* ws, size_t ws_bytes, void* stream);
+/* rtsds_bn_bwd without its statistics pass: part / nrb = the channel-major (sum g,
+ * sum g (x - mean)) partials of rtsds_conv2d_dgrad_bnstats (bf16, c % 8 == 0, no residual).  */
+int rtsds_bn_bwd_part(const void* dy, const void* x, void* dx, float* dgamma, float* dbeta, long rows, int c,
+                      const float* gamma, const float* beta, const float* save_mean, const float* save_invstd,
+                      int training, int act, int accumulate_params, const float* part, int nrb, int dtype, void* ws,
+                      size_t ws_bytes, void* stream);
 
 /* BatchNorm2d + ReLU + MaxPool2d(3, 2, p in {0,1}) fused -- the ResNet stem bn1 -> relu ->
  * maxpool (build_contextpath.py:15-18 via torchvision resnet.py; deeplabv2.py:106-110, ceil

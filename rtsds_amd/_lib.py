@@ -39,12 +39,16 @@ SIGNATURES = {
     "rtsds_conv2d_dgrad_workspace": (c_size_t, [ctypes.POINTER(ConvDesc)]),
     "rtsds_conv2d_dgrad": (c_int, [ctypes.POINTER(ConvDesc), P, P, P, c_int, P, c_size_t, P]),
     "rtsds_conv2d_dgrad_act": (c_int, [ctypes.POINTER(ConvDesc), P, P, P, P, c_int, P, c_size_t, P]),
+    "rtsds_conv2d_dgrad_bnstats_tiles": (c_int, [ctypes.POINTER(ConvDesc)]),
+    "rtsds_conv2d_dgrad_bnstats": (c_int, [ctypes.POINTER(ConvDesc), P, P, P, P, P, P, P, P, c_int, P, P, c_size_t, P]),
     "rtsds_conv2d_wgrad_workspace": (c_size_t, [ctypes.POINTER(ConvDesc)]),
     "rtsds_conv2d_wgrad": (c_int, [ctypes.POINTER(ConvDesc), P, P, P, P, c_int, P, c_size_t, P]),
     "rtsds_bn_workspace": (c_size_t, [c_long, c_int]),
     "rtsds_bn_fwd": (c_int, [P, P, P, c_long, c_int, P, P, P, P, P, P, P, c_float, c_float, c_int,
                              c_int, P, c_int, c_int, P, c_size_t, P]),
     "rtsds_bn_fold": (c_int, [P, P, P, P, P, c_float, c_int, P, P, P]),
+    "rtsds_bn_bwd_part": (c_int, [P, P, P, P, P, c_long, c_int, P, P, P, P, c_int, c_int, c_int, P, c_int, c_int, P,
+                                  c_size_t, P]),
     "rtsds_bn_bwd": (c_int, [P, P, P, P, P, P, P, c_long, c_int, P, P, P, P, c_int, c_int, c_int, c_int,
                              P, c_size_t, P]),
     "rtsds_bn_relu_maxpool_fwd": (c_int, [P, P, P] + [c_int] * 7 + [P, P, P, P, P, P, P, c_float, c_float, c_int, P,

@@ -636,15 +636,18 @@ extern "C" int rtsds_bn_fwd(const void* x, const void* res, void* y, long rows, 
 template <typename T, int VEC, class GS>
 static void bn_bwd_launch(const GS& gs, const void* x, const void* y, void* dx, void* dres, float* dgamma, float* dbeta,
                           long rows, int c, const float* gamma, const float* beta, const float* smean, const float* sinv, int training,
-                          int act, int accumulate, const BnWs& w, hipStream_t st) {
+                          int act, int accumulate, const BnWs& w, hipStream_t st, const float* pre = nullptr, int pre_nrb = 0) {
   int rb = bn_rb(rows, c, VEC);
-  float* part = w.part;
-  if (y && act)
+  const float* part = w.part;
+  if (pre) {  // statistics already produced by the consumer conv's data-gradient epilogue
+    part = pre;
+    rb = pre_nrb;
+  } else if (y && act)
     hipLaunchKernelGGL((bn_bwd_stats_kernel<T, VEC, true, GS>), dim3(rb, rt_cdiv(c, 256 * VEC)), dim3(256), 0, st, gs, (const T*)x,
-                       (const T*)y, gamma, beta, smean, sinv, part, rows, c, act);
+                       (const T*)y, gamma, beta, smean, sinv, w.part, rows, c, act);
   else
     hipLaunchKernelGGL((bn_bwd_stats_kernel<T, VEC, false, GS>), dim3(rb, rt_cdiv(c, 256 * VEC)), dim3(256), 0, st, gs, (const T*)x,
-                       (const T*)y, gamma, beta, smean, sinv, part, rows, c, act);
+                       (const T*)y, gamma, beta, smean, sinv, w.part, rows, c, act);
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(c), dim3(256), 0, st, part, rb, c, rows, gamma, beta, smean, sinv,
                      dgamma, dbeta, w.coef, training, accumulate);
   if (dx || dres) {
@@ -655,10 +658,23 @@ static void bn_bwd_launch(const GS& gs, const void* x, const void* y, void* dx, 
 template <typename T, int VEC>
 static void bn_bwd_launch(const void* dy, const void* x, const void* y, void* dx, void* dres, float* dgamma, float* dbeta,
                           long rows, int c, const float* gamma, const float* beta, const float* smean, const float* sinv, int training,
-                          int act, int accumulate, const BnWs& w, hipStream_t st) {
+                          int act, int accumulate, const BnWs& w, hipStream_t st, const float* pre = nullptr, int pre_nrb = 0) {
   const GradDirect<T> gs{(const T*)dy, c};
   bn_bwd_launch<T, VEC, GradDirect<T>>(gs, x, y, dx, dres, dgamma, dbeta, rows, c, gamma, beta, smean, sinv, training, act,
-                                       accumulate, w, st);
+                                       accumulate, w, st, pre, pre_nrb);
+}
+
+extern "C" int rtsds_bn_bwd_part(const void* dy, const void* x, void* dx, float* dgamma, float* dbeta, long rows, int c,
+                                 const float* gamma, const float* beta, const float* save_mean, const float* save_invstd,
+                                 int training, int act, int accumulate_params, const float* part, int nrb, int dtype, void* ws,
+                                 size_t ws_bytes, void* stream) {
+  if (rows <= 0 || c <= 0 || nrb <= 0 || !part) return RTSDS_ERR_SHAPE;
+  if (ws_bytes < rtsds_bn_workspace(rows, c)) return RTSDS_ERR_WORKSPACE;
+  if (dtype != RTSDS_BF16 || c % 8 != 0) return RTSDS_ERR_UNSUPPORTED;
+  if (!(act == RTSDS_ACT_NONE || act == RTSDS_ACT_RELU || act == RTSDS_ACT_LEAKY)) return RTSDS_ERR_UNSUPPORTED;
+  bn_bwd_launch<bf16, 8>(dy, x, nullptr, dx, nullptr, dgamma, dbeta, rows, c, gamma, beta, save_mean, save_invstd, training, act,
+                         accumulate_params, bn_ws(ws, rows, c), (hipStream_t)stream, part, nrb);
+  return hipGetLastError() == hipSuccess ? RTSDS_OK : RTSDS_ERR_LAUNCH;
 }
 
 extern "C" int rtsds_bn_bwd(const void* dy, const void* x, const void* y, void* dx, void* dres, float* dgamma, float* dbeta,

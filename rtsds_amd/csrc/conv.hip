@@ -41,6 +41,13 @@ struct ConvArgs {
   // produced this conv's input (mask = that input, NHWC like dx), fused into the epilogue
   const void* mask;
   int mask_act;
+  // DGRAD: the backward statistics of the BatchNorm (+ ReLU / LeakyReLU) that produced this
+  // conv's input, from the stored dx values: per M tile and channel (sum g, sum g (x - mean)),
+  // g = dx * act'(x * scale + shift) -- bn_bwd_stats_kernel's quantities, [N][mtile][2]
+  float* bnb_part;
+  const void* bnb_x;               // the BatchNorm's input, NHWC like dx
+  const float *bnb_gamma, *bnb_beta, *bnb_mean, *bnb_invstd;
+  int bnb_act;
   float* stats;       // FWD: per-M-tile BatchNorm partials [N][mtile][count, mean, M2, 0] (or null)
   long split_stride;  // elements between WGRAD split slabs (and DGRAD split-K slabs)
   float* slab;        // DGRAD split-K: fp32 partials [split][M][N] instead of the bf16 epilogue
@@ -923,6 +930,21 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(const ConvArgs P0) {
         static_assert(BM * CP <= NBUF * (A_EL + B_EL), "epilogue staging fits the operand LDS");
         T* cs = smem;
         const bool post = has_res || P.accum || has_mask;
+        const bool bnb = MODE == MODE_DGRAD && P.bnb_part != nullptr;  // (host: CPR divides 256)
+        float bg[V], bgx[V], bmu[V], bsc[V], bsh[V];
+        if (bnb) {
+          const int ch0 = n0 + (tid % CPR) * V;  // this thread's fixed channel chunk
+#pragma unroll
+          for (int q = 0; q < V; ++q) {
+            const int ch = min(ch0 + q, P.N - 1);
+            const float g = P.bnb_gamma ? P.bnb_gamma[ch] : 1.f, b = P.bnb_beta ? P.bnb_beta[ch] : 0.f;
+            bmu[q] = P.bnb_mean[ch];
+            bsc[q] = g * P.bnb_invstd[ch];     // bn_coef
+            bsh[q] = fmaf(-bmu[q], bsc[q], b);
+            bg[q] = 0.f;
+            bgx[q] = 0.f;
+          }
+        }
         __syncthreads();
 #pragma unroll
         for (int j = 0; j < FN; ++j) {
@@ -969,6 +991,37 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(const ConvArgs P0) {
               for (int q = 0; q < V; ++q) v[q] = from_f<T>(act_f(f[q]));
             }
             *(V16*)(out + o) = v;
+            if (bnb) {
+              const V16 xr = *(const V16*)((const T*)P.bnb_x + o);
+#pragma unroll
+              for (int q = 0; q < V; ++q) {
+                const float xv = to_f(xr[q]);
+                float g = to_f(v[q]);
+                g *= fmaf(xv, bsc[q], bsh[q]) > 0.f ? 1.f : (P.bnb_act == RTSDS_ACT_LEAKY ? 0.2f : 0.f);
+                bg[q] += g;
+                bgx[q] = fmaf(g, xv - bmu[q], bgx[q]);
+              }
+            }
+          }
+        }
+        if (bnb) {
+          // threads tid = cc + CPR * k share chunk cc: sum their partials in a fixed order
+          __syncthreads();
+          float* red = (float*)smem;  // [256][2 V]
+#pragma unroll
+          for (int q = 0; q < V; ++q) {
+            red[tid * 2 * V + q] = bg[q];
+            red[tid * 2 * V + V + q] = bgx[q];
+          }
+          __syncthreads();
+          for (int e = tid; e < CPR * V; e += 256) {
+            const int cc = e / V, q = e - cc * V, ch = n0 + cc * V + q;
+            float a = 0.f, b = 0.f;
+            for (int t = cc; t < 256; t += CPR) {
+              a += red[t * 2 * V + q];
+              b += red[t * 2 * V + V + q];
+            }
+            if (ch < P.N) *(float2*)(P.bnb_part + ((long)ch * gridDim.x + mt) * 2) = make_float2(a, b);
           }
         }
         stored = true;
@@ -1738,12 +1791,45 @@ static void phase_taps(int a, int pad, int dil, int ksz, int size, int& off, int
 
 // mask: see ConvArgs::mask.  Paths whose epilogue does not apply it (pooled, narrow 1x1, halo,
 // split-K) report false and the caller masks dx in place afterwards.
+struct BnbArgs {  // see ConvArgs::bnb_part
+  float* part;
+  const void* x;
+  const float *gamma, *beta, *mean, *invstd;
+  int act;
+};
 static int dgrad_impl(const rtsds_conv_desc* d0, const void* dy, const void* w, void* dx, int accumulate, const void* mask,
-                      int mask_act, bool& masked, void* ws, size_t ws_bytes, void* stream);
+                      int mask_act, bool& masked, void* ws, size_t ws_bytes, void* stream, const BnbArgs* bnb = nullptr);
 extern "C" int rtsds_conv2d_dgrad(const rtsds_conv_desc* d0, const void* dy, const void* w, void* dx,
                                   int accumulate, void* ws, size_t ws_bytes, void* stream) {
   bool masked = false;
   return dgrad_impl(d0, dy, w, dx, accumulate, nullptr, 0, masked, ws, ws_bytes, stream);
+}
+static bool dgrad_hconv(const rtsds_conv_desc* d, int kp);
+static DgradSplit dgrad_split(const rtsds_conv_desc* d, int kp);
+// M tiles of the data-gradient GEMM when its epilogue can emit the BatchNorm backward
+// statistics (bf16, stride 1, plain GEMM path: not the pooled / narrow-1x1 / halo / split-K
+// routes, vector epilogue), else 0
+extern "C" int rtsds_conv2d_dgrad_bnstats_tiles(const rtsds_conv_desc* d) {
+  if (check_desc(d) || d->dtype != RTSDS_BF16 || d->sh != 1 || d->sw != 1 || d->c % 8 != 0) return 0;
+  if (pooled_1x1(d) || pw_ok(d)) return 0;
+  const int kp = pad_c(d->k, d->dtype);
+  if (dgrad_hconv(d, kp) || dgrad_split(d, kp).splits > 1) return 0;
+  int bm, bn;
+  const long M = (long)d->n * d->h * d->w;
+  pick_tile(M, d->c, true, bm, bn, false);
+  if (256 % (bn / 8) != 0) return 0;
+  return (int)((M + bm - 1) / bm);
+}
+extern "C" int rtsds_conv2d_dgrad_bnstats(const rtsds_conv_desc* d0, const void* dy, const void* w, void* dx, const void* bn_x,
+                                          const float* gamma, const float* beta, const float* save_mean,
+                                          const float* save_invstd, int act, float* part, void* ws, size_t ws_bytes,
+                                          void* stream) {
+  if (rtsds_conv2d_dgrad_bnstats_tiles(d0) == 0) return RTSDS_ERR_UNSUPPORTED;
+  if (!bn_x || !save_mean || !save_invstd || !part || (act != RTSDS_ACT_NONE && act != RTSDS_ACT_RELU && act != RTSDS_ACT_LEAKY))
+    return RTSDS_ERR_UNSUPPORTED;
+  const BnbArgs b = {part, bn_x, gamma, beta, save_mean, save_invstd, act};
+  bool masked = false;
+  return dgrad_impl(d0, dy, w, dx, 0, nullptr, 0, masked, ws, ws_bytes, stream, &b);
 }
 extern "C" int rtsds_act_bwd(const void* dy, const void* y, void* dx, long n, int act, float alpha, int dtype, void* stream);
 extern "C" int rtsds_conv2d_dgrad_act(const rtsds_conv_desc* d0, const void* dy, const void* w, void* dx, const void* x_act,
@@ -1755,7 +1841,7 @@ extern "C" int rtsds_conv2d_dgrad_act(const rtsds_conv_desc* d0, const void* dy,
   return rtsds_act_bwd(dx, x_act, dx, (long)d0->n * d0->h * d0->w * d0->c, act, 1.f, d0->dtype, stream);
 }
 static int dgrad_impl(const rtsds_conv_desc* d0, const void* dy, const void* w, void* dx, int accumulate, const void* mask,
-                      int mask_act, bool& masked, void* ws, size_t ws_bytes, void* stream) {
+                      int mask_act, bool& masked, void* ws, size_t ws_bytes, void* stream, const BnbArgs* bnb) {
   masked = false;
   int e = check_desc(d0);
   if (e) return e;
@@ -1850,6 +1936,10 @@ static int dgrad_impl(const rtsds_conv_desc* d0, const void* dy, const void* w, 
     p.accum = accumulate ? 1 : 0;
     p.mask = mask;
     p.mask_act = mask_act;
+    if (bnb) {  // (rtsds_conv2d_dgrad_bnstats_tiles checked this route)
+      p.bnb_part = bnb->part; p.bnb_x = bnb->x; p.bnb_gamma = bnb->gamma; p.bnb_beta = bnb->beta;
+      p.bnb_mean = bnb->mean; p.bnb_invstd = bnb->invstd; p.bnb_act = bnb->act;
+    }
     p.M = d.n * d.h * d.w;
     p.N = d.c;
     p.K = d.kh * d.kw * kp;

@@ -135,7 +135,8 @@ class ConvFn(torch.autograd.Function):
     parameter itself or its bf16 shadow); gradients are returned for ``weight``."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, wq, stride, padding, dilation, act, stats, join=None, fold=(0, False)):
+    def forward(ctx, x, weight, bias, wq, stride, padding, dilation, act, stats, join=None, fold=(0, False),
+                bn_link=None):
         """``fold = (in_act, out_folded)``: ``in_act`` -- x is the output of a ReLU / LeakyReLU
         whose backward this conv's data gradient applies in its epilogue
         (rtsds_conv2d_dgrad_act); ``out_folded`` -- the single consumer of y does that for this
@@ -155,6 +156,7 @@ class ConvFn(torch.autograd.Function):
                                         ws.numel(), stream())
         ctx.xflag = flag
         ctx.in_act, ctx.out_folded = fold
+        ctx.bn_link = bn_link if join is None and not fold[0] else None
         if ctx.in_act and join is not None:
             raise RuntimeError("rtsds_amd: a conv whose input gradient is masked cannot join other readers")
         ctx.d, ctx.act, ctx.has_bias = d, act, bias is not None
@@ -193,8 +195,18 @@ class ConvFn(torch.autograd.Function):
             acc = join is not None and join.buf is not None  # accumulate onto the earlier contribution
             dx = join.buf if acc else empty_nhwc(d.n, d.c, d.h, d.w, x.dtype, x.device)
             ws = workspace(lib.rtsds_conv2d_dgrad_workspace(ctypes.byref(d)), x.device)
+            link = ctx.bn_link
+            tiles = 0
+            if link is not None and link.src is not None and not acc and g.dtype == torch.bfloat16:
+                tiles = lib.rtsds_conv2d_dgrad_bnstats_tiles(ctypes.byref(d))
             with _Timed(d, "dgrad"):
-                if ctx.in_act:
+                if tiles:
+                    bx, bsm, bsi, bg, bb, bact = link.src
+                    part = torch.empty(d.c * tiles * 2, dtype=torch.float32, device=x.device)
+                    lib.rtsds_conv2d_dgrad_bnstats(ctypes.byref(d), _P(g), _P(wq), _P(dx), _P(bx), _P(bg), _P(bb),
+                                                   _P(bsm), _P(bsi), bact, _P(part), _P(ws), ws.numel(), stream())
+                    link.part, link.nrb = part, tiles
+                elif ctx.in_act:
                     lib.rtsds_conv2d_dgrad_act(ctypes.byref(d), _P(g), _P(wq), _P(dx), _P(x), ctx.in_act, _P(ws),
                                                ws.numel(), stream())
                 else:
@@ -221,11 +233,11 @@ class ConvFn(torch.autograd.Function):
                                                   ws.numel(), stream())
                 if not ctx.needs_input_grad[1]:
                     dw = None
-        return dx, dw, db, None, None, None, None, None, None, None, None
+        return dx, dw, db, None, None, None, None, None, None, None, None, None
 
 
 def conv2d(x, weight, bias, wq, stride=(1, 1), padding=(0, 0), dilation=(1, 1), act=0, bn_stats=False,
-           join=None, in_act=0, fold_out=False):
+           join=None, in_act=0, fold_out=False, bn_link=None):
     """bn_stats=True: the conv epilogue also emits the following BatchNorm's per-tile batch
     statistics, attached to the output as ``_rt_bn_stats`` and consumed by batch_norm().
     ``join``: GradJoin shared with the other readers of ``x``."""
@@ -237,7 +249,7 @@ def conv2d(x, weight, bias, wq, stride=(1, 1), padding=(0, 0), dilation=(1, 1), 
         nrb = lib.rtsds_conv2d_fwd_stats_tiles(ctypes.byref(d))
         stats = torch.empty(nrb * k * 4, dtype=torch.float32, device=x.device)  # [k][nrb][4]
     y = ConvFn.apply(x, weight, bias, wq, tuple(stride), tuple(padding), tuple(dilation), act, stats, join,
-                     (in_act, bool(fold_out and act in (1, 2))))
+                     (in_act, bool(fold_out and act in (1, 2))), bn_link)
     if stats is not None:
         y._rt_bn_stats = (stats, nrb)
     return y
@@ -334,12 +346,30 @@ class ConvSumFn(torch.autograd.Function):
 
 
 # ----------------------------------------------------------------------------- batch norm
+BN_BWD_LINK = True  # False: every BatchNorm backward computes its own statistics (A/B tests)
+
+
+class BnBwdLink:
+    """Hands a train-mode BatchNorm's backward statistics from the data gradient of the conv
+    that reads its (activated) output to the BatchNorm's backward, which then skips its own
+    statistics pass (rtsds_conv2d_dgrad_bnstats -> rtsds_bn_bwd_part).  Created by a module
+    whose BatchNorm output has exactly that one reader (ResNet BasicBlock bn1 -> conv2,
+    Bottleneck bn1 -> conv2 -> bn2 -> conv3); ignored wherever a route does not apply."""
+
+    __slots__ = ("src", "part", "nrb")
+
+    def __init__(self):
+        self.src = None   # (bn input x, save_mean, save_invstd, gamma, beta, act), set by the BN forward
+        self.part = None  # set by the conv backward, consumed by the BN backward
+        self.nrb = 0
+
+
 class BatchNormFn(torch.autograd.Function):
     """BatchNorm2d (+ residual add) (+ ReLU/LeakyReLU) fused, train or eval statistics."""
 
     @staticmethod
     def forward(ctx, x, gamma, beta, res, running_mean, running_var, training, momentum, eps, act,
-                stats, stats_nrb, nbt, res_join=None):
+                stats, stats_nrb, nbt, res_join=None, link=None):
         require_hip(x)
         x = nhwc(x)
         if res is not None:
@@ -361,6 +391,11 @@ class BatchNormFn(torch.autograd.Function):
         # (bit-identical pre-activation), so y is neither kept nor re-read.
         keep_y = res is not None or act == ACT_SIGMOID
         ctx.save_for_backward(x, y if keep_y else None, gamma, beta, sm, si)
+        ctx.link = None
+        if link is not None and BN_BWD_LINK and training and res is None and act in (0, 1, 2) \
+                and x.dtype == torch.bfloat16 and c % 8 == 0:
+            link.src, link.part = (x, sm, si, gamma, beta, act), None
+            ctx.link = link
         return y
 
     @staticmethod
@@ -380,24 +415,33 @@ class BatchNormFn(torch.autograd.Function):
             db = torch.empty(c, dtype=torch.float32, device=x.device) if need_b else None
             acc = 0
         ws = workspace(lib.rtsds_bn_workspace(rows, c), x.device)
-        lib.rtsds_bn_bwd(_P(dy), _P(x), _P(y), _P(dx), _P(dres), _P(dg), _P(db), rows, c,
-                         _P(gamma), _P(beta), _P(sm), _P(si), training, act, acc, dcode(x), _P(ws), ws.numel(),
-                         stream())
+        link = ctx.link
+        if link is not None and link.part is not None and dy.dtype == x.dtype:
+            # statistics from the reading conv's data-gradient epilogue
+            lib.rtsds_bn_bwd_part(_P(dy), _P(x), _P(dx), _P(dg), _P(db), rows, c, _P(gamma), _P(beta), _P(sm),
+                                  _P(si), training, act, acc, _P(link.part), link.nrb, dcode(x), _P(ws), ws.numel(),
+                                  stream())
+        else:
+            lib.rtsds_bn_bwd(_P(dy), _P(x), _P(y), _P(dx), _P(dres), _P(dg), _P(db), rows, c,
+                             _P(gamma), _P(beta), _P(sm), _P(si), training, act, acc, dcode(x), _P(ws), ws.numel(),
+                             stream())
+        if link is not None:
+            link.src = link.part = None
         if acc:
             dg = db = None
         if dres is not None:
             dres = _join_add(ctx.res_join, dres)
-        return dx, dg, db, dres, None, None, None, None, None, None, None, None, None, None
+        return dx, dg, db, dres, None, None, None, None, None, None, None, None, None, None, None
 
 
 def batch_norm(x, gamma, beta, running_mean, running_var, training, momentum, eps, act=0,
-               residual=None, num_batches_tracked=None, res_join=None):
+               residual=None, num_batches_tracked=None, res_join=None, link=None):
     """``num_batches_tracked`` (int64, optional) is incremented by the finalize kernel.
     ``res_join``: GradJoin shared with the other readers of ``residual``."""
     st = getattr(x, "_rt_bn_stats", None) if training else None
     stats, nrb = st if st is not None else (None, None)
     return BatchNormFn.apply(x, gamma, beta, residual, running_mean, running_var, training,
-                             momentum, eps, act, stats, nrb, num_batches_tracked, res_join)
+                             momentum, eps, act, stats, nrb, num_batches_tracked, res_join, link)
 
 
 # ----------------------------------------------------------------------------- layout / dtype

@@ -11,6 +11,7 @@ import torch
 import torch.nn as nn
 
 from rtsds_amd import functional as F
+from rtsds_amd.functional import BnBwdLink
 from rtsds_amd.nn import BatchNorm2d, Conv2d, MaxPool2d, ReLU, conv_bn, conv_bn_relu_maxpool, grad_join, to_input
 from rtsds_amd.nn import _shadow
 
@@ -43,10 +44,11 @@ class Bottleneck(nn.Module):
         # x's two readers accumulate their gradients into one buffer (nn.grad_join)
         join = grad_join(x, 2)
         skip = x if self.downsample is None else conv_bn(self.downsample[0], self.downsample[1], x, join=join)
-        t = conv_bn(self.conv1, self.bn1, x, "relu", join=join)
-        t = conv_bn(self.conv2, self.bn2, t, "relu")
+        l1, l2 = BnBwdLink(), BnBwdLink()  # bn1 -> conv2, bn2 -> conv3 (single readers)
+        t = conv_bn(self.conv1, self.bn1, x, "relu", join=join, out_link=l1)
+        t = conv_bn(self.conv2, self.bn2, t, "relu", in_link=l1, out_link=l2)
         return conv_bn(self.conv3, self.bn3, t, "relu", skip,
-                       res_join=join if self.downsample is None else None)
+                       res_join=join if self.downsample is None else None, in_link=l2)
 
 
 class ClassifierModule(nn.Module):

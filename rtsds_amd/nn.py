@@ -48,18 +48,18 @@ class Conv2d(nn.Conv2d):
             self.weight.data = self.weight.data.contiguous(memory_format=CL)
         return out
 
-    def forward(self, x, act=None, bn_stats=False, join=None, in_act=None, fold_out=False):
+    def forward(self, x, act=None, bn_stats=False, join=None, in_act=None, fold_out=False, bn_link=None):
         """``bn_stats``: also emit the batch statistics of a directly following train-mode
         BatchNorm from the conv epilogue (see functional.conv2d).  ``join``: a
         functional.GradJoin shared with the other readers of ``x``.  ``in_act`` / ``fold_out``:
         activation-backward folding between chained convs (functional.ConvFn)."""
         wq = _shadow(self.weight, x.dtype)
         return F.conv2d(x, self.weight, self.bias, wq, self.stride, self.padding, self.dilation,
-                        ACT[act], bn_stats, join, ACT[in_act], fold_out)
+                        ACT[act], bn_stats, join, ACT[in_act], fold_out, bn_link)
 
 
 class BatchNorm2d(nn.BatchNorm2d):
-    def forward(self, x, act=None, residual=None, res_join=None):
+    def forward(self, x, act=None, residual=None, res_join=None, link=None):
         training = self.training or not self.track_running_stats
         if training and x.shape[0] * x.shape[2] * x.shape[3] == 1:
             raise ValueError(f"Expected more than 1 value per channel when training, got input size {tuple(x.shape)}")
@@ -70,7 +70,7 @@ class BatchNorm2d(nn.BatchNorm2d):
         # num_batches_tracked.add_(1) happens inside the statistics-finalize kernel
         nbt = self.num_batches_tracked if (self.training and self.track_running_stats) else None
         return F.batch_norm(x, self.weight, self.bias, rm, rv, training, self.momentum, self.eps,
-                            ACT[act], residual, nbt, res_join)
+                            ACT[act], residual, nbt, res_join, link)
 
 
 class ReLU(nn.Module):
@@ -127,18 +127,22 @@ def _no_grad_needed(conv, bn, x, residual):
     return not any(t is not None and t.requires_grad for t in ts)
 
 
-def conv_bn(conv, bn, x, act=None, residual=None, join=None, res_join=None):
+def conv_bn(conv, bn, x, act=None, residual=None, join=None, res_join=None, in_link=None, out_link=None):
     """bn(conv(x)) with the BatchNorm's batch statistics produced by the conv epilogue
     (train mode) instead of a separate pass over the conv output.  Eval mode without
     autograd (inference, validation): the BN (+ residual + act) folds into the conv's
     epilogue -- one launch per ConvBlock / residual branch.  ``join`` / ``res_join``:
-    functional.GradJoin shared by the readers of ``x`` / ``residual`` (residual blocks)."""
+    functional.GradJoin shared by the readers of ``x`` / ``residual`` (residual blocks).
+    ``in_link``: functional.BnBwdLink of the BatchNorm that produced ``x`` (its backward
+    statistics come from this conv's data gradient); ``out_link``: the link this BatchNorm
+    registers with (its output's single reader passes it as ``in_link``)."""
     use_batch = bn.training or not bn.track_running_stats
     if not use_batch and bn.momentum is not None and _no_grad_needed(conv, bn, x, residual):
         wq = _shadow(conv.weight, x.dtype)
         return F.conv_bn_eval(x, conv.weight, conv.bias, wq, conv.stride, conv.padding, conv.dilation,
                               bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.eps, ACT[act], residual)
-    return bn(conv(x, bn_stats=use_batch, join=join), act=act, residual=residual, res_join=res_join)
+    return bn(conv(x, bn_stats=use_batch, join=join, bn_link=in_link), act=act, residual=residual, res_join=res_join,
+              link=out_link)
 
 
 def conv_bn_relu_maxpool(conv, bn, pool, x):

@@ -650,3 +650,45 @@ def test_discriminator_activation_fold_bit_identical(dt, cls):
     assert torch.equal(gx0, gx1)
     for k in p0:
         assert torch.equal(p0[k], p1[k]), k
+
+
+@pytest.mark.parametrize("block", ["basic", "bottleneck", "bottleneck_dil"])
+def test_bn_backward_stats_from_dgrad_epilogue(block):
+    """BnBwdLink: a BatchNorm's backward statistics taken from the reading conv's data-gradient
+    epilogue (rtsds_conv2d_dgrad_bnstats -> rtsds_bn_bwd_part) vs the BatchNorm's own
+    statistics pass.  Same quantities, different fp32 summation order: outputs identical,
+    gradients within a few bf16 ulps."""
+    from rtsds_amd import functional as Fn
+    from rtsds_amd.models.bisenet.build_contextpath import BasicBlock, Bottleneck as TvBottleneck
+    from rtsds_amd.models.deeplabv2.deeplabv2 import Bottleneck as DlBottleneck
+    g = torch.Generator().manual_seed(13)
+    if block == "basic":
+        make, c = (lambda: BasicBlock(64, 64)), 64
+    elif block == "bottleneck":
+        make, c = (lambda: TvBottleneck(256, 64)), 256
+    else:
+        make, c = (lambda: DlBottleneck(256, 64, dilation=2)), 256
+    x = torch.randn(4, c, 32, 48, generator=g)
+    gy = torch.randn(4, c, 32, 48, generator=g)
+    res = []
+    with rtsds_amd.precision(torch.bfloat16):
+        for on in (False, True):
+            Fn.BN_BWD_LINK = on
+            try:
+                torch.manual_seed(4)
+                m = make().to(DEV).train()
+                xi = x.to(DEV).requires_grad_()
+                y = m(xi)
+                y.backward(gy.to(DEV).to(y.dtype))
+                torch.cuda.synchronize()
+                res.append((y.detach().float().cpu(), xi.grad.float().cpu(),
+                            {k: p.grad.detach().float().cpu().clone() for k, p in m.named_parameters() if p.grad is not None}))
+            finally:
+                Fn.BN_BWD_LINK = True
+    (y0, gx0, p0), (y1, gx1, p1) = res
+    assert torch.equal(y0, y1)
+    assert (gx0 - gx1).abs().max() <= 2e-2 * gx0.abs().max()
+    assert (gx0 - gx1).abs().mean() <= 1e-3 * gx0.abs().mean() + 1e-6
+    assert set(p0) == set(p1)
+    for k in p0:
+        assert (p0[k] - p1[k]).abs().max() <= 1e-2 * p0[k].abs().max() + 1e-6, k

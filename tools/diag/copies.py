@@ -10,7 +10,7 @@ import bench
 from rtsds_amd import set_compute_dtype
 
 set_compute_dtype(torch.bfloat16)
-wl = sys.argv[1] if len(sys.argv) > 1 else "bisenet-seg"
+wl = sys.argv.pop(1) if len(sys.argv) > 1 else "bisenet-seg"
 args = bench.parse()
 args.workload, args.batch, args.da_unfused = wl, bench.WORKLOADS[wl][2], False
 dev = torch.device("cuda", 0)
@@ -28,7 +28,9 @@ rows = [e for e in ka if e.device_type.name == "CUDA" or "Memcpy" in e.key or "M
 for e in prof.events():
     pass
 print(prof.key_averages(group_by_input_shape=True).table(sort_by="self_cuda_time_total", row_limit=40))
-print(prof.key_averages(group_by_stack_n=8).table(sort_by="cpu_time_total", row_limit=0)[:0])
+for e in prof.key_averages(group_by_input_shape=True):
+    if any(k in e.key for k in ("copy", "Memcpy", "Memset", "fill", "elementwise", "zero", "Copy")):
+        print(f"{e.key[:70]:70s} n={e.count:3d} cuda_us={e.self_device_time_total:8.1f} shapes={str(e.input_shapes)[:120]}")
 # aten ops that launch device work, with stacks
 for e in prof.key_averages(group_by_stack_n=8):
     if e.key.startswith("aten::") and e.key in ("aten::copy_", "aten::zero_", "aten::fill_", "aten::zeros", "aten::add_",
