@@ -13,6 +13,8 @@ from torch import nn
 
 from rtsds_amd import functional as F
 from rtsds_amd.nn import AdaptiveAvgPool2d, BatchNorm2d, Conv2d, ReLU, Sigmoid, conv_bn, grad_join, to_input
+from rtsds_amd.runtime import BranchOut, branch_stream
+
 from .build_contextpath import build_contextpath
 
 
@@ -95,6 +97,10 @@ _HEADS = {"resnet18": (256, 512), "resnet101": (1024, 2048)}
 class BiSeNet(torch.nn.Module):
     """build_bisenet.py:84-172."""
 
+    # training: spatial path on runtime.branch_stream beside the context path (bs 8 train step
+    # +2.5 %; at inference the fork / join edges cost more than the overlap gains)
+    branch_parallel = True
+
     def __init__(self, num_classes, context_path, with_interpolation=True):
         super().__init__()
         self.with_interpolation = with_interpolation
@@ -132,8 +138,22 @@ class BiSeNet(torch.nn.Module):
         heads (build_bisenet.py:151-166).  main_only: skip the supervision heads (1x1 convs
         with no state; for callers that discard them, e.g. the DA target branch)."""
         x = to_input(input)
-        sx = self.saptial_path(x)
-        f3, f4, tail = self.context_path(x)
+        if self.branch_parallel and self.training and x.is_cuda and F.CONV_PROFILE is None:
+            # (not while bench.py event-times each conv: concurrent branches would inflate them)
+            # spatial path on the branch stream, concurrently with the context path (forward and,
+            # through autograd's per-op streams, backward); joined before the fusion module
+            main = torch.cuda.current_stream(x.device)
+            side = branch_stream(x.device)
+            side.wait_stream(main)
+            x.record_stream(side)  # read (and saved for backward) on the branch stream
+            with torch.cuda.stream(side):
+                sx = BranchOut.apply(self.saptial_path(x), main, side)
+            f3, f4, tail = self.context_path(x)
+            main.wait_stream(side)
+            sx.record_stream(main)
+        else:
+            sx = self.saptial_path(x)
+            f3, f4, tail = self.context_path(x)
         cx1 = self.attention_refinement_module1(f3)
         cx2 = F.channel_scale(self.attention_refinement_module2(f4), tail)
         hw = sx.shape[-2:]

@@ -140,6 +140,41 @@ def side_join():
     _side["armed"] = False
 
 
+# ----------------------------------------------------------------------------- branch streams
+# Independent branches of one network (BiSeNet's spatial path beside its ResNet context path)
+# run on a second stream: forward forks after the shared input and joins before the first op
+# that reads both; autograd runs each backward op on its forward op's stream, so the backward
+# branches overlap too, and an engine callback queued by the branch's first backward op joins
+# the branch back into the ambient stream at the end of backward (its weight gradients go
+# straight into optimizer arenas, which autograd does not see).  Under hipGraph capture the
+# fork / joins are graph edges.
+_branch = {}
+
+
+def branch_stream(device):
+    s = _branch.get(device)
+    if s is None:
+        s = _branch[device] = torch.cuda.Stream(device=device)
+    return s
+
+
+class BranchOut(torch.autograd.Function):
+    """Identity on a branch's output (applied on the branch stream); its backward -- the
+    branch's first backward op -- queues the end-of-backward join of ``side`` into ``main``."""
+
+    @staticmethod
+    def forward(ctx, x, main, side):
+        ctx.main, ctx.side = main, side
+        return x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        g.record_stream(ctx.side)
+        main, side = ctx.main, ctx.side
+        torch.autograd.Variable._execution_engine.queue_callback(lambda: main.wait_stream(side))
+        return g, None, None
+
+
 class GraphedForward:
     """hipGraph capture of a fixed-shape inference forward (torch.cuda.CUDAGraph is a hipGraph
     on ROCm): every rtsds kernel of ``module(x)`` is recorded once on a side stream and the

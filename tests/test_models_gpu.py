@@ -692,3 +692,33 @@ def test_bn_backward_stats_from_dgrad_epilogue(block):
     assert set(p0) == set(p1)
     for k in p0:
         assert (p0[k] - p1[k]).abs().max() <= 1e-2 * p0[k].abs().max() + 1e-6, k
+
+
+@pytest.mark.parametrize("graphed", [False, True])
+def test_bisenet_branch_streams_bit_identical(graphed):
+    """BiSeNet.branch_parallel (spatial path on runtime.branch_stream beside the context path,
+    forward and backward) leaves losses, parameters and optimizer state bit-identical to the
+    single-stream iteration, eagerly and as hipGraph replays."""
+    from rtsds_amd.runtime import GraphedStep
+    g = torch.Generator().manual_seed(8)
+    x = torch.randn(2, 3, 128, 256, generator=g).to(DEV)
+    y = torch.randint(0, 20, (2, 128, 256), generator=g).to(DEV)
+    ce = losses.CrossEntropyLoss(ignore_index=19)
+    runs = []
+    with rtsds_amd.precision(torch.bfloat16):
+        for par in (False, True):
+            torch.manual_seed(2)
+            net = BiSeNet(19, "resnet18").to(DEV).train()
+            net.branch_parallel = par
+            opt = optim.Adam(net.parameters(), lr=1e-3)
+            core = lambda: rtrain.seg_step(net, ce, opt, x, y)  # noqa: E731
+            step = GraphedStep(core, [opt], warmup=1) if graphed else core
+            ls = [float(step()[0]) for _ in range(3)]
+            torch.cuda.synchronize()
+            st = {k: v.detach().float().cpu().clone() for k, v in net.state_dict().items()}
+            st.update({f"m{i}": a.m.cpu() for i, a in enumerate(opt.arenas())})
+            runs.append((ls, st))
+    (l0, s0), (l1, s1) = runs
+    assert l0 == l1
+    for k in s0:
+        assert torch.equal(s0[k], s1[k]), k
