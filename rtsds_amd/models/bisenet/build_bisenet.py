@@ -13,7 +13,7 @@ from torch import nn
 
 from rtsds_amd import functional as F
 from rtsds_amd.nn import AdaptiveAvgPool2d, BatchNorm2d, Conv2d, ReLU, Sigmoid, conv_bn, grad_join, to_input
-from rtsds_amd.runtime import BranchOut, branch_stream
+from rtsds_amd.runtime import BranchOut, branch_stream, branches_enabled
 
 from .build_contextpath import build_contextpath
 
@@ -138,7 +138,7 @@ class BiSeNet(torch.nn.Module):
         heads (build_bisenet.py:151-166).  main_only: skip the supervision heads (1x1 convs
         with no state; for callers that discard them, e.g. the DA target branch)."""
         x = to_input(input)
-        if self.branch_parallel and self.training and x.is_cuda and F.CONV_PROFILE is None:
+        if self.branch_parallel and self.training and x.is_cuda and F.CONV_PROFILE is None and branches_enabled():
             # (not while bench.py event-times each conv: concurrent branches would inflate them)
             # spatial path on the branch stream, concurrently with the context path (forward and,
             # through autograd's per-op streams, backward); joined before the fusion module

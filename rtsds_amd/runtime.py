@@ -151,10 +151,28 @@ def side_join():
 _branch = {}
 
 
-def branch_stream(device):
-    s = _branch.get(device)
+_branch_off = {"depth": 0}
+
+
+@contextlib.contextmanager
+def branches_serial():
+    """Modules issue their branches on the current stream (already a concurrent branch: a
+    fork nested in it measured no gain and broke hipGraph capture of the DA iteration)."""
+    _branch_off["depth"] += 1
+    try:
+        yield
+    finally:
+        _branch_off["depth"] -= 1
+
+
+def branches_enabled():
+    return _branch_off["depth"] == 0
+
+
+def branch_stream(device, name="spatial"):
+    s = _branch.get((device, name))
     if s is None:
-        s = _branch[device] = torch.cuda.Stream(device=device)
+        s = _branch[(device, name)] = torch.cuda.Stream(device=device)
     return s
 
 

@@ -6,11 +6,13 @@ The per-iteration bodies are factored into ``seg_step`` (train.py:65-113) and ``
 one ``.item()`` batch per iteration (losses + pixel-accuracy counter fetched together)
 instead of the reference's 6-9 separate syncs; the logged values are identical.
 """
+import contextlib
+
 import torch
 
 from . import functional as F
 from . import losses, utils
-from .runtime import dp_world
+from .runtime import branch_stream, branches_serial, dp_world
 from .callbacks import Callback
 from .validation import val_GTA5
 
@@ -152,6 +154,11 @@ def _seg_loss(model, criterion, x, label, correct):
     return loss, outs[0], None
 
 
+# da_step (fused path, single process): target forward on a second stream during the source
+# backward (see _da_step_fused); False = strictly serial issue (A/B tests)
+DA_OVERLAP = True
+
+
 def _start_allreduce(optimizer):
     if dp_world() > 1 and hasattr(optimizer, "start_grad_allreduce"):
         optimizer.start_grad_allreduce()
@@ -176,12 +183,12 @@ def da_step(generator, discriminator, generator_optimizer, discriminator_optimiz
     correct = torch.zeros(1, dtype=torch.int64, device=source_image.device)
     loss_seg, main, geo = _seg_loss(generator, generator_loss, source_image, source_label, correct)
     loss_seg = loss_seg / iterations
-    loss_seg.backward()
     if geo is not None and getattr(discriminator, "accepts_padded_probs", False) and \
             hasattr(generator, "forward_lowres") and main.shape[1] <= 32:
         return _da_step_fused(generator, discriminator, generator_optimizer, discriminator_optimizer,
                               discriminator_loss, main, geo, target_image, lambda_, iterations, loss_seg,
                               correct)
+    loss_seg.backward()
     with torch.no_grad():
         source_features = _full(main.detach(), geo)
 
@@ -217,14 +224,38 @@ def _da_step_fused(generator, discriminator, generator_optimizer, discriminator_
     reference's D(softmax(G(x))) at train.py:225,245,256 -- without the full-resolution logits,
     the separate softmax pass or the conv's channel-pad pass.  softmax(target_feature.detach())
     (train.py:256) equals the G-phase target probabilities, so they are computed once."""
+    amb = torch.cuda.current_stream(main.device)
+    overlap = DA_OVERLAP and dp_world() <= 1
+    if overlap:
+        # the target forward (G, resize + softmax, frozen D, loss) depends only on parameters
+        # the source backward does not touch: it runs on a second stream, concurrently with
+        # loss_seg.backward() (BatchNorm running statistics still update source then target;
+        # the adversarial backward, on the target ops' stream, starts after the source backward
+        # -- autograd orders it after the ambient stream -- so G's gradient accumulation order
+        # is unchanged)
+        side = branch_stream(main.device, "da_target")
+        side.wait_stream(amb)
+        target_image.record_stream(side)
+        ctx = torch.cuda.stream(side)
+    else:
+        loss_seg.backward()
+        ctx = contextlib.nullcontext()
+    with ctx, (branches_serial() if overlap else contextlib.nullcontext()):
+        (t_low, t_geo), = generator.forward_lowres(target_image, main_only=True)
+        target_probs = F.upsample_softmax(t_low, t_geo)
+        pred_t = discriminator(target_probs)
+        ones = torch.ones(pred_t.size(), device=pred_t.device)
+        loss_adv = lambda_ * discriminator_loss(pred_t, ones) / iterations
+    if overlap:
+        loss_seg.backward()
+        amb.wait_stream(side)
+        for t in (target_probs, loss_adv):
+            t.record_stream(amb)
     with torch.no_grad():
         source_probs = F.upsample_softmax(main.detach(), geo)
-    (t_low, t_geo), = generator.forward_lowres(target_image, main_only=True)
-    target_probs = F.upsample_softmax(t_low, t_geo)
-    pred_t = discriminator(target_probs)
-    ones = torch.ones(pred_t.size(), device=pred_t.device)
-    loss_adv = lambda_ * discriminator_loss(pred_t, ones) / iterations
     loss_adv.backward()
+    if overlap:
+        amb.wait_stream(side)  # the adversarial backward ran on the target ops' streams
     _start_allreduce(generator_optimizer)
 
     for p in discriminator.parameters():

@@ -722,3 +722,41 @@ def test_bisenet_branch_streams_bit_identical(graphed):
     assert l0 == l1
     for k in s0:
         assert torch.equal(s0[k], s1[k]), k
+
+
+@pytest.mark.parametrize("graphed", [False, True])
+def test_da_step_overlap_bit_identical(graphed):
+    """train.DA_OVERLAP (target forward on a second stream during the source backward) leaves
+    the four losses, G/D parameters, optimizer state and BN buffers bit-identical to the
+    serial issue order, eagerly and as hipGraph replays."""
+    from rtsds_amd.runtime import GraphedStep
+    g = torch.Generator().manual_seed(17)
+    x = torch.randn(2, 3, 128, 256, generator=g).to(DEV)
+    xt = torch.randn(2, 3, 128, 256, generator=g).to(DEV)
+    y = torch.randint(0, 20, (2, 128, 256), generator=g).to(DEV)
+    ce, bce = losses.CrossEntropyLoss(ignore_index=19), losses.BCEWithLogitsLoss()
+    runs = []
+    with rtsds_amd.precision(torch.bfloat16):
+        for ov in (False, True):
+            rtrain.DA_OVERLAP = ov
+            try:
+                torch.manual_seed(6)
+                net = BiSeNet(19, "resnet18").to(DEV).train()
+                disc = TinyDomainDiscriminator(19).to(DEV).train()
+                opt = optim.Adam(net.parameters(), lr=1e-3)
+                dopt = optim.Adam(disc.parameters(), lr=1e-3, weight_decay=1e-4)
+                core = lambda: rtrain.da_step(net, disc, opt, dopt, ce, bce, x, y, xt, 0.1, 2)  # noqa: E731
+                step = GraphedStep(core, [opt, dopt], warmup=1) if graphed else core
+                logs = [[float(v) for v in step()] for _ in range(3)]
+                torch.cuda.synchronize()
+                st = {k: v.detach().float().cpu().clone() for k, v in
+                      [("G." + k, v) for k, v in net.state_dict().items()] +
+                      [("D." + k, v) for k, v in disc.state_dict().items()]}
+                st.update({f"m{i}": a.m.cpu() for i, a in enumerate(opt.arenas() + dopt.arenas())})
+                runs.append((logs, st))
+            finally:
+                rtrain.DA_OVERLAP = True
+    (l0, s0), (l1, s1) = runs
+    assert l0 == l1
+    for k in s0:
+        assert torch.equal(s0[k], s1[k]), k
