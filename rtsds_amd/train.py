@@ -253,16 +253,27 @@ def _da_step_fused(generator, discriminator, generator_optimizer, discriminator_
             t.record_stream(amb)
     with torch.no_grad():
         source_probs = F.upsample_softmax(main.detach(), geo)
-    loss_adv.backward()
     if overlap:
-        amb.wait_stream(side)  # the adversarial backward ran on the target ops' streams
+        # D's source phase needs only source_probs and D's (unchanged) weights, and writes only
+        # D's gradients, which the adversarial backward (through the frozen D into G) never
+        # touches: it runs on a third stream beside that backward; D's target phase follows it
+        # (D's gradient accumulation order source -> target is kept)
+        side2 = branch_stream(main.device, "da_disc")
+        side2.wait_stream(amb)
+        source_probs.record_stream(side2)
+    loss_adv.backward()
     _start_allreduce(generator_optimizer)
 
     for p in discriminator.parameters():
         p.requires_grad = True
-    pred_s = discriminator(source_probs)
-    loss_dsrc = discriminator_loss(pred_s, torch.ones(pred_s.size(), device=pred_s.device)) / iterations
-    loss_dsrc.backward()
+    with torch.cuda.stream(side2) if overlap else contextlib.nullcontext():
+        pred_s = discriminator(source_probs)
+        loss_dsrc = discriminator_loss(pred_s, torch.ones(pred_s.size(), device=pred_s.device)) / iterations
+        loss_dsrc.backward()
+    if overlap:
+        amb.wait_stream(side)  # the adversarial backward ran on the target ops' streams
+        amb.wait_stream(side2)
+        loss_dsrc.record_stream(amb)
     pred_t2 = discriminator(F.detach_padded(target_probs))
     loss_dtgt = discriminator_loss(pred_t2, torch.zeros(pred_t2.size(), device=pred_t2.device)) / iterations
     loss_dtgt.backward()
