@@ -144,11 +144,15 @@ class BiSeNet(torch.nn.Module):
             # through autograd's per-op streams, backward); joined before the fusion module
             main = torch.cuda.current_stream(x.device)
             side = branch_stream(x.device)
-            side.wait_stream(main)
-            x.record_stream(side)  # read (and saved for backward) on the branch stream
-            with torch.cuda.stream(side):
-                sx = BranchOut.apply(self.saptial_path(x), main, side)
-            f3, f4, tail = self.context_path(x)
+            box = []
+
+            def fork():  # after the context path's layer2: beside its narrow late layers
+                side.wait_stream(main)
+                x.record_stream(side)  # read (and saved for backward) on the branch stream
+                with torch.cuda.stream(side):
+                    box.append(BranchOut.apply(self.saptial_path(x), main, side))
+            f3, f4, tail = self.context_path(x, mid=fork)
+            sx = box[0]
             main.wait_stream(side)
             sx.record_stream(main)
         else:

@@ -119,10 +119,15 @@ class _ContextPath(nn.Module):
         self.layer1, self.layer2 = trunk.layer1, trunk.layer2
         self.layer3, self.layer4 = trunk.layer3, trunk.layer4
 
-    def forward(self, x):
-        """x: NHWC compute-dtype batch -> (1/16 features, 1/32 features, GAP(1/32))."""
+    def forward(self, x, mid=None):
+        """x: NHWC compute-dtype batch -> (1/16 features, 1/32 features, GAP(1/32)).  ``mid``:
+        called after layer2 (BiSeNet forks its spatial path there, beside the narrow late
+        layers)."""
         t = conv_bn_relu_maxpool(self.conv1, self.bn1, self.maxpool1, x)
-        f3 = self.layer3(self.layer2(self.layer1(t)))
+        t = self.layer2(self.layer1(t))
+        if mid is not None:
+            mid()
+        f3 = self.layer3(t)
         f4 = self.layer4(f3)
         return f3, f4, F.global_avg_pool(f4)
 
