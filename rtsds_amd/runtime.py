@@ -166,7 +166,11 @@ def branches_serial():
 
 
 def branches_enabled():
-    return _branch_off["depth"] == 0
+    """Branch streams in use: not inside branches_serial(), and not while side-stream weight
+    gradients are on -- the two overlap schemes are alternatives (a side fork from a branch
+    stream would be joined only into the first forking stream, leaving the branch un-joined,
+    which breaks hipGraph capture)."""
+    return _branch_off["depth"] == 0 and not _side["on"]
 
 
 def branch_stream(device, name="spatial"):

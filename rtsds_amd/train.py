@@ -12,7 +12,7 @@ import torch
 
 from . import functional as F
 from . import losses, utils
-from .runtime import branch_stream, branches_serial, dp_world
+from .runtime import branch_stream, branches_enabled, branches_serial, dp_world
 from .callbacks import Callback
 from .validation import val_GTA5
 
@@ -225,7 +225,7 @@ def _da_step_fused(generator, discriminator, generator_optimizer, discriminator_
     the separate softmax pass or the conv's channel-pad pass.  softmax(target_feature.detach())
     (train.py:256) equals the G-phase target probabilities, so they are computed once."""
     amb = torch.cuda.current_stream(main.device)
-    overlap = DA_OVERLAP and dp_world() <= 1
+    overlap = DA_OVERLAP and dp_world() <= 1 and branches_enabled()
     if overlap:
         # the target forward (G, resize + softmax, frozen D, loss) depends only on parameters
         # the source backward does not touch: it runs on a second stream, concurrently with
