@@ -48,6 +48,10 @@ CONV_CASES = [
     (1, 128, 9, 11, 19, 3, 1, 6, 6, True),     # ASPP-like, Cout=19
     (2, 19, 16, 16, 19, 1, 1, 0, 1, True),     # final 1x1 19->19
     (8, 256, 1, 1, 256, 1, 1, 0, 1, True),     # ARM 1x1 on pooled vectors
+    (8, 512, 1, 1, 512, 1, 1, 0, 1, True),     # pooled, vector kernels (16-B chunks, butterfly dgrad)
+    (5, 64, 1, 1, 40, 1, 1, 0, 1, True),       # pooled vector kernels: 5 rows, k < 64 lanes
+    (12, 256, 1, 1, 128, 1, 1, 0, 1, True),    # pooled: 12 rows (32-row vector fwd, scalar dgrad)
+    (2, 19, 1, 1, 19, 1, 1, 0, 1, True),       # pooled, C % 8 != 0: scalar kernels (FFM attention)
     (2, 1024, 8, 16, 19, 3, 1, 1, 1, False),   # FFM conv (K=9216, N=19)
     (2, 256, 8, 8, 512, 3, 2, 1, 1, False),    # layer4 conv1
     (1, 32, 13, 17, 64, 3, 2, 1, 1, False),    # stride-2 dgrad phases, odd sizes
@@ -500,12 +504,15 @@ def _upce_reference(heads, t, geo_args, ignore):
     (1, 19, 13, 17, {"size": (97, 129)}, 2),         # non-integer scale, ragged tiles
     (2, 5, 7, 9, {"scale_factor": 4}, 1),            # other factor, few classes
     (1, 19, 9, 33, {"size": (72, 264)}, 1),          # several column tiles
+    (2, 19, 8, 16, {"scale_factor": 8}, 2, 40.0),    # wide logit ranges (softmax shift, exp
+    (2, 19, 8, 16, {"scale_factor": 8}, 1, 12.0),    # underflow of the far classes)
 ])
 def test_upsample_cross_entropy_fused(case, dt):
     """Fused resize+CE+accuracy (rtsds_upce_*) vs torch fp64 interpolate -> CrossEntropyLoss."""
-    n, c, hl, wl, geo_args, k = case
+    n, c, hl, wl, geo_args, k = case[:6]
+    amp = case[6] if len(case) > 6 else 2.0
     g = torch.Generator().manual_seed(21)
-    heads = [torch.randn(n, c, hl, wl, generator=g, dtype=torch.float64) * 2 for _ in range(k)]
+    heads = [torch.randn(n, c, hl, wl, generator=g, dtype=torch.float64) * amp for _ in range(k)]
     if dt == torch.bfloat16:
         heads = [h.bfloat16().double() for h in heads]
     hd = [_dev(h, dt).requires_grad_() for h in heads]
