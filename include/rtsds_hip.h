@@ -35,8 +35,10 @@ enum {
 enum { RTSDS_ACT_NONE = 0, RTSDS_ACT_RELU = 1, RTSDS_ACT_LEAKY = 2, RTSDS_ACT_SIGMOID = 3 };
 #define RTSDS_ACCUMULATE 0x100 /* conv fwd flag: y += conv(...) (ASPP sum, deeplabv2.py:62-66) */
 /* conv fwd (act) / wgrad (accumulate) flag: x is already stored with the padded channel pitch
- * the GEMM gathers (19 -> 32 for the discriminator's class-probability input, written by
- * rtsds_upsoftmax_fwd) and zero in channels c..pitch-1: the internal pad pass is skipped.   */
+ * the GEMM gathers (rtsds_conv2d_input_pitch: 19 -> 32 for the discriminator's class-probability
+ * input, written by rtsds_upsoftmax_fwd; 3 -> 4 for the image of the stem / spatial-path convs,
+ * written by rtsds_nchw_to_nhwc_pad) and zero in channels c..pitch-1: the internal pad pass is
+ * skipped.  Rejected (RTSDS_ERR_UNSUPPORTED) where the pitch is c itself.                   */
 #define RTSDS_INPUT_PADDED 0x400
 
 typedef struct {
@@ -61,6 +63,8 @@ typedef struct {
  * by rtsds_bn_fwd(stats_part=...) -- the statistics pass over y is then skipped.
  * ws >= rtsds_conv2d_fwd_workspace(d) (non-zero only when Cin needs channel padding).   */
 size_t rtsds_conv2d_fwd_workspace(const rtsds_conv_desc* d);
+/* Channel pitch of x that the forward / weight-gradient gathers of d read (0: bad descriptor). */
+int rtsds_conv2d_input_pitch(const rtsds_conv_desc* d);
 int rtsds_conv2d_fwd_stats_tiles(const rtsds_conv_desc* d);
 int rtsds_conv2d_fwd(const rtsds_conv_desc* d, const void* x, const void* w, const float* bias,
                      void* y, int act, float* bn_stats, void* ws, size_t ws_bytes, void* stream);
@@ -167,6 +171,10 @@ int rtsds_bn_relu_maxpool_bwd(const void* dy_pool, const uint8_t* idx, const voi
  * copy_channels: torch.cat along channels and its backward split (build_bisenet.py:72,153);
  * accumulate != 0: dst += src (a split slice whose tensor also has another reader).      */
 int rtsds_nchw_to_nhwc(const float* x, void* y, int n, int c, int h, int w, int dtype, void* stream);
+/* Same, written with channel pitch `pitch` (channels c..pitch-1 zero; pitch 4): the 3-channel
+ * image batch in the layout rtsds_conv2d_input_pitch reports for the stem / spatial-path convs,
+ * passed to them with RTSDS_INPUT_PADDED (main.py:46-108 loaders -> model input).           */
+int rtsds_nchw_to_nhwc_pad(const float* x, void* y, int n, int c, int h, int w, int pitch, int dtype, void* stream);
 int rtsds_cast(const void* src, int src_dtype, void* dst, int dst_dtype, long n, void* stream);
 int rtsds_copy_channels(const void* src, int src_ld, int src_off, void* dst, int dst_ld, int dst_off,
                         long rows, int cnt, int accumulate, int dtype, void* stream);

@@ -33,6 +33,7 @@ P = c_void_p
 # name -> (restype, argtypes)
 SIGNATURES = {
     "rtsds_conv2d_fwd_workspace": (c_size_t, [ctypes.POINTER(ConvDesc)]),
+    "rtsds_conv2d_input_pitch": (c_int, [ctypes.POINTER(ConvDesc)]),
     "rtsds_conv2d_fwd_stats_tiles": (c_int, [ctypes.POINTER(ConvDesc)]),
     "rtsds_conv2d_fwd": (c_int, [ctypes.POINTER(ConvDesc), P, P, P, P, c_int, P, P, c_size_t, P]),
     "rtsds_conv2d_fwd_bn": (c_int, [ctypes.POINTER(ConvDesc), P, P, P, P, P, P, c_int, P, c_size_t, P]),
@@ -56,6 +57,7 @@ SIGNATURES = {
     "rtsds_bn_relu_maxpool_bwd": (c_int, [P, P, P, P, P, P] + [c_int] * 7 + [P, P, P, P, c_int, c_int, c_int, P,
                                                                             c_size_t, P]),
     "rtsds_nchw_to_nhwc": (c_int, [P, P, c_int, c_int, c_int, c_int, c_int, P]),
+    "rtsds_nchw_to_nhwc_pad": (c_int, [P, P, c_int, c_int, c_int, c_int, c_int, c_int, P]),
     "rtsds_cast": (c_int, [P, c_int, P, c_int, c_long, P]),
     "rtsds_copy_channels": (c_int, [P, c_int, c_int, P, c_int, c_int, c_long, c_int, c_int, c_int, P]),
     "rtsds_act_fwd": (c_int, [P, P, c_long, c_int, c_int, P]),
@@ -130,7 +132,7 @@ class _Lib:
 
         def call(*args):
             rc = fn(*args)
-            if name.endswith("_workspace") or name.endswith("_tiles"):
+            if name.endswith(("_workspace", "_tiles", "_pitch")):  # queries: the value itself
                 return rc
             if rc != 0:
                 raise RuntimeError(f"rtsds_amd: {name} failed: {ERRORS.get(rc, rc)}")

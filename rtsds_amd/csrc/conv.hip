@@ -1694,6 +1694,18 @@ extern "C" int rtsds_conv2d_fwd_stats_tiles(const rtsds_conv_desc* d) {
   return (int)((M + bm - 1) / bm);
 }
 
+// Channel pitch of x the forward / weight-gradient gathers read (RTSDS_INPUT_PADDED: the caller
+// hands x with this pitch, zero beyond c): 4 for the superpixel image convs, the vector-padded
+// channel count for the implicit GEMM, c itself for the pooled and halo paths.
+static int input_pitch(const rtsds_conv_desc* d) {
+  if (pooled_1x1(d) || hconv_ok(d)) return d->c;
+  if (sp_path(d)) return 4;
+  return pad_c(d->c, d->dtype);
+}
+extern "C" int rtsds_conv2d_input_pitch(const rtsds_conv_desc* d) {
+  return check_desc(d) ? 0 : input_pitch(d);
+}
+
 // FWD workspace: channel-padded copies of x and w when Cin is not a vector multiple.
 extern "C" size_t rtsds_conv2d_fwd_workspace(const rtsds_conv_desc* d) {
   if (pooled_1x1(d) || hconv_ok(d)) return 0;
@@ -1712,12 +1724,12 @@ static void fwd_prepare(const rtsds_conv_desc* d0, const void*& x, const void*& 
   if (sp_path(d0)) {
     void* x4 = ws;
     void* wp = (char*)ws + sp_x4_bytes(d0);
-    sp_pad4(d0, x, x4, st);
+    if (!x_padded) sp_pad4(d0, x, x4, st);
     const int n = d0->k * d0->kh * ((d0->kw + 1) / 2) * 8;
     hipLaunchKernelGGL(sp_repack_w_kernel, dim3(rt_cdiv(n, 256)), dim3(256), 0, st, (const bf16*)w, (bf16*)wp, d0->k,
                        d0->kh, d0->kw, (d0->kw + 1) / 2);
     d = sp_desc(d0);
-    x = x4;
+    if (!x_padded) x = x4;
     w = wp;
     return;
   }
@@ -1750,7 +1762,7 @@ extern "C" int rtsds_conv2d_fwd(const rtsds_conv_desc* d0, const void* x, const 
     return hipGetLastError() == hipSuccess ? RTSDS_OK : RTSDS_ERR_LAUNCH;
   }
   const bool x_padded = (act & RTSDS_INPUT_PADDED) != 0;
-  if (x_padded && (sp_path(d0) || hconv_ok(d0) || pad_c(d0->c, d0->dtype) == d0->c)) return RTSDS_ERR_UNSUPPORTED;
+  if (x_padded && input_pitch(d0) == d0->c) return RTSDS_ERR_UNSUPPORTED;
   if (hconv_ok(d0) && !(act & RTSDS_ACCUMULATE)) {
     if (bn_stats && (act & 0xff)) return RTSDS_ERR_UNSUPPORTED;
     hconv_fwd(d0, x, w, bias, nullptr, y, act & 0xff, bn_stats, st);
@@ -1781,13 +1793,15 @@ extern "C" int rtsds_conv2d_fwd_bn(const rtsds_conv_desc* d0, const void* x, con
   int e = check_desc(d0);
   if (e) return e;
   if (ws_bytes < rtsds_conv2d_fwd_workspace(d0)) return RTSDS_ERR_WORKSPACE;
+  const bool x_padded = (act & RTSDS_INPUT_PADDED) != 0;
+  if (x_padded && input_pitch(d0) == d0->c) return RTSDS_ERR_UNSUPPORTED;
   hipStream_t st = (hipStream_t)stream;
   if (hconv_ok(d0) && !res) {
     hconv_fwd(d0, x, w, shift, scale, y, act & 0xff, nullptr, st);
     return hipGetLastError() == hipSuccess ? RTSDS_OK : RTSDS_ERR_LAUNCH;
   }
   rtsds_conv_desc d;
-  fwd_prepare(d0, x, w, ws, d, st);
+  fwd_prepare(d0, x, w, ws, d, st, x_padded);
   ConvArgs p = make_args(&d);
   p.a = x; p.b = w; p.bias = shift; p.scale = scale; p.res = res; p.out = y;
   p.act = act & 0xff;
@@ -2132,7 +2146,7 @@ extern "C" int rtsds_conv2d_wgrad(const rtsds_conv_desc* d0, const void* x, cons
   if (e) return e;
   const bool x_padded = (accumulate & RTSDS_INPUT_PADDED) != 0;
   accumulate &= ~RTSDS_INPUT_PADDED;
-  if (x_padded && (sp_path(d0) || pooled_1x1(d0) || pad_c(d0->c, d0->dtype) == d0->c)) return RTSDS_ERR_UNSUPPORTED;
+  if (x_padded && (pooled_1x1(d0) || (!sp_path(d0) && pad_c(d0->c, d0->dtype) == d0->c))) return RTSDS_ERR_UNSUPPORTED;
   if (ws_bytes < rtsds_conv2d_wgrad_workspace(d0)) return RTSDS_ERR_WORKSPACE;
   hipStream_t st = (hipStream_t)stream;
   if (pooled_1x1(d0)) {
@@ -2154,8 +2168,10 @@ extern "C" int rtsds_conv2d_wgrad(const rtsds_conv_desc* d0, const void* x, cons
   if (sp) {
     void* x4 = (char*)part + pl.colsum_bytes;
     dws = (float*)((char*)x4 + sp_x4_bytes(d0));
-    sp_pad4(d0, x, x4, st);
-    x = x4;
+    if (!x_padded) {  // RTSDS_INPUT_PADDED: x already is the 4-channel superpixel image
+      sp_pad4(d0, x, x4, st);
+      x = x4;
+    }
   }
   if (pl.kp != d.k) {
     pad_any(d.dtype, dy, dyp, R, d.k, pl.kp, st);

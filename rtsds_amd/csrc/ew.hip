@@ -46,6 +46,33 @@ extern "C" int rtsds_nchw_to_nhwc(const float* x, void* y, int n, int c, int h, 
   RET_LAUNCH();
 }
 
+// NCHW fp32 -> NHWC T with channel pitch cp >= c, channels c..cp-1 zero: the image batch in
+// the layout its convs gather (3 -> 4 channels: the superpixel view of the stem / spatial-path
+// convs, conv.hip sp_path), so they skip their own pad pass.  One thread per pixel.
+template <typename T, int CP>
+__global__ void nchw_to_nhwc_pad_kernel(const float* __restrict__ x, T* __restrict__ y, int c, long hw, long pixels) {
+  GRID_STRIDE(p, pixels) {
+    const long img = p / hw, s = p - img * hw;
+    T v[CP];
+#pragma unroll
+    for (int ch = 0; ch < CP; ++ch) v[ch] = from_f<T>(ch < c ? x[(img * c + ch) * hw + s] : 0.f);
+    if constexpr (CP * sizeof(T) == 8) {
+      typedef __attribute__((ext_vector_type(2))) unsigned u32x2;
+      *(u32x2*)(y + p * CP) = __builtin_bit_cast(u32x2, v);
+    } else {
+#pragma unroll
+      for (int ch = 0; ch < CP; ++ch) y[p * CP + ch] = v[ch];
+    }
+  }
+}
+extern "C" int rtsds_nchw_to_nhwc_pad(const float* x, void* y, int n, int c, int h, int w, int pitch, int dtype, void* stream) {
+  const long px = (long)n * h * w;
+  if (px <= 0 || c <= 0 || pitch != 4 || c > pitch) return RTSDS_ERR_UNSUPPORTED;
+  DISPATCH_T(dtype, hipLaunchKernelGGL((nchw_to_nhwc_pad_kernel<T, 4>), dim3(ew_blocks(px)), dim3(256), 0, (hipStream_t)stream, x,
+                                       (T*)y, c, (long)h * w, px));
+  RET_LAUNCH();
+}
+
 // dst (dtype_dst) = src (dtype_src), elementwise.
 template <typename S, typename D>
 __global__ void cast_kernel(const S* __restrict__ s, D* __restrict__ d, long n) {

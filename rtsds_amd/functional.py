@@ -79,12 +79,15 @@ def _conv_desc(x, k, kh, kw, stride, padding, dilation):
     return d
 
 
-def is_padded_input(x):
-    """A class-probability tensor written with the padded channel pitch the conv gathers
-    (upsample_softmax): [N, C, H, W] view of an NHWC [N, H, W, Cp] buffer, zero in C..Cp-1."""
+def is_padded_input(x, d=None):
+    """A tensor written with the padded channel pitch a conv gathers (upsample_softmax's class
+    probabilities, pitch 32; pack_input's 3-channel images, pitch 4): [N, C, H, W] view of an
+    NHWC [N, H, W, Cp] buffer, zero in C..Cp-1.  With a conv descriptor ``d``: and Cp is the
+    pitch that conv reads (rtsds_conv2d_input_pitch)."""
     cp = getattr(x, "_rt_cpad", None)
-    return cp is not None and x.dim() == 4 and x.stride(1) == 1 and x.stride(3) == cp and \
+    ok = cp is not None and x.dim() == 4 and x.stride(1) == 1 and x.stride(3) == cp and \
         x.stride(2) == cp * x.shape[3] and x.stride(0) == cp * x.shape[2] * x.shape[3]
+    return ok and (d is None or lib.rtsds_conv2d_input_pitch(ctypes.byref(d)) == cp)
 
 
 def detach_padded(x):
@@ -143,10 +146,10 @@ class ConvFn(torch.autograd.Function):
         conv's own ``act``, so the backward takes dy as the pre-activation gradient.  Set only
         by modules whose intermediate activations have exactly one reader (discriminators)."""
         require_hip(x, weight)
-        padded = is_padded_input(x)
+        k, _, kh, kw = weight.shape
+        padded = hasattr(x, "_rt_cpad") and is_padded_input(x, _conv_desc(x, k, kh, kw, stride, padding, dilation))
         if not padded:
             x = nhwc(x)
-        k, _, kh, kw = weight.shape
         d = _conv_desc(x, k, kh, kw, stride, padding, dilation)
         y = empty_nhwc(d.n, k, d.ho, d.wo, x.dtype, x.device)
         ws = workspace(lib.rtsds_conv2d_fwd_workspace(ctypes.byref(d)), x.device)
@@ -262,8 +265,11 @@ def conv_bn_eval(x, weight, bias, wq, stride, padding, dilation, gamma, beta, ru
     epilogue (rtsds_bn_fold + rtsds_conv2d_fwd_bn).  Same function as the unfused
     conv2d -> batch_norm(training=False) chain, with the BN applied to the fp32 accumulators."""
     require_hip(x, weight)
-    x = nhwc(x)
     k, _, kh, kw = weight.shape
+    flag = INPUT_PADDED if hasattr(x, "_rt_cpad") and \
+        is_padded_input(x, _conv_desc(x, k, kh, kw, stride, padding, dilation)) else 0
+    if not flag:
+        x = nhwc(x)
     d = _conv_desc(x, k, kh, kw, stride, padding, dilation)
     ss = torch.empty(2 * k, dtype=torch.float32, device=x.device)
     lib.rtsds_bn_fold(_P(gamma), _P(beta), _P(running_mean), _P(running_var), _P(bias), float(eps), k,
@@ -276,7 +282,7 @@ def conv_bn_eval(x, weight, bias, wq, stride, padding, dilation, gamma, beta, ru
     ws = workspace(lib.rtsds_conv2d_fwd_workspace(ctypes.byref(d)), x.device)
     with _Timed(d, "fwd"):
         lib.rtsds_conv2d_fwd_bn(ctypes.byref(d), _P(x), _P(wq), _P(ss), ss.data_ptr() + 4 * k, _P(residual), _P(y),
-                                act, _P(ws), ws.numel(), stream())
+                                act | flag, _P(ws), ws.numel(), stream())
     return y
 
 
@@ -472,6 +478,15 @@ def _pack(x, dtype):
     xf = x if x.dtype == torch.float32 else cast(x, torch.float32)
     xf = xf.contiguous()
     n, c, h, w = xf.shape
+    if c == 3 and dtype == torch.bfloat16:
+        # the image in the 4-channel pitch of its convs' superpixel gathers (stem / spatial
+        # path, RTSDS_INPUT_PADDED): they skip their own pad pass; other readers see a
+        # [N, 3, H, W] tensor (non-conv readers make an NHWC copy via nhwc())
+        buf = torch.empty((n, h, w, 4), dtype=dtype, device=x.device)
+        lib.rtsds_nchw_to_nhwc_pad(_P(xf), _P(buf), n, c, h, w, 4, 1, stream())
+        y = buf.permute(0, 3, 1, 2)[:, :3]
+        y._rt_cpad = 4
+        return y
     y = empty_nhwc(n, c, h, w, dtype, x.device)
     lib.rtsds_nchw_to_nhwc(_P(xf), _P(y), n, c, h, w, 0 if dtype == torch.float32 else 1, stream())
     return y

@@ -722,3 +722,35 @@ def test_upsample_softmax_fused(dt, geo):
     y2.backward(_dev(gy, dt))
     assert torch.equal(y.detach().float(), y2.detach().float())
     assert torch.equal(xd.grad, x2.grad)
+
+
+@pytest.mark.parametrize("kh,pad", [(7, 3), (3, 1)])
+def test_padded_image_input_bit_identical(kh, pad):
+    """pack_input writes a 3-channel bf16 image with the 4-channel pitch of the superpixel
+    stem / spatial-path convs (RTSDS_INPUT_PADDED, no pad pass): forward, weight gradient and
+    the eval-mode folded conv equal the same convs on an ordinary NHWC copy bit for bit."""
+    g = torch.Generator().manual_seed(17)
+    x = torch.randn(2, 3, 64, 96, generator=g) * 50
+    xp = F.pack_input(x.to(DEV), torch.bfloat16)
+    assert F.is_padded_input(xp) and xp.shape == (2, 3, 64, 96) and xp._rt_cpad == 4
+    xu = xp.contiguous(memory_format=CL)
+    assert not F.is_padded_input(xu)
+    assert torch.equal(xu.float().cpu(), x.bfloat16().float())
+    wt = torch.randn(64, 3, kh, kh, generator=g) / (3 * kh * kh) ** 0.5
+    gy = None
+    outs = []
+    for xi in (xp, xu):
+        wp = torch.nn.Parameter(wt.to(DEV).contiguous(memory_format=CL))
+        y = F.conv2d(xi, wp, None, _shadow(wp, torch.bfloat16), (2, 2), (pad, pad), (1, 1), 0)
+        if gy is None:
+            gy = torch.randn(y.shape, generator=g).to(DEV, torch.bfloat16).contiguous(memory_format=CL)
+        y.backward(gy)
+        with torch.no_grad():
+            k = 64
+            ye = F.conv_bn_eval(xi, wp.detach(), None, _shadow(wp.detach(), torch.bfloat16), (2, 2), (pad, pad),
+                                (1, 1), torch.ones(k, device=DEV), torch.zeros(k, device=DEV),
+                                torch.zeros(k, device=DEV), torch.ones(k, device=DEV), 1e-5, 1)
+        torch.cuda.synchronize()
+        outs.append((y.detach().float().cpu(), wp.grad.float().cpu(), ye.float().cpu()))
+    for a, b in zip(outs[0], outs[1]):
+        assert torch.equal(a, b)
