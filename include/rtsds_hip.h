@@ -40,6 +40,10 @@ enum { RTSDS_ACT_NONE = 0, RTSDS_ACT_RELU = 1, RTSDS_ACT_LEAKY = 2, RTSDS_ACT_SI
  * written by rtsds_nchw_to_nhwc_pad) and zero in channels c..pitch-1: the internal pad pass is
  * skipped.  Rejected (RTSDS_ERR_UNSUPPORTED) where the pitch is c itself.                   */
 #define RTSDS_INPUT_PADDED 0x400
+/* conv dgrad flag (rtsds_conv2d_dgrad: accumulate; _act / _bnstats: act): w is the packed
+ * copy rtsds_conv2d_dgrad_pack_many wrote for this descriptor, not the [Cout][KH][KW][Cin]
+ * weight -- the per-call repack is skipped.                                                 */
+#define RTSDS_WEIGHT_PACKED 0x800
 
 typedef struct {
   int n, h, w, c;   /* input  [n][h][w][c]                                     */
@@ -78,6 +82,13 @@ int rtsds_conv2d_fwd_bn(const rtsds_conv_desc* d, const void* x, const void* w, 
 /* dx (+)= conv_transpose(dy, w) (accumulate != 0: dx += ...).  Needs ws >=
  * rtsds_conv2d_dgrad_workspace(d).  Strides 1 and 2 only.                               */
 size_t rtsds_conv2d_dgrad_workspace(const rtsds_conv_desc* d);
+/* Pre-packed data-gradient weights: bytes of d's packed copy (0: its route reads w as is --
+ * pooled / narrow 1x1 -- and takes no RTSDS_WEIGHT_PACKED); pack_many writes the packed copies
+ * wt[i] of count convs (descs[i], weights w[i] in [Cout][KH][KW][Cin]) in one launch per 16
+ * segments -- the optimizer's per-step refresh after its update (optim.py).                 */
+size_t rtsds_conv2d_dgrad_pack_bytes(const rtsds_conv_desc* d);
+int rtsds_conv2d_dgrad_pack_many(int count, const rtsds_conv_desc* descs, const void* const* w, void* const* wt,
+                                 void* stream);
 int rtsds_conv2d_dgrad(const rtsds_conv_desc* d, const void* dy, const void* w, void* dx,
                        int accumulate, void* ws, size_t ws_bytes, void* stream);
 /* dx = conv_transpose(dy, w) * act'(x_act): the data gradient of this conv followed by the

@@ -18,6 +18,7 @@ F32, BF16 = 0, 1
 ACT_NONE, ACT_RELU, ACT_LEAKY, ACT_SIGMOID = 0, 1, 2, 3
 ACCUMULATE = 0x100
 INPUT_PADDED = 0x400
+WEIGHT_PACKED = 0x800
 ERRORS = {1: "bad shape", 2: "unsupported configuration", 3: "HIP launch failure", 4: "workspace too small"}
 
 c_int, c_long, c_float, c_size_t, c_void_p = (ctypes.c_int, ctypes.c_long, ctypes.c_float,
@@ -38,6 +39,8 @@ SIGNATURES = {
     "rtsds_conv2d_fwd": (c_int, [ctypes.POINTER(ConvDesc), P, P, P, P, c_int, P, P, c_size_t, P]),
     "rtsds_conv2d_fwd_bn": (c_int, [ctypes.POINTER(ConvDesc), P, P, P, P, P, P, c_int, P, c_size_t, P]),
     "rtsds_conv2d_dgrad_workspace": (c_size_t, [ctypes.POINTER(ConvDesc)]),
+    "rtsds_conv2d_dgrad_pack_bytes": (c_size_t, [ctypes.POINTER(ConvDesc)]),
+    "rtsds_conv2d_dgrad_pack_many": (c_int, [c_int, ctypes.POINTER(ConvDesc), P, P, P]),
     "rtsds_conv2d_dgrad": (c_int, [ctypes.POINTER(ConvDesc), P, P, P, c_int, P, c_size_t, P]),
     "rtsds_conv2d_dgrad_act": (c_int, [ctypes.POINTER(ConvDesc), P, P, P, P, c_int, P, c_size_t, P]),
     "rtsds_conv2d_dgrad_bnstats_tiles": (c_int, [ctypes.POINTER(ConvDesc)]),
@@ -132,7 +135,7 @@ class _Lib:
 
         def call(*args):
             rc = fn(*args)
-            if name.endswith(("_workspace", "_tiles", "_pitch")):  # queries: the value itself
+            if name.endswith(("_workspace", "_tiles", "_pitch", "_bytes")):  # queries: the value itself
                 return rc
             if rc != 0:
                 raise RuntimeError(f"rtsds_amd: {name} failed: {ERRORS.get(rc, rc)}")

@@ -1906,6 +1906,116 @@ static void phase_taps(int a, int pad, int dil, int ksz, int size, int& off, int
   else { r0 = 0; rstep = 1; tk = a == 0 ? ksz : 0; }
 }
 
+// ---- pre-packed DGRAD weights.  Every GEMM / halo DGRAD route reads the weights transposed
+// ([ci][tap][co_p], taps flipped for the halo conv, split per parity phase at stride 2).  The
+// optimizer re-packs every conv weight it owns right after its update, all of them in one
+// launch (rtsds_conv2d_dgrad_pack_many), and the backward passes the packed copy with
+// RTSDS_WEIGHT_PACKED instead of repacking per call (one tiny launch per conv and backward).
+struct PackSeg {
+  const void* w;
+  void* wt;  // segment base (phase offset applied)
+  int co_n, co_p, kh, kw, ci_n, tkh, tkw, r0h, r0w, rstep, blk0;
+};
+static const int kPackSegs = 16, kPackPer = 8;
+struct PackBatch {
+  PackSeg s[kPackSegs];
+  int nseg;
+};
+template <typename T>
+__global__ void __launch_bounds__(256) dgrad_pack_kernel(const PackBatch b) {
+  int si = 0;
+  for (int i = 1; i < b.nseg; ++i)
+    if (b.s[i].blk0 <= (int)blockIdx.x) si = i;
+  const PackSeg& g = b.s[si];
+  const int taps = g.tkh * g.tkw, total = g.co_p * taps * g.ci_n;
+  const T* __restrict__ w = (const T*)g.w;
+  T* __restrict__ wt = (T*)g.wt;
+  const int i0 = ((int)blockIdx.x - g.blk0) * 256 * kPackPer + threadIdx.x;
+#pragma unroll
+  for (int e = 0; e < kPackPer; ++e) {
+    const int i = i0 + e * 256;
+    if (i >= total) break;
+    const int co = i % g.co_p, rest = i / g.co_p;
+    const int tap = rest % taps, ci = rest / taps;
+    const int r = g.r0h + (tap / g.tkw) * g.rstep, sc = g.r0w + (tap % g.tkw) * g.rstep;
+    wt[i] = co < g.co_n ? w[((co * g.kh + r) * g.kw + sc) * g.ci_n + ci] : (T)0.0f;
+  }
+}
+static bool dgrad_hconv(const rtsds_conv_desc* d, int kp);
+// Segments of d's DGRAD weight repack (the layout dgrad_impl reads); 0 = no repack on its route.
+static int dgrad_pack_plan(const rtsds_conv_desc* d, PackSeg* seg, int& kp) {
+  kp = pad_c(d->k, d->dtype);
+  if (pooled_1x1(d) || pw_ok(d)) return 0;
+  auto one = [&](int tkh, int tkw, int r0h, int r0w, int rstep, long boff) {
+    PackSeg q = {};
+    q.co_n = d->k; q.co_p = kp; q.kh = d->kh; q.kw = d->kw; q.ci_n = d->c;
+    q.tkh = tkh; q.tkw = tkw; q.r0h = r0h; q.r0w = r0w; q.rstep = rstep;
+    q.wt = (void*)(intptr_t)boff;  // element offset until the caller adds the base
+    return q;
+  };
+  if (dgrad_hconv(d, kp)) {
+    seg[0] = one(d->kh, d->kw, d->kh - 1, d->kw - 1, -1, 0);
+    return 1;
+  }
+  if (d->sh == 2 && d->sw == 2) {
+    int n = 0;
+    long boff = 0;
+    for (int a = 0; a < 2; ++a)
+      for (int b = 0; b < 2; ++b) {
+        int offh, hp, r0h, rsh, tkh, offw, wp, r0w, rsw, tkw;
+        phase_taps(a, d->ph, d->dh, d->kh, d->h, offh, hp, r0h, rsh, tkh);
+        phase_taps(b, d->pw, d->dw, d->kw, d->w, offw, wp, r0w, rsw, tkw);
+        if (hp == 0 || wp == 0) continue;
+        if (tkh * tkw > 0) seg[n++] = one(tkh, tkw, r0h, r0w, rsh, boff);
+        boff += (long)tkh * tkw * kp * d->c;
+      }
+    return n;
+  }
+  if (d->sh != 1 || d->sw != 1) return 0;
+  seg[0] = one(d->kh, d->kw, 0, 0, 1, 0);
+  return 1;
+}
+extern "C" size_t rtsds_conv2d_dgrad_pack_bytes(const rtsds_conv_desc* d) {
+  if (check_desc(d)) return 0;
+  PackSeg seg[4];
+  int kp;
+  if (dgrad_pack_plan(d, seg, kp) == 0) return 0;
+  return al256((size_t)kp * d->kh * d->kw * d->c * esize(d->dtype));
+}
+extern "C" int rtsds_conv2d_dgrad_pack_many(int count, const rtsds_conv_desc* descs, const void* const* w, void* const* wt,
+                                            void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  PackBatch b = {};
+  int blocks = 0, dtype = -1;
+  auto flush = [&]() {
+    if (b.nseg == 0) return;
+    if (dtype == RTSDS_BF16) hipLaunchKernelGGL(dgrad_pack_kernel<bf16>, dim3(blocks), dim3(256), 0, st, b);
+    else hipLaunchKernelGGL(dgrad_pack_kernel<float>, dim3(blocks), dim3(256), 0, st, b);
+    b.nseg = 0;
+    blocks = 0;
+  };
+  for (int i = 0; i < count; ++i) {
+    const rtsds_conv_desc* d = descs + i;
+    if (check_desc(d) || !w[i] || !wt[i]) return RTSDS_ERR_SHAPE;
+    PackSeg seg[4];
+    int kp;
+    const int n = dgrad_pack_plan(d, seg, kp);
+    if (n == 0) return RTSDS_ERR_UNSUPPORTED;
+    if (d->dtype != dtype || b.nseg + n > kPackSegs) flush();
+    dtype = d->dtype;
+    for (int j = 0; j < n; ++j) {
+      PackSeg q = seg[j];
+      q.w = w[i];
+      q.wt = (char*)wt[i] + (intptr_t)q.wt * esize(d->dtype);
+      q.blk0 = blocks;
+      blocks += rt_cdiv(q.co_p * q.tkh * q.tkw * q.ci_n, 256 * kPackPer);
+      b.s[b.nseg++] = q;
+    }
+  }
+  flush();
+  return hipGetLastError() == hipSuccess ? RTSDS_OK : RTSDS_ERR_LAUNCH;
+}
+
 // mask: see ConvArgs::mask.  Paths whose epilogue does not apply it (pooled, narrow 1x1, halo,
 // split-K) report false and the caller masks dx in place afterwards.
 struct BnbArgs {  // see ConvArgs::bnb_part
@@ -1915,11 +2025,14 @@ struct BnbArgs {  // see ConvArgs::bnb_part
   int act;
 };
 static int dgrad_impl(const rtsds_conv_desc* d0, const void* dy, const void* w, void* dx, int accumulate, const void* mask,
-                      int mask_act, bool& masked, void* ws, size_t ws_bytes, void* stream, const BnbArgs* bnb = nullptr);
+                      int mask_act, bool& masked, void* ws, size_t ws_bytes, void* stream, const BnbArgs* bnb = nullptr,
+                      bool packed = false);
 extern "C" int rtsds_conv2d_dgrad(const rtsds_conv_desc* d0, const void* dy, const void* w, void* dx,
                                   int accumulate, void* ws, size_t ws_bytes, void* stream) {
   bool masked = false;
-  return dgrad_impl(d0, dy, w, dx, accumulate, nullptr, 0, masked, ws, ws_bytes, stream);
+  const bool packed = (accumulate & RTSDS_WEIGHT_PACKED) != 0;
+  return dgrad_impl(d0, dy, w, dx, accumulate & ~RTSDS_WEIGHT_PACKED, nullptr, 0, masked, ws, ws_bytes, stream, nullptr,
+                    packed);
 }
 static bool dgrad_hconv(const rtsds_conv_desc* d, int kp);
 static DgradSplit dgrad_split(const rtsds_conv_desc* d, int kp);
@@ -1941,24 +2054,28 @@ extern "C" int rtsds_conv2d_dgrad_bnstats(const rtsds_conv_desc* d0, const void*
                                           const float* gamma, const float* beta, const float* save_mean,
                                           const float* save_invstd, int act, float* part, void* ws, size_t ws_bytes,
                                           void* stream) {
+  const bool packed = (act & RTSDS_WEIGHT_PACKED) != 0;
+  act &= ~RTSDS_WEIGHT_PACKED;
   if (rtsds_conv2d_dgrad_bnstats_tiles(d0) == 0) return RTSDS_ERR_UNSUPPORTED;
   if (!bn_x || !save_mean || !save_invstd || !part || (act != RTSDS_ACT_NONE && act != RTSDS_ACT_RELU && act != RTSDS_ACT_LEAKY))
     return RTSDS_ERR_UNSUPPORTED;
   const BnbArgs b = {part, bn_x, gamma, beta, save_mean, save_invstd, act};
   bool masked = false;
-  return dgrad_impl(d0, dy, w, dx, 0, nullptr, 0, masked, ws, ws_bytes, stream, &b);
+  return dgrad_impl(d0, dy, w, dx, 0, nullptr, 0, masked, ws, ws_bytes, stream, &b, packed);
 }
 extern "C" int rtsds_act_bwd(const void* dy, const void* y, void* dx, long n, int act, float alpha, int dtype, void* stream);
 extern "C" int rtsds_conv2d_dgrad_act(const rtsds_conv_desc* d0, const void* dy, const void* w, void* dx, const void* x_act,
                                       int act, void* ws, size_t ws_bytes, void* stream) {
+  const bool packed = (act & RTSDS_WEIGHT_PACKED) != 0;
+  act &= ~RTSDS_WEIGHT_PACKED;
   if (!x_act || (act != RTSDS_ACT_RELU && act != RTSDS_ACT_LEAKY)) return RTSDS_ERR_UNSUPPORTED;
   bool masked = false;
-  const int e = dgrad_impl(d0, dy, w, dx, 0, x_act, act, masked, ws, ws_bytes, stream);
+  const int e = dgrad_impl(d0, dy, w, dx, 0, x_act, act, masked, ws, ws_bytes, stream, nullptr, packed);
   if (e || masked) return e;
   return rtsds_act_bwd(dx, x_act, dx, (long)d0->n * d0->h * d0->w * d0->c, act, 1.f, d0->dtype, stream);
 }
 static int dgrad_impl(const rtsds_conv_desc* d0, const void* dy, const void* w, void* dx, int accumulate, const void* mask,
-                      int mask_act, bool& masked, void* ws, size_t ws_bytes, void* stream, const BnbArgs* bnb) {
+                      int mask_act, bool& masked, void* ws, size_t ws_bytes, void* stream, const BnbArgs* bnb, bool packed) {
   masked = false;
   int e = check_desc(d0);
   if (e) return e;
@@ -1977,7 +2094,8 @@ static int dgrad_impl(const rtsds_conv_desc* d0, const void* dy, const void* w, 
   rtsds_conv_desc d = *d0;
   const int kp = pad_c(d.k, d.dtype);
   const size_t es = esize(d.dtype);
-  void* wt = ws;
+  // packed: w already is the transposed copy (rtsds_conv2d_dgrad_pack_many); else repack it here
+  void* wt = packed ? const_cast<void*>(w) : ws;
   if (kp != d.k) {
     void* dyp = (char*)ws + al256((size_t)kp * d.kh * d.kw * d.c * es);
     pad_any(d.dtype, dy, dyp, (long)d.n * d.ho * d.wo, d.k, kp, st);
@@ -1987,7 +2105,7 @@ static int dgrad_impl(const rtsds_conv_desc* d0, const void* dy, const void* w, 
   d.k = kp;
   if (dgrad_hconv(d0, kp)) {
     // narrow-output 3x3 conv: halo direct conv over dY with the flipped, transposed weights
-    repack_launch(d.dtype, w, wt, k_real, kp, d.kh, d.kw, d.c, d.kh, d.kw, d.kh - 1, d.kw - 1, -1, st);
+    if (!packed) repack_launch(d.dtype, w, wt, k_real, kp, d.kh, d.kw, d.c, d.kh, d.kw, d.kh - 1, d.kw - 1, -1, st);
     hconv_dgrad(d0, dy, kp, wt, dx, accumulate, st);
     return hipGetLastError() == hipSuccess ? RTSDS_OK : RTSDS_ERR_LAUNCH;
   }
@@ -2028,7 +2146,7 @@ static int dgrad_impl(const rtsds_conv_desc* d0, const void* dy, const void* w, 
         ++nph;
       }
     if (nph == 0) return RTSDS_OK;
-    if (max_w > 0) {
+    if (max_w > 0 && !packed) {
       const dim3 g(std::min(4096, (max_w + 255) / 256), nph);
       if (d.dtype == RTSDS_BF16)
         hipLaunchKernelGGL(repack_phases_kernel<bf16>, g, dim3(256), 0, st, (const bf16*)w, (bf16*)wt, k_real, kp, d.kh, d.kw,
@@ -2047,7 +2165,7 @@ static int dgrad_impl(const rtsds_conv_desc* d0, const void* dy, const void* w, 
     if (d.dtype == RTSDS_BF16) dispatch_align<bf16, MODE_DGRAD>(p, kp, st);
     else dispatch_align<float, MODE_DGRAD>(p, kp, st);
   } else {
-    repack_launch(d.dtype, w, wt, k_real, kp, d.kh, d.kw, d.c, d.kh, d.kw, 0, 0, 1, st);
+    if (!packed) repack_launch(d.dtype, w, wt, k_real, kp, d.kh, d.kw, d.c, d.kh, d.kw, 0, 0, 1, st);
     ConvArgs p = make_args(&d);
     p.a = dy; p.b = wt; p.bias = nullptr; p.out = dx; p.act = 0;
     p.accum = accumulate ? 1 : 0;

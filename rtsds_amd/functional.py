@@ -10,7 +10,7 @@ import ctypes
 import numpy as np
 import torch
 
-from ._lib import ACT_RELU, ACT_SIGMOID, INPUT_PADDED, ConvDesc, lib
+from ._lib import ACT_RELU, ACT_SIGMOID, INPUT_PADDED, WEIGHT_PACKED, ConvDesc, lib
 from .runtime import (CL, collective, dcode, dp_world, empty_nhwc, nhwc, require_hip, side_enabled, side_fork,
                       stream, workspace)
 
@@ -96,6 +96,53 @@ def detach_padded(x):
     if getattr(x, "_rt_cpad", None) is not None:
         y._rt_cpad = x._rt_cpad
     return y
+
+
+# ----------------------------------------------------------------------------- packed dgrad weights
+# The data-gradient GEMMs read each conv weight transposed ([ci][tap][co], flipped / split per
+# stride-2 phase by route).  For weights owned by an rtsds optimizer the transposed copy is
+# refreshed by the optimizer right after its update -- every registered conv in one launch
+# (optim._Arena.repack -> rtsds_conv2d_dgrad_pack_many) -- and the backward passes it with
+# RTSDS_WEIGHT_PACKED instead of repacking per call.  A conv registers on its first backward;
+# the copy is used once the optimizer has packed it from the current bf16 shadow.
+_DPACK = {"on": True}
+
+
+def set_dgrad_packs(on):
+    """Use optimizer-maintained packed dgrad weights (default on; off: repack per call)."""
+    _DPACK["on"] = bool(on)
+
+
+class _DPack:
+    __slots__ = ("arena", "key", "desc", "buf", "valid")
+
+
+def _desc_key(d):
+    return tuple(getattr(d, f) for f, _ in ConvDesc._fields_)
+
+
+def _dgrad_weight(weight, wq, d):
+    """(weight operand, flag) for a data-gradient launch of ``weight`` with descriptor ``d``."""
+    if not _DPACK["on"] or wq.dtype != torch.bfloat16 or weight is None:
+        return wq, 0
+    ref = getattr(weight, "_rt_arena", None)
+    if ref is None:
+        return wq, 0
+    pk = getattr(weight, "_rt_dpack", None)
+    if pk is not None and pk.arena is ref[0]:
+        if pk.key == _desc_key(d) and pk.buf is not None and pk.valid is not None and \
+                pk.valid == getattr(weight, "_rt_shadow_key", None) and wq is getattr(weight, "_rt_shadow", None):
+            return pk.buf, WEIGHT_PACKED
+        return wq, 0
+    pk = _DPack()
+    pk.arena, pk.key, pk.valid = ref[0], _desc_key(d), None
+    pk.desc = ConvDesc(*pk.key)
+    nb = lib.rtsds_conv2d_dgrad_pack_bytes(ctypes.byref(d))
+    pk.buf = torch.empty(nb // 2, dtype=torch.bfloat16, device=wq.device) if nb else None
+    weight._rt_dpack = pk
+    if nb:
+        ref[0].dpacks.append(weight)
+    return wq, 0
 
 
 class GradJoin:
@@ -199,6 +246,7 @@ class ConvFn(torch.autograd.Function):
             dx = join.buf if acc else empty_nhwc(d.n, d.c, d.h, d.w, x.dtype, x.device)
             ws = workspace(lib.rtsds_conv2d_dgrad_workspace(ctypes.byref(d)), x.device)
             link = ctx.bn_link
+            wd, wpk = _dgrad_weight(ctx.params[0], wq, d)
             tiles = 0
             if link is not None and link.src is not None and not acc and g.dtype == torch.bfloat16:
                 tiles = lib.rtsds_conv2d_dgrad_bnstats_tiles(ctypes.byref(d))
@@ -206,14 +254,14 @@ class ConvFn(torch.autograd.Function):
                 if tiles:
                     bx, bsm, bsi, bg, bb, bact = link.src
                     part = torch.empty(d.c * tiles * 2, dtype=torch.float32, device=x.device)
-                    lib.rtsds_conv2d_dgrad_bnstats(ctypes.byref(d), _P(g), _P(wq), _P(dx), _P(bx), _P(bg), _P(bb),
-                                                   _P(bsm), _P(bsi), bact, _P(part), _P(ws), ws.numel(), stream())
+                    lib.rtsds_conv2d_dgrad_bnstats(ctypes.byref(d), _P(g), _P(wd), _P(dx), _P(bx), _P(bg), _P(bb),
+                                                   _P(bsm), _P(bsi), bact | wpk, _P(part), _P(ws), ws.numel(), stream())
                     link.part, link.nrb = part, tiles
                 elif ctx.in_act:
-                    lib.rtsds_conv2d_dgrad_act(ctypes.byref(d), _P(g), _P(wq), _P(dx), _P(x), ctx.in_act, _P(ws),
-                                               ws.numel(), stream())
+                    lib.rtsds_conv2d_dgrad_act(ctypes.byref(d), _P(g), _P(wd), _P(dx), _P(x), ctx.in_act | wpk,
+                                               _P(ws), ws.numel(), stream())
                 else:
-                    lib.rtsds_conv2d_dgrad(ctypes.byref(d), _P(g), _P(wq), _P(dx), 1 if acc else 0, _P(ws),
+                    lib.rtsds_conv2d_dgrad(ctypes.byref(d), _P(g), _P(wd), _P(dx), (1 if acc else 0) | wpk, _P(ws),
                                            ws.numel(), stream())
             if join is not None:
                 dx = join.put(dx)
@@ -327,8 +375,9 @@ class ConvSumFn(torch.autograd.Function):
                 if dx is None:
                     dx = empty_nhwc(d.n, d.c, d.h, d.w, x.dtype, x.device)
                 ws = workspace(lib.rtsds_conv2d_dgrad_workspace(ctypes.byref(d)), x.device)
+                wd, wpk = _dgrad_weight(ctx.params[i], wqs[i], d)
                 with _Timed(d, "dgrad"):
-                    lib.rtsds_conv2d_dgrad(ctypes.byref(d), _P(dy), _P(wqs[i]), _P(dx), 1 if i else 0,
+                    lib.rtsds_conv2d_dgrad(ctypes.byref(d), _P(dy), _P(wd), _P(dx), (1 if i else 0) | wpk,
                                            _P(ws), ws.numel(), stream())
             if ctx.needs_input_grad[2 + i] or ctx.needs_input_grad[2 + m + i]:
                 w_i, b_i = ctx.params[i], ctx.params[m + i]

@@ -19,12 +19,13 @@ gradient, per-parameter step counts, parameters whose gradient was not produced 
 are skipped (tracked with post-accumulate-grad hooks instead of ``grad is None``).
 ``zero_grad`` zeroes the arena rather than dropping ``.grad`` tensors.
 """
+import ctypes
 import warnings
 
 import torch
 import torch.distributed as dist
 
-from ._lib import lib
+from ._lib import ConvDesc, lib
 from .runtime import collective, dp_world, stream
 
 
@@ -122,6 +123,7 @@ class _Arena:
         self.shadow = torch.empty(total, dtype=torch.bfloat16, device=dev)
         self.steps = [0] * len(params)
         self.touched = [False] * len(params)
+        self.dpacks = []  # conv weights whose packed dgrad copy this arena refreshes (functional._dgrad_weight)
         with torch.no_grad():
             for i, p in enumerate(params):
                 off, n = self.offsets[i], p.numel()
@@ -143,6 +145,20 @@ class _Arena:
         def mark(_p):
             self.touched[i] = True
         return mark
+
+    def repack(self):
+        """Refresh the packed data-gradient copies of the registered conv weights from the bf16
+        shadows just updated (one rtsds_conv2d_dgrad_pack_many launch per 16 segments)."""
+        live = [p for p in self.dpacks if p._rt_dpack.arena is self and getattr(p, "_rt_shadow", None) is not None]
+        if not live:
+            return
+        n = len(live)
+        descs = (ConvDesc * n)(*[p._rt_dpack.desc for p in live])
+        src = (ctypes.c_void_p * n)(*[p._rt_shadow.data_ptr() for p in live])
+        dst = (ctypes.c_void_p * n)(*[p._rt_dpack.buf.data_ptr() for p in live])
+        lib.rtsds_conv2d_dgrad_pack_many(n, descs, src, dst, stream())
+        for p in live:
+            p._rt_dpack.valid = p._rt_shadow_key
 
     def sink(self, i):
         """Gradient view a backward kernel may accumulate into directly (marks the parameter
@@ -313,6 +329,9 @@ class _FlatOptimizer(torch.optim.Optimizer):
             self._launch(g, a, lo, hi, a.steps[i] + 1, hyper, gscale)
             for k in range(i, j + 1):
                 a.steps[k] += 1
+        for a in arenas:
+            if a.shadow is not None:
+                a.repack()
         return loss
 
     # ------------------------------------------------------------------ hipGraph support

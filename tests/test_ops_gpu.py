@@ -754,3 +754,96 @@ def test_padded_image_input_bit_identical(kh, pad):
         outs.append((y.detach().float().cpu(), wp.grad.float().cpu(), ye.float().cpu()))
     for a, b in zip(outs[0], outs[1]):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("case", [
+    (2, 64, 16, 24, 64, 3, 1, 1, 1),      # stride-1 GEMM route
+    (2, 64, 16, 16, 128, 3, 2, 1, 1),     # stride-2 parity phases
+    (1, 32, 13, 17, 64, 3, 2, 1, 1),      # stride-2 phases, odd sizes
+    (2, 64, 16, 16, 128, 1, 2, 0, 1),     # 1x1 s2: phases without taps
+    (2, 128, 8, 128, 19, 3, 1, 1, 1),     # halo route (flipped weights), Cout padded to 32
+    (2, 512, 16, 32, 512, 3, 1, 1, 1),    # DGRAD split-K
+    (1, 64, 13, 17, 64, 3, 1, 2, 2),      # dilated
+    (2, 512, 32, 64, 19, 1, 1, 0, 1),     # narrow 1x1 (pw.hip): no packed copy
+])
+def test_dgrad_packed_weights_bit_identical(case):
+    """rtsds_conv2d_dgrad_pack_many (all cases in one call) + RTSDS_WEIGHT_PACKED equals the
+    per-call repack bit for bit: plain, accumulate and the LeakyReLU-masked variant."""
+    import ctypes
+    from rtsds_amd._lib import ConvDesc, WEIGHT_PACKED, lib
+    from rtsds_amd.functional import _conv_desc, _P
+    from rtsds_amd.runtime import stream, workspace
+
+    n, c, h, w, k, kh, s, p, dil = case
+    g = torch.Generator().manual_seed(23)
+    x = _dev(torch.randn(n, c, h, w, generator=g), torch.bfloat16)
+    wq = _dev(torch.randn(k, c, kh, kh, generator=g) / (kh * kh * c) ** 0.5, torch.bfloat16)
+    d = _conv_desc(x, k, kh, kh, (s, s), (p, p), (dil, dil))
+    nb = lib.rtsds_conv2d_dgrad_pack_bytes(ctypes.byref(d))
+    if case[4] == 19 and kh == 1:
+        assert nb == 0
+        return
+    assert nb > 0
+    dy = _dev(torch.randn(n, k, d.ho, d.wo, generator=g), torch.bfloat16)
+    pk = torch.full((nb // 2,), float("nan"), dtype=torch.bfloat16, device=DEV)
+    descs = (ConvDesc * 1)(d)
+    assert lib.rtsds_conv2d_dgrad_pack_many(1, descs, (ctypes.c_void_p * 1)(wq.data_ptr()),
+                                            (ctypes.c_void_p * 1)(pk.data_ptr()), stream()) == 0
+    ws = workspace(lib.rtsds_conv2d_dgrad_workspace(ctypes.byref(d)), x.device)
+    base = _dev(torch.randn(n, c, h, w, generator=g), torch.bfloat16)
+    outs = []
+    for wt, flag in ((wq, 0), (pk, WEIGHT_PACKED)):
+        a, b, m = torch.empty_like(x), base.clone(), torch.empty_like(x)
+        assert lib.rtsds_conv2d_dgrad(ctypes.byref(d), _P(dy), _P(wt), _P(a), flag, _P(ws), ws.numel(), stream()) == 0
+        assert lib.rtsds_conv2d_dgrad(ctypes.byref(d), _P(dy), _P(wt), _P(b), 1 | flag, _P(ws), ws.numel(), stream()) == 0
+        assert lib.rtsds_conv2d_dgrad_act(ctypes.byref(d), _P(dy), _P(wt), _P(m), _P(x), 2 | flag, _P(ws), ws.numel(),
+                                          stream()) == 0
+        torch.cuda.synchronize()
+        outs.append((a.float().cpu(), b.float().cpu(), m.float().cpu()))
+    for u, v in zip(*outs):
+        assert torch.equal(u, v)
+    ref = TF.conv_transpose2d(dy.double().cpu(), wq.double().cpu(), stride=s, padding=p, dilation=dil,
+                              output_padding=(h - ((d.ho - 1) * s - 2 * p + dil * (kh - 1) + 1),
+                                              w - ((d.wo - 1) * s - 2 * p + dil * (kh - 1) + 1)))
+    _close(outs[1][0], ref, torch.bfloat16, "dx")
+
+
+def test_dgrad_packs_in_training_bit_identical():
+    """Three BiSeNet bf16 seg iterations and two DA iterations with the optimizer-maintained
+    packed dgrad weights (default) leave parameters, optimizer state and BN buffers identical to
+    the per-call repack (functional.set_dgrad_packs(False))."""
+    import rtsds_amd
+    from rtsds_amd import losses, optim
+    from rtsds_amd import train as rtrain
+    from rtsds_amd.models.bisenet.build_bisenet import BiSeNet
+    from rtsds_amd.models.domain_shift.adversarial.model import TinyDomainDiscriminator
+
+    g = torch.Generator().manual_seed(29)
+    x = torch.randn(2, 3, 64, 128, generator=g).to(DEV)
+    xt = torch.randn(2, 3, 64, 128, generator=g).to(DEV)
+    y = torch.randint(0, 20, (2, 64, 128), generator=g).to(DEV)
+    ce, bce = losses.CrossEntropyLoss(ignore_index=19), losses.BCEWithLogitsLoss()
+    states = []
+    try:
+        for on in (False, True):
+            F.set_dgrad_packs(on)
+            with rtsds_amd.precision(torch.bfloat16):
+                torch.manual_seed(3)
+                net = BiSeNet(19, "resnet18").to(DEV).train()
+                disc = TinyDomainDiscriminator(19).to(DEV).train()
+                opt = optim.Adam(net.parameters(), lr=1e-3)
+                dopt = optim.Adam(disc.parameters(), lr=1e-3, weight_decay=1e-4)
+                for _ in range(3):
+                    rtrain.seg_step(net, ce, opt, x, y)
+                for _ in range(2):
+                    rtrain.da_step(net, disc, opt, dopt, ce, bce, x, y, xt, 0.1, 100)
+                torch.cuda.synchronize()
+                if on:
+                    assert any(getattr(p, "_rt_dpack", None) is not None and p._rt_dpack.valid is not None
+                               for p in net.parameters())
+                states.append({k: v.detach().float().cpu().clone() for k, v in
+                               list(net.state_dict().items()) + list(disc.state_dict().items())})
+    finally:
+        F.set_dgrad_packs(True)
+    for k in states[0]:
+        assert torch.equal(states[0][k], states[1][k]), k
