@@ -1916,29 +1916,40 @@ struct PackSeg {
   void* wt;  // segment base (phase offset applied)
   int co_n, co_p, kh, kw, ci_n, tkh, tkw, r0h, r0w, rstep, blk0;
 };
-static const int kPackSegs = 16, kPackPer = 8;
+static const int kPackSegs = 16;
 struct PackBatch {
   PackSeg s[kPackSegs];
   int nseg;
 };
+// One workgroup per (tap, 64 Cout x 64 Cin tile): rows of Cin read coalesced, transposed
+// through LDS, rows of Cout written coalesced ([ci][tap][co_p], zero for co >= co_n).
+static int pack_tiles(const PackSeg& q) { return q.tkh * q.tkw * rt_cdiv(q.co_p, 64) * rt_cdiv(q.ci_n, 64); }
 template <typename T>
 __global__ void __launch_bounds__(256) dgrad_pack_kernel(const PackBatch b) {
+  __shared__ float tile[64][65];
   int si = 0;
   for (int i = 1; i < b.nseg; ++i)
     if (b.s[i].blk0 <= (int)blockIdx.x) si = i;
   const PackSeg& g = b.s[si];
-  const int taps = g.tkh * g.tkw, total = g.co_p * taps * g.ci_n;
+  const int nco = (g.co_p + 63) / 64, nci = (g.ci_n + 63) / 64, taps = g.tkh * g.tkw;
+  int t = (int)blockIdx.x - g.blk0;
+  const int ct = t % nci;
+  t /= nci;
+  const int ot = t % nco, tap = t / nco;
+  const int r = g.r0h + (tap / g.tkw) * g.rstep, sc = g.r0w + (tap % g.tkw) * g.rstep;
   const T* __restrict__ w = (const T*)g.w;
   T* __restrict__ wt = (T*)g.wt;
-  const int i0 = ((int)blockIdx.x - g.blk0) * 256 * kPackPer + threadIdx.x;
+  const int lx = threadIdx.x & 63, ly = threadIdx.x >> 6;
 #pragma unroll
-  for (int e = 0; e < kPackPer; ++e) {
-    const int i = i0 + e * 256;
-    if (i >= total) break;
-    const int co = i % g.co_p, rest = i / g.co_p;
-    const int tap = rest % taps, ci = rest / taps;
-    const int r = g.r0h + (tap / g.tkw) * g.rstep, sc = g.r0w + (tap % g.tkw) * g.rstep;
-    wt[i] = co < g.co_n ? w[((co * g.kh + r) * g.kw + sc) * g.ci_n + ci] : (T)0.0f;
+  for (int k = 0; k < 16; ++k) {
+    const int co = ot * 64 + ly + 4 * k, ci = ct * 64 + lx;
+    tile[ly + 4 * k][lx] = (co < g.co_n && ci < g.ci_n) ? to_f(w[((co * g.kh + r) * g.kw + sc) * g.ci_n + ci]) : 0.f;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int ci = ct * 64 + ly + 4 * k, co = ot * 64 + lx;
+    if (ci < g.ci_n && co < g.co_p) wt[((long)ci * taps + tap) * g.co_p + co] = from_f<T>(tile[lx][ly + 4 * k]);
   }
 }
 static bool dgrad_hconv(const rtsds_conv_desc* d, int kp);
@@ -2008,7 +2019,7 @@ extern "C" int rtsds_conv2d_dgrad_pack_many(int count, const rtsds_conv_desc* de
       q.w = w[i];
       q.wt = (char*)wt[i] + (intptr_t)q.wt * esize(d->dtype);
       q.blk0 = blocks;
-      blocks += rt_cdiv(q.co_p * q.tkh * q.tkw * q.ci_n, 256 * kPackPer);
+      blocks += pack_tiles(q);
       b.s[b.nseg++] = q;
     }
   }

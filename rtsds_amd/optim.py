@@ -206,7 +206,10 @@ class _FlatOptimizer(torch.optim.Optimizer):
     # ------------------------------------------------------------------ arena
     def _ensure(self):
         if self._arenas is None:
-            self._arenas = [_Arena(list(g["params"]), second=len(self._STATE) > 1) for g in self.param_groups]
+            # trainable parameters first: frozen ones (DeepLab's BatchNorm affines, deeplabv2.py:
+            # requires_grad = False) would otherwise split the update into one launch per conv
+            self._arenas = [_Arena(sorted(g["params"], key=lambda p: not p.requires_grad),
+                                   second=len(self._STATE) > 1) for g in self.param_groups]
             self._import_state()
         return self._arenas
 
