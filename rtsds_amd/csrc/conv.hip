@@ -857,7 +857,7 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(const ConvArgs P0) {
 
   // ---- epilogue: C[row][col], row = (lane>>4)*4 + e, col = lane&15 within each 16x16 block
   const int er = (lane >> 4) * 4, ec = lane & 15;
-  if (MODE == MODE_WGRAD || (MODE == MODE_DGRAD && P.slab != nullptr)) {
+  if (MODE == MODE_WGRAD || P.slab != nullptr) {  // FWD / DGRAD split-K: fp32 partials
     float* out = (MODE == MODE_WGRAD ? (float*)P.out : P.slab) + (long)kz * P.split_stride;
     if (P.N % 4 == 0) {
       // fp32 slab rows leave as 16-B chunks: the C fragments are staged through LDS one
@@ -1371,12 +1371,12 @@ static void launch_al(const ConvArgs& p, int cr, hipStream_t st, int splits = 1)
 }
 
 template <typename T, int MODE>
-static void dispatch_align(const ConvArgs& p, int cr, hipStream_t st) {
+static void dispatch_align(const ConvArgs& p, int cr, hipStream_t st, int splits = 1) {
   int bm, bn;
   pick_tile(p.M, p.N, sizeof(T) == 2, bm, bn, MODE == MODE_FWD);
   if constexpr (sizeof(T) == 2) {
-    if (bn == 32 && bm == 256) launch_al<T, MODE, 256, 32, 32, 4, 1>(p, cr, st);
-    else if (bn == 32) launch_al<T, MODE, 128, 32, 32, 4, 1>(p, cr, st);
+    if (bn == 32 && bm == 256) launch_al<T, MODE, 256, 32, 32, 4, 1>(p, cr, st, splits);
+    else if (bn == 32) launch_al<T, MODE, 128, 32, 32, 4, 1>(p, cr, st, splits);
     else if (bn == 64 && bm == 128) launch_al<T, MODE, 128, 64, 32, 2, 2>(p, cr, st);
     else if (bn == 64) launch_al<T, MODE, 64, 64, 64, 2, 2>(p, cr, st);
     else if (MODE == MODE_FWD && bm == 160) launch_al<T, MODE_FWD, 160, 128, 64, 2, 2>(p, cr, st);
@@ -1706,14 +1706,58 @@ extern "C" int rtsds_conv2d_input_pitch(const rtsds_conv_desc* d) {
   return check_desc(d) ? 0 : input_pitch(d);
 }
 
-// FWD workspace: channel-padded copies of x and w when Cin is not a vector multiple.
-extern "C" size_t rtsds_conv2d_fwd_workspace(const rtsds_conv_desc* d) {
+// FWD split-K for narrow outputs (<= 32 channels: DeepLab's ASPP branches, 2048 -> 19 classes
+// at 65x129, K = 18,432): the 128x32 tiles of M = 33,540 rows make 263 workgroups, one 4-wave
+// group per CU walking 288 K-tiles, latency-bound on the operand gathers.  S K-splits (>= 16
+// K-tiles each) into fp32 slabs [S][M][N] put ~6 groups on every CU (194 -> 100 us); fwd_split_reduce_kernel
+// sums them in split order and adds the bias (and y, for ConvSum's accumulate).  Only without
+// BatchNorm-statistics / activation epilogues; BK = 64 (LDS-DMA path: Cin % 32 == 0).
+struct FwdSplit {
+  int splits, tps;
+  size_t slab_bytes;
+};
+static FwdSplit fwd_split(const rtsds_conv_desc* d) {
+  FwdSplit s = {1, 1 << 30, 0};
+  if (d->dtype != RTSDS_BF16 || d->k > 32 || d->c % 32 != 0 || pooled_1x1(d) || hconv_ok(d) || sp_path(d)) return s;
+  const long M = (long)d->n * d->ho * d->wo;
+  const int nk = (d->kh * d->kw * d->c + 63) / 64;
+  int bm, bn;
+  pick_tile(M, d->k, true, bm, bn, true);
+  const long tiles = (M + bm - 1) / bm;
+  if (tiles >= 512 || nk < 32) return s;
+  const int want = (int)std::min<long>((1536 + tiles - 1) / tiles, nk / 16);
+  if (want < 2) return s;
+  s.tps = (nk + want - 1) / want;
+  s.splits = (nk + s.tps - 1) / s.tps;
+  s.slab_bytes = al256((size_t)s.splits * M * d->k * 4);
+  return s;
+}
+
+// y (+)= bias + sum_s slab[s] -> bf16, the split order fixed (deterministic)
+__global__ void __launch_bounds__(256) fwd_split_reduce_kernel(const float* __restrict__ slab, const float* __restrict__ bias,
+                                                               bf16* __restrict__ y, long total, int n, long stride,
+                                                               int splits, int accum) {
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    float s = slab[i];
+    for (int q = 1; q < splits; ++q) s += slab[q * stride + i];
+    if (bias) s += bias[i % n];
+    if (accum) s += to_f(y[i]);
+    y[i] = from_f<bf16>(s);
+  }
+}
+
+// FWD workspace: channel-padded copies of x and w when Cin is not a vector multiple, then the
+// split-K slabs (fwd_split).
+static size_t fwd_operand_ws(const rtsds_conv_desc* d) {
   if (pooled_1x1(d) || hconv_ok(d)) return 0;
   if (sp_path(d)) return sp_x4_bytes(d) + sp_w_bytes(d);
   const int cp = pad_c(d->c, d->dtype);
   if (cp == d->c) return 0;
   const size_t es = esize(d->dtype);
   return al256((size_t)d->n * d->h * d->w * cp * es) + al256((size_t)d->k * d->kh * d->kw * cp * es);
+}
+extern "C" size_t rtsds_conv2d_fwd_workspace(const rtsds_conv_desc* d) {
+  return fwd_operand_ws(d) + fwd_split(d).slab_bytes;
 }
 
 // Operands of the forward GEMM: the superpixel view of 3-channel stride-2 convs, or
@@ -1779,6 +1823,17 @@ extern "C" int rtsds_conv2d_fwd(const rtsds_conv_desc* d0, const void* x, const 
   p.M = d.n * d.ho * d.wo;
   p.N = d.k;
   p.K = d.kh * d.kw * d.c;
+  const FwdSplit fs = fwd_split(d0);
+  if (fs.splits > 1 && !bn_stats && p.act == 0) {
+    p.slab = (float*)((char*)ws + fwd_operand_ws(d0));
+    p.tiles_per_split = fs.tps;
+    p.split_stride = (long)p.M * p.N;
+    dispatch_align<bf16, MODE_FWD>(p, d.c, st, fs.splits);
+    const long total = (long)p.M * p.N;
+    hipLaunchKernelGGL(fwd_split_reduce_kernel, dim3((int)std::min<long>(8192, (total + 255) / 256)), dim3(256), 0, st,
+                       (const float*)p.slab, bias, (bf16*)y, total, p.N, p.split_stride, fs.splits, p.accum);
+    return hipGetLastError() == hipSuccess ? RTSDS_OK : RTSDS_ERR_LAUNCH;
+  }
   if (d.dtype == RTSDS_BF16) dispatch_align<bf16, MODE_FWD>(p, d.c, st);
   else dispatch_align<float, MODE_FWD>(p, d.c, st);
   return hipGetLastError() == hipSuccess ? RTSDS_OK : RTSDS_ERR_LAUNCH;
@@ -2231,7 +2286,16 @@ static WgradPlan wgrad_plan(const rtsds_conv_desc* d) {
   w.bn = b16 ? (N <= 64 ? 64 : 128) : 64;
   const long tiles = (long)rt_cdiv(M, w.bm) * rt_cdiv(N, w.bn);
   const long nk = (R + BK - 1) / BK;
-  long want = std::max<long>(1, 512 / tiles);
+  // narrow outputs (<= 32 rows of Cout: the 19-class convs) stream far more pixels per tile:
+  // ~6 groups per CU hide more of the gather latency (DeepLab ASPP 304 -> 226 us, FFM 147 ->
+  // 125).  Wide grids that fill only 432 of a round's 512 slots (DeepLab layer4 3x3, 144
+  // tiles x 3) take ~2 full rounds of splits instead when every split keeps >= 64 K-tiles
+  // (373 -> 325 us); short reductions (BiSeNet layer4, 64 K-tiles) would pay it in slab traffic.
+  long want = std::max<long>(1, (w.bm == 64 && M <= 32 ? 1536 : 512) / tiles);
+  if (!(w.bm == 64 && M <= 32) && tiles >= 64 && tiles * want < 480) {
+    const long w2 = 1024 / tiles;
+    if (tiles * w2 >= 922 && nk / w2 >= 64) want = w2;
+  }
   want = std::min<long>(want, std::max<long>(1, nk / 8));
   want = std::min<long>(want, 256);
   w.tps = (int)((nk + want - 1) / want);

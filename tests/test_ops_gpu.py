@@ -63,6 +63,7 @@ CONV_CASES = [
     (1, 256, 8, 64, 64, 3, 1, 1, 1, True),     # hconv N-tiled (Cin >= 256, Cout 2 x 32), fwd and dgrad
     (2, 512, 16, 32, 512, 3, 1, 1, 1, False),  # layer4-like: DGRAD split-K (128x128 tiles, fp32 slabs)
     (2, 512, 16, 32, 512, 3, 1, 2, 2, False),  # dilated (DeepLab layer3-like, small M): DGRAD split-K
+    (2, 256, 16, 32, 19, 3, 1, 2, 2, True),    # ASPP-like narrow output, few M tiles: FWD split-K slabs
     (2, 512, 32, 64, 19, 1, 1, 0, 1, True),    # supervision 1x1 (pw.hip backward): 1 row group
     (2, 40, 32, 64, 32, 1, 1, 0, 1, True),     # pw.hip: Cout 32, 12 row groups
     (4, 19, 32, 32, 19, 1, 1, 0, 1, True),     # pw.hip: final 19->19, odd Cin (scalar lanes)
@@ -123,6 +124,32 @@ def test_dgrad_split_k_accumulate():
     ref = TF.conv_transpose2d(dy.double().cpu(), wq.double().cpu(), padding=1)
     _close(fresh, ref, torch.bfloat16, "dx")
     _close(dx, dx0.double() + fresh.double(), torch.bfloat16, "dx accum", tol=1e-2)
+
+
+def test_fwd_split_k_accumulate():
+    """FWD split-K (narrow output, few M tiles: DeepLab's ASPP branches) with bias and the
+    accumulate flag (ConvSum: y += conv + bias), against the non-accumulating call."""
+    import ctypes
+    from rtsds_amd._lib import ACCUMULATE, lib
+    from rtsds_amd.functional import _conv_desc, _P
+    from rtsds_amd.runtime import stream, workspace
+
+    g = torch.Generator().manual_seed(7)
+    n, c, h, w, k = 2, 512, 13, 21, 19
+    x = _dev(torch.randn(n, c, h, w, generator=g), torch.bfloat16)
+    wq = _dev(torch.randn(k, c, 3, 3, generator=g) / (9 * c) ** 0.5, torch.bfloat16)
+    b = torch.randn(k, generator=g).to(DEV)
+    d = _conv_desc(x, k, 3, 3, (1, 1), (4, 4), (4, 4))
+    y0 = _dev(torch.randn(n, k, h, w, generator=g), torch.bfloat16)
+    y, fresh = y0.clone(), torch.empty_like(y0)
+    ws = workspace(lib.rtsds_conv2d_fwd_workspace(ctypes.byref(d)), x.device)
+    for out, acc in ((y, ACCUMULATE), (fresh, 0)):
+        assert lib.rtsds_conv2d_fwd(ctypes.byref(d), _P(x), _P(wq), _P(b), _P(out), acc, None, _P(ws), ws.numel(),
+                                    stream()) == 0
+    torch.cuda.synchronize()
+    ref = TF.conv2d(x.double().cpu(), wq.double().cpu(), b.double().cpu(), padding=4, dilation=4)
+    _close(fresh, ref, torch.bfloat16, "y")
+    _close(y, y0.double() + fresh.double(), torch.bfloat16, "y accum", tol=1e-2)
 
 
 @pytest.mark.parametrize("c", [512, 19])
