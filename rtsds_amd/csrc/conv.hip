@@ -1329,9 +1329,14 @@ static void launch(const ConvArgs& p, int splits, hipStream_t st) {
 // workgroups on the 256 CUs.  bf16: 128x128 (or 160x128, see below) / 128x64 / 256x32 (19- and
 // 1-channel outputs), falling back to 64x64 / 128x32 for small-M layers (ResNet layer4, pooled
 // vectors).
-static void pick_tile(long M, int N, bool b16, int& bm, int& bn, bool fwd = false) {
+static void pick_tile(long M, int N, bool b16, int& bm, int& bn, bool fwd = false, long K = 0) {
   auto blocks = [&](int a, int b) { return ((M + a - 1) / a) * (long)((N + b - 1) / b); };
   if (b16) {
+    // short reductions (K <= 512: 1-8 K-steps, DeepLab's layer1-3 1x1 convs) cannot hide the
+    // gather latency or the epilogue inside one workgroup; 128 x 64 tiles (48 KB of LDS: 3
+    // groups per CU instead of 2) overlap more of them across workgroups (64 -> 256 1x1
+    // forward 44 -> 33 us, 1024 -> 256 data gradient 72 -> 66 us; profiles/r2_conv_shortk_ab.txt)
+    if (N > 64 && K > 0 && K <= 512 && blocks(128, 64) >= 1024) { bm = 128; bn = 64; return; }
     // (data gradients keep 128 rows: 4 groups per CU instead of 2 hide more of the gather
     // latency -- TinyD conv1's dgrad on the padded probabilities 313 -> 296 us at bs 8, 140 ->
     // 119 us at 1280x720 bs 2)
@@ -1376,7 +1381,7 @@ static void launch_al(const ConvArgs& p, int cr, hipStream_t st, int splits = 1)
 template <typename T, int MODE>
 static void dispatch_align(const ConvArgs& p, int cr, hipStream_t st, int splits = 1) {
   int bm, bn;
-  pick_tile(p.M, p.N, sizeof(T) == 2, bm, bn, MODE == MODE_FWD);
+  pick_tile(p.M, p.N, sizeof(T) == 2, bm, bn, MODE == MODE_FWD, p.K);
   if constexpr (sizeof(T) == 2) {
     if (bn == 32 && bm == 256) launch_al<T, MODE, 256, 32, 32, 4, 1>(p, cr, st, splits);
     else if (bn == 32) launch_al<T, MODE, 128, 32, 32, 4, 1>(p, cr, st, splits);
@@ -1693,7 +1698,8 @@ extern "C" int rtsds_conv2d_fwd_stats_tiles(const rtsds_conv_desc* d) {
   if (hconv_ok(d)) return hconv_tiles(d);
   int bm, bn;
   const long M = (long)d->n * d->ho * d->wo;
-  pick_tile(M, d->k, d->dtype == RTSDS_BF16, bm, bn, true);
+  const long K = sp_path(d) ? 0 : (long)d->kh * d->kw * pad_c(d->c, d->dtype);  // rtsds_conv2d_fwd's p.K
+  pick_tile(M, d->k, d->dtype == RTSDS_BF16, bm, bn, true, K);
   return (int)((M + bm - 1) / bm);
 }
 

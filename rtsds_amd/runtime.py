@@ -67,6 +67,11 @@ def require_hip(*tensors):
 
 
 CL = torch.channels_last
+# hipGraph captures are thread-local: under the default global mode a HIP call from ANY thread
+# during a capture -- RCCL's process-group watchdog polling its events -- is rejected
+# ("operation not permitted when stream is capturing") and aborts the process; seen on the
+# one-rank RCCL test of the data-parallel graph segments.
+CAPTURE_MODE = "thread_local"
 
 
 def empty_nhwc(n, c, h, w, dtype, device):
@@ -215,7 +220,7 @@ class GraphedForward:
                 module(self.static_in)
         torch.cuda.current_stream(x.device).wait_stream(side)
         self.graph = torch.cuda.CUDAGraph()
-        with torch.no_grad(), torch.cuda.graph(self.graph):
+        with torch.no_grad(), torch.cuda.graph(self.graph, capture_error_mode=CAPTURE_MODE):
             self.static_out = module(self.static_in)
 
     def __call__(self, x):
@@ -285,7 +290,7 @@ class GraphedStep:
         try:
             with torch.cuda.stream(cap_stream):
                 self._graph = torch.cuda.CUDAGraph()
-                self._graph.capture_begin(pool=self._pool)
+                self._graph.capture_begin(pool=self._pool, capture_error_mode=CAPTURE_MODE)
                 _capture["step"] = self
                 try:
                     self.outputs = fn()
@@ -304,7 +309,7 @@ class GraphedStep:
         self._graph.capture_end()
         self.segments.append((self._graph, coll))
         self._graph = torch.cuda.CUDAGraph()
-        self._graph.capture_begin(pool=self._pool)
+        self._graph.capture_begin(pool=self._pool, capture_error_mode=CAPTURE_MODE)
 
     def __call__(self):
         for o in self.optimizers:
