@@ -945,6 +945,23 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(const ConvArgs P0) {
             bgx[q] = 0.f;
           }
         }
+        // the BatchNorm input chunks this thread folds into the statistics, loaded up front (all
+        // in flight across the LDS staging): read after each chunk's store they serialised
+        // behind it (the compiler cannot reorder them past the possibly-aliasing store)
+        constexpr int NIT = (BM * CPR + 255) / 256;
+        constexpr int NXP = MODE == MODE_DGRAD ? NIT : 1;
+        V16 xpre[NXP];
+        if constexpr (MODE == MODE_DGRAD) {
+          if (bnb) {
+#pragma unroll
+            for (int it = 0; it < NIT; ++it) {
+              const int c = tid + it * 256;
+              const int row = c / CPR, cc = c - row * CPR;
+              const int gm = m0 + row, gn = n0 + cc * V;
+              if (c < BM * CPR && gm < P.M && gn < P.N) xpre[it] = *(const V16*)((const T*)P.bnb_x + out_row(gm) * P.N + gn);
+            }
+          }
+        }
         __syncthreads();
 #pragma unroll
         for (int j = 0; j < FN; ++j) {
@@ -962,7 +979,9 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(const ConvArgs P0) {
         }
         __syncthreads();
 #pragma unroll
-        for (int c = tid; c < BM * CPR; c += 256) {
+        for (int it = 0; it < NIT; ++it) {
+          const int c = tid + it * 256;
+          if (c >= BM * CPR) break;
           const int row = c / CPR, cc = c - row * CPR;
           const int gm = m0 + row, gn = n0 + cc * V;
           if (gm < P.M && gn < P.N) {
@@ -991,8 +1010,8 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(const ConvArgs P0) {
               for (int q = 0; q < V; ++q) v[q] = from_f<T>(act_f(f[q]));
             }
             *(V16*)(out + o) = v;
-            if (bnb) {
-              const V16 xr = *(const V16*)((const T*)P.bnb_x + o);
+            if (MODE == MODE_DGRAD && bnb) {
+              const V16 xr = xpre[MODE == MODE_DGRAD ? it : 0];
 #pragma unroll
               for (int q = 0; q < V; ++q) {
                 const float xv = to_f(xr[q]);
