@@ -977,6 +977,23 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(const ConvArgs P0) {
               cs[(wm0 + i * 16 + er + e) * CP + col] = from_f<T>(post ? v : act_f(v));
             }
         }
+        // the mask / accumulate operand chunks, loaded before the staging barrier (all in
+        // flight, the accumulators dead by now); read after each chunk's store they serialised
+        const bool pmask = MODE == MODE_DGRAD && has_mask;  // (mask and accumulate exclusive)
+        const bool ppre_on = pmask || P.accum;
+        V16 ppre[NIT];
+        if (ppre_on) {
+#pragma unroll
+          for (int it = 0; it < NIT; ++it) {
+            const int c = tid + it * 256;
+            const int row = c / CPR, cc = c - row * CPR;
+            const int gm = m0 + row, gn = n0 + cc * V;
+            if (c < BM * CPR && gm < P.M && gn < P.N) {
+              const long o = out_row(gm) * P.N + gn;
+              ppre[it] = pmask ? *(const V16*)((const T*)P.mask + o) : *(const V16*)(out + o);
+            }
+          }
+        }
         __syncthreads();
 #pragma unroll
         for (int it = 0; it < NIT; ++it) {
@@ -997,12 +1014,12 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(const ConvArgs P0) {
                 for (int q = 0; q < V; ++q) f[q] += to_f(r[q]);
               }
               if (has_mask) {  // (accumulate is refused together with a mask)
-                const V16 r = *(const V16*)((const T*)P.mask + o);
+                const V16 r = pmask ? ppre[it] : *(const V16*)((const T*)P.mask + o);
 #pragma unroll
                 for (int q = 0; q < V; ++q) f[q] = mask_f(f[q], to_f(r[q]));
               }
               if (P.accum) {
-                const V16 r = *(const V16*)(out + o);
+                const V16 r = pmask ? *(const V16*)(out + o) : ppre[it];
 #pragma unroll
                 for (int q = 0; q < V; ++q) f[q] += to_f(r[q]);
               }
