@@ -84,13 +84,39 @@ def synthetic_batch(n, seed, device, h=H, w=W):
     return x.to(device), y.to(device)
 
 
+def host_cpus():
+    """CPUs this process may actually run on: the affinity mask, further capped by a cgroup
+    CPU quota when one is set (the GPU box gives a job a share of a larger machine, and
+    os.cpu_count() reports the whole machine there)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = period = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:  # cgroup v2
+            quota, period = f.read().split()[:2]
+    except (OSError, ValueError):
+        try:  # cgroup v1
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+                quota = f.read().strip()
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+                period = f.read().strip()
+        except OSError:
+            pass
+    try:
+        if quota not in (None, "max", "-1"):
+            n = min(n, max(1, -(-int(quota) // int(period))))
+    except ValueError:
+        pass
+    return max(1, n)
+
+
 def cpu_baseline(seconds=15.0):
     """Oracle (plain-PyTorch CPU restatement of the reference, pinned to the reference's
-    golden captures) timed on the host: train step at 1024x512, batch 2."""
+    golden captures) timed on the host: train step at 1024x512, batch 2, with one intra-op
+    thread per CPU available to the process (host_cpus)."""
     from oracle import models as om
     from oracle import steps as osteps
     from oracle.weights import apply_recipe, synthetic_images, synthetic_labels
-    threads = max(1, min(16, os.cpu_count() or 1))
+    threads = host_cpus()
     torch.set_num_threads(threads)
     net = apply_recipe(om.BiSeNet(NC, "resnet18"), seed=1).train()
     opt = torch.optim.Adam(net.parameters(), lr=1e-4)
@@ -106,6 +132,7 @@ def cpu_baseline(seconds=15.0):
             break
     dt = time.perf_counter() - t0
     return {"value": round(2 * n / dt, 4), "unit": "images/s", "cores": threads, "kind": "port",
+            "host_cpu_count": os.cpu_count(), "affinity_cpus": len(os.sched_getaffinity(0)),
             "sample": f"oracle BiSeNet-R18 train step (fwd+3xCE+bwd+Adam), fp32, 2x3x512x1024, "
                       f"{n} timed steps after 1 warm-up ({dt:.1f} s)"}
 

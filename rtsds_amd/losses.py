@@ -4,7 +4,7 @@ import torch
 from torch import nn
 
 from . import functional as F
-from .runtime import collective, dp_world
+from .runtime import dp_world
 
 
 class CrossEntropyLoss(nn.Module):
@@ -23,10 +23,17 @@ class CrossEntropyLoss(nn.Module):
 
 
 class BCEWithLogitsLoss(nn.Module):
+    """Mean of the logistic loss.  Under data parallelism the mean runs over every rank's
+    elements.  D's logits have a data-independent size, so the global element count is
+    all-reduced once per local size and cached: the ranks see the same sequence of local batch
+    sizes (DistributedSampler pads its shards to equal length, synthetic loaders are equal),
+    so they miss the cache together.  Unequal shards still get the exact weighted mean."""
+
     def __init__(self, reduction="mean"):
         super().__init__()
         if reduction != "mean":
             raise NotImplementedError("rtsds_amd.BCEWithLogitsLoss: mean only (main.py:132)")
+        self._global = {}
 
     def forward(self, input, target):
         loss = F.bce_with_logits(input, target)
@@ -36,7 +43,12 @@ class BCEWithLogitsLoss(nn.Module):
         # weighted by its share of the all-reduced element count, so shards of unequal size
         # still sum to the gathered-batch mean (a graph-segment break under capture)
         import torch.distributed as dist
-        n = float(input.numel())
-        cnt = torch.full((1,), n, dtype=torch.float32, device=input.device)
-        collective(lambda: dist.all_reduce(cnt))
-        return loss * (n / cnt[0])
+        n = int(input.numel())
+        total = self._global.get((n, dp_world()))
+        if total is None:
+            if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
+                raise RuntimeError("rtsds_amd.BCEWithLogitsLoss: run an eager iteration before graph capture")
+            cnt = torch.full((1,), float(n), dtype=torch.float64, device=input.device)
+            dist.all_reduce(cnt)  # eager, outside any graph capture: warm-up iterations fill the cache
+            total = self._global[(n, dp_world())] = float(cnt.item())
+        return loss * (n / total)

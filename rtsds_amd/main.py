@@ -107,7 +107,8 @@ def real_datasets_loader(config, is_augmented, device="cuda"):
     """main.py:60-108 on the device pipeline: the reference's readers (PNG decode on CPU
     DataLoader workers) deliver raw uint8 samples, batches go to HBM and through the
     torchvision-equivalent HIP transforms (rtsds_amd.transforms); under data parallelism each
-    rank reads a disjoint shard (DistributedSampler)."""
+    rank reads a disjoint shard of the training sets (DistributedSampler, a new permutation per
+    iterator -- transforms.DeviceLoader advances its epoch); validation reads the whole set."""
     from torch.utils.data import DataLoader
     from torch.utils.data.distributed import DistributedSampler
 
@@ -117,8 +118,9 @@ def real_datasets_loader(config, is_augmented, device="cuda"):
     cs_size, gta_size = T.parse_size(cs["image_size"]), T.parse_size(gta["image_size"])
     rank, _, world = dist_env()
 
-    def loader(ds, bs, workers, shuffle):
-        sampler = DistributedSampler(ds, num_replicas=world, rank=rank, shuffle=shuffle) if world > 1 else None
+    def loader(ds, bs, workers, shuffle, shard=True):
+        sampler = DistributedSampler(ds, num_replicas=world, rank=rank, shuffle=shuffle) \
+            if world > 1 and shard else None
         return DataLoader(ds, batch_size=bs, shuffle=shuffle and sampler is None, sampler=sampler, pin_memory=False,
                           num_workers=workers, collate_fn=T.collate_raw)
 
@@ -130,7 +132,11 @@ def real_datasets_loader(config, is_augmented, device="cuda"):
     val_ds = CityScapes(cs["segmentation_val_dir"], cs["images_val_dir"])
     gta_ds = GTA5(gta["images_dir"], gta["segmentation_dir"], None, None)
     return (T.DeviceLoader(loader(train_ds, cs["batch_size"], cs["num_workers"], True), city_img, city_lbl, device),
-            T.DeviceLoader(loader(val_ds, cs["batch_size"], cs["num_workers"], False), city_img, city_lbl, device),
+            # validation is not sharded: a DistributedSampler pads shards with duplicates and
+            # the confusion histogram is per process, so every rank evaluates the full val set
+            # and reports the reference's full-set mIoU
+            T.DeviceLoader(loader(val_ds, cs["batch_size"], cs["num_workers"], False, shard=False),
+                           city_img, city_lbl, device),
             T.DeviceLoader(loader(gta_ds, gta["batch_size"], gta["num_workers"], True), gta_img, gta_lbl, device))
 
 

@@ -201,6 +201,8 @@ class _FlatOptimizer(torch.optim.Optimizer):
         self._capturing = False  # inside stream capture: the hyper values are staged outside
         self._runs = None        # [(group, i, j)] of the last step
         self._hyper = None       # device fp32 [runs][3]
+        self._ring = [[None, None] for _ in range(8)]  # pinned staging buffers + their copy events
+        self._ring_pos = 0
         self._finish = None      # pending early gradient all-reduce (start_grad_allreduce)
 
     # ------------------------------------------------------------------ arena
@@ -346,12 +348,28 @@ class _FlatOptimizer(torch.optim.Optimizer):
         device hyper buffer (stream-ordered H2D copy from pinned memory)."""
         runs = self._runs or []
         arenas = self._ensure()
-        vals = torch.empty(max(1, 3 * len(runs)), dtype=torch.float32, pin_memory=True)
-        for r, (gi, i, _) in enumerate(runs):
-            vals[3 * r:3 * r + 3] = torch.tensor(self._hyper3(self.param_groups[gi], arenas[gi].steps[i] + 1))
-        if self._hyper is None or self._hyper.numel() < vals.numel():
-            self._hyper = torch.empty(vals.numel(), dtype=torch.float32, device=arenas[0].flat.device)
-        self._hyper[:vals.numel()].copy_(vals, non_blocking=True)
+        flat = []
+        for gi, i, _ in runs:
+            flat.extend(self._hyper3(self.param_groups[gi], arenas[gi].steps[i] + 1))
+        n = max(1, len(flat))
+        if self._hyper is None or self._hyper.numel() < n:
+            self._hyper = torch.empty(n, dtype=torch.float32, device=arenas[0].flat.device)
+        # A ring of pinned staging buffers, each reused only after its previous copy has
+        # completed (its event).  A fresh pinned tensor per replay -- round 2 -- hit the host
+        # allocator whenever the host ran ahead of the GPU (the cached block's copy still
+        # pending), and the new pinned allocation waited for the device: enqueue ~= step time.
+        slot = self._ring[self._ring_pos]
+        self._ring_pos = (self._ring_pos + 1) % len(self._ring)
+        if slot[0] is None or slot[0].numel() < n:
+            slot[0] = torch.empty(n, dtype=torch.float32, pin_memory=True)
+            slot[1] = torch.cuda.Event()
+        else:
+            slot[1].synchronize()
+        buf = slot[0][:n]
+        if flat:
+            buf.numpy()[:] = flat
+        self._hyper[:n].copy_(buf, non_blocking=True)
+        slot[1].record()
 
     def steps_snapshot(self):
         return [list(a.steps) for a in self._ensure()]

@@ -189,14 +189,25 @@ class DeviceLoader:
         self.image_pipe, self.label_pipe = image_pipe, label_pipe
         self.device = device
         self.decode = decode_rgb_labels
+        self.epoch = 0
 
     def __len__(self):
         return len(self.loader)
 
     def _move(self, ts):
+        if torch.device(self.device).type == "cpu":
+            return list(ts)
         return [t.pin_memory().to(self.device, non_blocking=True) if t.device.type == "cpu" else t for t in ts]
 
     def __iter__(self):
+        # A DistributedSampler replays the permutation of its current epoch on every iter();
+        # the reference's RandomSampler draws a new one each time (adversarial_train takes
+        # next(iter(loader)) per iteration, train.py:186-187), so every new iterator advances
+        # the sampler's epoch.
+        sampler = getattr(self.loader, "sampler", None)
+        if hasattr(sampler, "set_epoch"):
+            sampler.set_epoch(self.epoch)
+            self.epoch += 1
         for images, labels in self.loader:
             images, labels = self._move(images), self._move(labels)
             if self.decode:

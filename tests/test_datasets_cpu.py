@@ -62,3 +62,25 @@ def test_oracle_transform_restatements():
     ids = torch.arange(19).view(1, 19)
     rgb = torch.tensor(OT.TRAIN_ID_COLORS).t()[:, ids[0]].view(3, 1, 19)
     assert torch.equal(OT.decode_gta5(rgb), ids)
+
+
+def test_device_loader_new_permutation_per_iterator():
+    """ADVICE r2: adversarial_train takes next(iter(loader)) every iteration (train.py:186-187);
+    with a DistributedSampler each new iterator must draw a new permutation, as the
+    reference's RandomSampler does, instead of replaying epoch 0's first batch."""
+    from torch.utils.data import DataLoader
+    from torch.utils.data.distributed import DistributedSampler
+    from rtsds_amd.transforms import DeviceLoader, collate_raw
+    ds = [(torch.tensor([i]), torch.tensor([i])) for i in range(64)]
+    firsts = {0: [], 1: []}
+    for rank in (0, 1):
+        sampler = DistributedSampler(ds, num_replicas=2, rank=rank, shuffle=True, seed=3)
+        dl = DeviceLoader(DataLoader(ds, batch_size=4, sampler=sampler, collate_fn=collate_raw), lambda t: t, lambda t: t, device="cpu")
+        for _ in range(4):
+            x, _ = next(iter(dl))
+            firsts[rank].append(tuple(int(t) for t in x))
+    for rank in (0, 1):
+        assert len(set(firsts[rank])) == 4, firsts[rank]
+    # the two ranks' shards stay disjoint for each epoch
+    for a, b in zip(firsts[0], firsts[1]):
+        assert not set(a) & set(b)
