@@ -200,7 +200,8 @@ int rtsds_act_bwd(const void* dy, const void* y, void* dx, long n, int act, floa
 
 /* ---------------------------------------------------------------- pooling
  * MaxPool2d (build_contextpath.py:21 via torchvision; deeplabv2.py:79 ceil_mode -- the
- * caller sizes ho/wo).  idx: uint8 tap index per output, consumed by the backward.       */
+ * caller sizes ho/wo).  idx: uint8 tap index per output, consumed by the backward; NULL for
+ * inference (3x3 windows with 16-B channel vectors only, else RTSDS_ERR_UNSUPPORTED).     */
 int rtsds_maxpool_fwd(const void* x, void* y, uint8_t* idx, int n, int h, int w, int c, int ho,
                       int wo, int k, int s, int p, int dtype, void* stream);
 int rtsds_maxpool_bwd(const void* dy, const uint8_t* idx, void* dx, int n, int h, int w, int c,
@@ -217,6 +218,13 @@ int rtsds_gap_bwd(const void* dy, void* dx, int n, long hw, int c, int dtype, vo
  * mode 0: y = x*a[n][c] (build_bisenet.py:52,149); mode 1: y = x*a + x (build_bisenet.py:79-80).
  * Backward: dx (may be NULL), da[n][c] = sum_hw dy*x (may be NULL; needs
  * ws = rtsds_gap_workspace(n, hw, c) bytes).                                              */
+/* Inference tail of FeatureFusionModule + the final 1x1 conv (build_bisenet.py:75-80, 167), one
+ * launch: out = conv3(f * a + f) + b3 with a = sigmoid(conv2(relu(conv1(GAP(f)) + b1)) + b2);
+ * f / out NHWC [n][hw][c] (c = 19 -- the class maps -- and hw a multiple of the 16-B vector length,
+ * else RTSDS_ERR_UNSUPPORTED); w1..w3 [c][c] in the compute dtype, biases fp32 (NULL = 0).     */
+int rtsds_ffm_head_eval(const void* f, const void* w1, const float* b1, const void* w2, const float* b2,
+                        const void* w3, const float* b3, void* out, int n, long hw, int c, int dtype,
+                        void* stream);
 int rtsds_chscale_fwd(const void* x, const void* a, void* y, int n, long hw, int c, int mode,
                       int dtype, void* stream);
 int rtsds_chscale_bwd(const void* dy, const void* x, const void* a, void* dx, void* da, int n,
@@ -363,6 +371,23 @@ int rtsds_resize_aa(const void* src, int src_u8, int c, int h, int w, void* dst,
 int rtsds_gaussian_blur(const void* src, int src_u8, float* dst, int c, int h, int w, int kx, int ky,
                         float sigma_x, float sigma_y, void* stream);
 int rtsds_gta5_decode(const uint8_t* rgb, int64_t* out, int h, int w, void* stream);
+
+/* ---------------------------------------------------------------- graph replay
+ * Replaces hipGraphLaunch of a captured multi-stream iteration (runtime.GraphedStep /
+ * GraphedForward; the reference has no graphs: its train.py:65-113 / 172-284 loop bodies
+ * launch every ATen kernel from the host).  rtsds_graph_split decomposes a captured hipGraph
+ * (kernel / memcpy / memset / empty nodes) into at most max_lanes chains, cuts each chain at its
+ * cross-chain edges into linear segments and instantiates one executable graph per segment;
+ * rtsds_graph_split_launch replays them on one stream per chain (chain 0 = `stream`, which
+ * also waits for the other chains at the end), with events for the cross-chain edges.  The
+ * captured graph is only read (the caller keeps it and the memory it references alive).
+ * Returns RTSDS_ERR_UNSUPPORTED for other node types (the caller replays the graph itself). */
+int rtsds_graph_split(void* graph, int max_lanes, void** handle, int* n_segments, int* n_lanes);
+/* Number of chains (<= max_lanes) rtsds_graph_split would use for `graph` -- 1 for a linear
+ * (single-stream) capture; a negative RTSDS_ERR_* code on failure.  Nothing is instantiated. */
+int rtsds_graph_lanes(void* graph, int max_lanes);
+int rtsds_graph_split_launch(void* handle, void* stream);
+int rtsds_graph_split_destroy(void* handle);
 
 #ifdef __cplusplus
 }

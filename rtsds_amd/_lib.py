@@ -62,6 +62,11 @@ SIGNATURES = {
     "rtsds_nchw_to_nhwc": (c_int, [P, P, c_int, c_int, c_int, c_int, c_int, P]),
     "rtsds_nchw_to_nhwc_pad": (c_int, [P, P, c_int, c_int, c_int, c_int, c_int, c_int, P]),
     "rtsds_cast": (c_int, [P, c_int, P, c_int, c_long, P]),
+    "rtsds_ffm_head_eval": (c_int, [P, P, P, P, P, P, P, P, c_int, c_long, c_int, c_int, P]),
+    "rtsds_graph_split": (c_int, [P, c_int, P, P, P]),
+    "rtsds_graph_split_launch": (c_int, [P, P]),
+    "rtsds_graph_lanes": (c_int, [P, c_int]),
+    "rtsds_graph_split_destroy": (c_int, [P]),
     "rtsds_copy_channels": (c_int, [P, c_int, c_int, P, c_int, c_int, c_long, c_int, c_int, c_int, P]),
     "rtsds_act_fwd": (c_int, [P, P, c_long, c_int, c_int, P]),
     "rtsds_act_bwd": (c_int, [P, P, P, c_long, c_int, c_float, c_int, P]),

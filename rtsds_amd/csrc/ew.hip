@@ -360,6 +360,7 @@ __global__ void __launch_bounds__(256) maxpool_fwd_k3(const T* __restrict__ x, T
       ib |= (unsigned long long)(bi[j] < 0 ? 0 : bi[j]) << (8 * j);
     }
     *(V16*)(y + oi) = o;
+    if (idx == nullptr) continue;  // inference: no backward reads the argmax bytes
     if constexpr (V == 8) {
       *(unsigned long long*)(idx + oi) = ib;
     } else {
@@ -426,6 +427,8 @@ extern "C" int rtsds_maxpool_fwd(const void* x, void* y, uint8_t* idx, int n, in
     if (c % VecT<T>::N == 0 && k == 3 && total < (1L << 31))
       hipLaunchKernelGGL(maxpool_fwd_k3<T>, dim3(ew_blocks(total / VecT<T>::N, 256, 1 << 20)), dim3(256), 0, (hipStream_t)stream, (const T*)x, (T*)y, idx,
                          n, h, w, c, ho, wo, s, p, fastdiv_make(c / VecT<T>::N), fastdiv_make(wo), fastdiv_make(ho));
+    else if (idx == nullptr)
+      return RTSDS_ERR_UNSUPPORTED;
     else if (c % VecT<T>::N == 0)
       hipLaunchKernelGGL(maxpool_fwd_vec<T>, dim3(ew_blocks(total / VecT<T>::N)), dim3(256), 0, (hipStream_t)stream, (const T*)x, (T*)y, idx, n, h, w, c, ho, wo, k, s, p);
     else
@@ -607,6 +610,110 @@ extern "C" int rtsds_chscale_fwd(const void* x, const void* a, void* y, int n, l
   DISPATCH_T(dtype, hipLaunchKernelGGL(chscale_fwd_kernel<T>, dim3(ew_blocks(total)), dim3(256), 0, (hipStream_t)stream, (const T*)x, (const T*)a, (T*)y, n, hw, c, mode));
   RET_LAUNCH();
 }
+// Inference tail of the FeatureFusionModule plus BiSeNet's final 1x1 conv (build_bisenet.py:75-80,
+// 167): a = sigmoid(conv2(relu(conv1(GAP(f))))), r = f * a + f, out = conv(r) + bias, for a
+// narrow class map f [N][hw][C] (C <= 32).  Unfused these are 8 launches (two-stage GAP, two
+// pooled 1x1 convs, the channel scale, two channel pads and the padded GEMM: ~54 us at bs 8,
+// all launch-bound).  Grid (chunks, N): every workgroup reduces its image's GAP itself (the
+// image's map is ~0.3 MB, L2-resident) with 16-B loads of V-pixel groups (C vectors whose
+// element -> channel map is static), evaluates the two pooled convs in LDS, then stages its
+// chunk of pixels in LDS (coalesced 16-B loads), maps each pixel in place (one pixel per
+// thread, the C x C head weights in LDS) and writes the chunk back with 16-B stores.  Each
+// intermediate is rounded to T where the unfused chain stores it.
+template <typename T, int C>
+__global__ void __launch_bounds__(256) ffm_head_eval_kernel(const T* __restrict__ f, const T* __restrict__ w1,
+                                                            const float* __restrict__ b1, const T* __restrict__ w2,
+                                                            const float* __restrict__ b2, const T* __restrict__ w3,
+                                                            const float* __restrict__ b3, T* __restrict__ out, int hw, int chunk) {
+  typedef typename VecT<T>::v16 V16;
+  constexpr int V = VecT<T>::N;
+  __shared__ float red[256][C + 1];
+  __shared__ float wl[3][C][C + 1];
+  __shared__ float gap[C], hid[C], att[C], bias3[C];
+  extern __shared__ __attribute__((aligned(16))) unsigned char stage_raw[];
+  T* stage = (T*)stage_raw;  // [chunk][C]
+  const int tid = threadIdx.x, img = blockIdx.y;
+  const T* fi = f + (long)img * hw * C;
+  for (int e = tid; e < C * C; e += 256) {
+    const int o = e / C, i = e - o * C;
+    wl[0][o][i] = to_f(w1[e]);
+    wl[1][o][i] = to_f(w2[e]);
+    wl[2][o][i] = to_f(w3[e]);
+  }
+  float s[C];
+#pragma unroll
+  for (int ch = 0; ch < C; ++ch) s[ch] = 0.f;
+  const int groups = hw / V;  // hw % V == 0 (host)
+  for (int g = tid; g < groups; g += 256) {
+    const V16* q = (const V16*)(fi + (long)g * V * C);
+    V16 v[C];
+#pragma unroll
+    for (int k = 0; k < C; ++k) v[k] = q[k];
+#pragma unroll
+    for (int k = 0; k < C; ++k)
+#pragma unroll
+      for (int j = 0; j < V; ++j) s[(k * V + j) % C] += to_f(v[k][j]);
+  }
+#pragma unroll
+  for (int ch = 0; ch < C; ++ch) red[tid][ch] = s[ch];
+  __syncthreads();
+  if (tid < C) {  // fixed-order reduction over the 256 thread partials
+    float t = 0.f;
+    for (int r = 0; r < 256; ++r) t += red[r][tid];
+    gap[tid] = to_f(from_f<T>(t / (float)hw));
+    bias3[tid] = b3 ? b3[tid] : 0.f;
+  }
+  __syncthreads();
+  if (tid < C) {
+    float v = b1 ? b1[tid] : 0.f;
+    for (int i = 0; i < C; ++i) v = fmaf(wl[0][tid][i], gap[i], v);
+    hid[tid] = to_f(from_f<T>(fmaxf(v, 0.f)));
+  }
+  __syncthreads();
+  if (tid < C) {
+    float v = b2 ? b2[tid] : 0.f;
+    for (int i = 0; i < C; ++i) v = fmaf(wl[1][tid][i], hid[i], v);
+    att[tid] = to_f(from_f<T>(1.f / (1.f + expf(-v))));
+  }
+  const int p0 = blockIdx.x * chunk, np = min(chunk, hw - p0);  // np % V == 0
+  const int nvec = np * C / V;
+  const V16* src = (const V16*)(fi + (long)p0 * C);
+  for (int e = tid; e < nvec; e += 256) ((V16*)stage)[e] = src[e];
+  __syncthreads();
+  for (int p = tid; p < np; p += 256) {
+    T* q = stage + p * C;
+    float r[C];
+#pragma unroll
+    for (int i = 0; i < C; ++i) {
+      const float x = to_f(q[i]);
+      r[i] = to_f(from_f<T>(fmaf(x, att[i], x)));
+    }
+#pragma unroll
+    for (int k = 0; k < C; ++k) {
+      float v = bias3[k];
+#pragma unroll
+      for (int i = 0; i < C; ++i) v = fmaf(wl[2][k][i], r[i], v);
+      q[k] = from_f<T>(v);
+    }
+  }
+  __syncthreads();
+  V16* dst = (V16*)(out + ((long)img * hw + p0) * C);
+  for (int e = tid; e < nvec; e += 256) dst[e] = ((const V16*)stage)[e];
+}
+extern "C" int rtsds_ffm_head_eval(const void* f, const void* w1, const float* b1, const void* w2, const float* b2,
+                                   const void* w3, const float* b3, void* out, int n, long hw, int c, int dtype,
+                                   void* stream) {
+  if (n <= 0 || hw <= 0 || hw >= (1L << 31)) return RTSDS_ERR_SHAPE;
+  if (c != 19) return RTSDS_ERR_UNSUPPORTED;  // instantiated for the 19-class maps
+  const int V = dtype == RTSDS_BF16 ? 8 : 4;
+  if (hw % V) return RTSDS_ERR_UNSUPPORTED;
+  const int chunk = dtype == RTSDS_BF16 ? 1024 : 512;  // 38 KB of staged pixels
+  const int chunks = (int)((hw + chunk - 1) / chunk);
+  const size_t lds = (size_t)chunk * c * (dtype == RTSDS_BF16 ? 2 : 4);
+  DISPATCH_T(dtype, hipLaunchKernelGGL((ffm_head_eval_kernel<T, 19>), dim3(chunks, n), dim3(256), lds, (hipStream_t)stream, (const T*)f,
+                                       (const T*)w1, b1, (const T*)w2, b2, (const T*)w3, b3, (T*)out, (int)hw, chunk));
+  RET_LAUNCH();
+}
 extern "C" int rtsds_chscale_bwd(const void* dy, const void* x, const void* a, void* dx, void* da, int n, long hw, int c, int mode,
                                  int dtype, void* ws, size_t ws_bytes, void* stream) {
   const long total = (long)n * hw * c;
@@ -734,6 +841,55 @@ __global__ void bilinear_fwd_kernel(const T* __restrict__ x, T* __restrict__ y, 
       for (int ch = cs; ch < ce; ++ch)
         o[ch] = from_f<T>(bil_mix(to_f(p00[ch]), to_f(p01[ch]), to_f(p10[ch]), to_f(p11[ch]), lh0, lh1, lw0, lw1));
     }
+  }
+}
+
+// Narrow channel counts that are not a 16-B multiple (the 19-class logits of the eval forward's
+// final x8 resize, build_bisenet.py:165-166): one workgroup per output row.  The row's two source
+// rows are staged in LDS as fp32 (coalesced), then every thread writes whole 16-B vectors of the
+// dense output row (a wave writes 1 KB contiguously; the whole-pixel loop wrote 38-B runs at a
+// 38-B lane stride, 1.8 TB/s) from 4 LDS taps per element.  Same taps, weights and bil_mix
+// expression as the other modes.
+template <typename T>
+__global__ void __launch_bounds__(256) bilinear_fwd_rows_kernel(const T* __restrict__ x, T* __restrict__ y, int hi, int wi, int c,
+                                                                 int ho, int wo, float sh, float sw, FastDiv f_c) {
+  typedef typename VecT<T>::v16 V16;
+  constexpr int V = VecT<T>::N;
+  extern __shared__ float rows[];  // [2][wi * c]
+  const int row = blockIdx.x, img = row / ho, oh = row - img * ho;
+  int h0, h1;
+  float lh0, lh1;
+  bil_src(oh, sh, hi, h0, h1, lh0, lh1);
+  const int rl = wi * c;
+  const T* r0 = x + ((long)img * hi + h0) * rl;
+  const T* r1 = x + ((long)img * hi + h1) * rl;
+  for (int e = threadIdx.x; e < rl; e += 256) {
+    rows[e] = to_f(r0[e]);
+    rows[rl + e] = to_f(r1[e]);
+  }
+  __syncthreads();
+  const int nv = wo * c / V;  // (wo * c) % V == 0 (host)
+  T* yo = y + (long)row * wo * c;
+  for (int v = threadIdx.x; v < nv; v += 256) {
+    const int e = v * V;
+    int ow = (int)fdiv((uint32_t)e, f_c), ch = e - ow * c;
+    int w0, w1;
+    float lw0, lw1;
+    bil_src(ow, sw, wi, w0, w1, lw0, lw1);
+    V16 r;
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+      if (ch == c) {
+        ch = 0;
+        ++ow;
+        bil_src(ow, sw, wi, w0, w1, lw0, lw1);
+      }
+      const float* a = rows + w0 * c + ch;
+      const float* b = rows + w1 * c + ch;
+      r[k] = from_f<T>(bil_mix(a[0], b[0], a[rl], b[rl], lh0, lh1, lw0, lw1));
+      ++ch;
+    }
+    *(V16*)(yo + e) = r;
   }
 }
 
@@ -893,6 +1049,9 @@ extern "C" int rtsds_bilinear_fwd(const void* x, void* y, int n, int hi, int wi,
     const long pix = (long)n * ho * wo;
     if (c % V == 0 && y_ld % V == 0 && y_off % V == 0)
       hipLaunchKernelGGL((bilinear_fwd_kernel<T, 0>), dim3(ew_blocks(pix * (c / V))), dim3(256), 0, st, (const T*)x, (T*)y, n, hi, wi, c, ho, wo, scale_h, scale_w, y_ld, y_off);
+    else if (c >= V && y_ld == c && y_off == 0 && (wo * c) % V == 0 && 2L * wi * c * 4 <= 64 * 1024)
+      hipLaunchKernelGGL((bilinear_fwd_rows_kernel<T>), dim3(n * ho), dim3(256), 2 * wi * c * 4, st, (const T*)x, (T*)y, hi, wi, c, ho,
+                         wo, scale_h, scale_w, fastdiv_make(c));
     else if (c <= 64)
       hipLaunchKernelGGL((bilinear_fwd_kernel<T, 1>), dim3(ew_blocks(pix)), dim3(256), 0, st, (const T*)x, (T*)y, n, hi, wi, c, ho, wo, scale_h, scale_w, y_ld, y_off);
     else

@@ -11,8 +11,8 @@ import numpy as np
 import torch
 
 from ._lib import ACT_RELU, ACT_SIGMOID, INPUT_PADDED, WEIGHT_PACKED, ConvDesc, lib
-from .runtime import (CL, collective, dcode, dp_world, empty_nhwc, nhwc, require_hip, side_enabled, side_fork,
-                      stream, workspace)
+from .runtime import (CL, bump_params_epoch, collective, dcode, dp_world, empty_nhwc, nhwc, params_epoch,
+                      register_fold, require_hip, side_enabled, side_fork, stream, workspace)
 
 _P = lambda t: None if t is None else t.data_ptr()  # noqa: E731
 
@@ -306,6 +306,36 @@ def conv2d(x, weight, bias, wq, stride=(1, 1), padding=(0, 0), dilation=(1, 1), 
     return y
 
 
+def _bn_fold(gamma, beta, running_mean, running_var, bias, eps, k):
+    """Eval-mode BatchNorm folded with the conv bias into [scale | shift] (rtsds_bn_fold), cached
+    on the running-mean tensor: recomputed -- in place, so captured graphs keep reading the
+    same buffer -- only when a parameter / statistic changed (tensor versions for torch-side
+    writes, runtime.params_epoch for the rtsds optimizer and train-mode BatchNorm, which write
+    through raw pointers).  A GraphedForward capture registers the refresh, run before every
+    replay."""
+    ts = (gamma, beta, running_mean, running_var, bias)
+
+    def key():
+        return (params_epoch(), float(eps)) + tuple((t.data_ptr(), t._version) if t is not None else None for t in ts)
+
+    ent = getattr(running_mean, "_rt_fold", None)
+    if ent is None or ent[1].numel() != 2 * k or ent[1].device != running_mean.device:
+        ent = [None, torch.empty(2 * k, dtype=torch.float32, device=running_mean.device)]
+        running_mean._rt_fold = ent
+    ss = ent[1]
+
+    def refresh():
+        kk = key()
+        if ent[0] != kk:
+            lib.rtsds_bn_fold(_P(gamma), _P(beta), _P(running_mean), _P(running_var), _P(bias), float(eps), k,
+                              _P(ss), ss.data_ptr() + 4 * k, stream())
+            ent[0] = kk
+
+    refresh()
+    register_fold(refresh)
+    return ss
+
+
 def conv_bn_eval(x, weight, bias, wq, stride, padding, dilation, gamma, beta, running_mean, running_var,
                  eps, act=0, residual=None):
     """Inference (no autograd) conv -> BatchNorm(running statistics) [-> + residual] [-> act]
@@ -319,9 +349,7 @@ def conv_bn_eval(x, weight, bias, wq, stride, padding, dilation, gamma, beta, ru
     if not flag:
         x = nhwc(x)
     d = _conv_desc(x, k, kh, kw, stride, padding, dilation)
-    ss = torch.empty(2 * k, dtype=torch.float32, device=x.device)
-    lib.rtsds_bn_fold(_P(gamma), _P(beta), _P(running_mean), _P(running_var), _P(bias), float(eps), k,
-                      _P(ss), ss.data_ptr() + 4 * k, stream())
+    ss = _bn_fold(gamma, beta, running_mean, running_var, bias, eps, k)
     if residual is not None:
         residual = nhwc(residual)
         if residual.dtype != x.dtype or tuple(residual.shape) != (d.n, k, d.ho, d.wo):
@@ -495,6 +523,8 @@ def batch_norm(x, gamma, beta, running_mean, running_var, training, momentum, ep
     ``res_join``: GradJoin shared with the other readers of ``residual``."""
     st = getattr(x, "_rt_bn_stats", None) if training else None
     stats, nrb = st if st is not None else (None, None)
+    if training and running_mean is not None:
+        bump_params_epoch()  # running statistics change (raw-pointer write)
     return BatchNormFn.apply(x, gamma, beta, residual, running_mean, running_var, training,
                              momentum, eps, act, stats, nrb, num_batches_tracked, res_join, link)
 
@@ -592,6 +622,41 @@ class CatFn(torch.autograd.Function):
         return tuple(outs)
 
 
+def concat_resized(x0, xs, size):
+    """Inference only (no autograd): cat([x0] + [interpolate_bilinear(x, size) for x in xs],
+    dim=1) with each resize written straight into its channel slice of the output
+    (rtsds_bilinear_fwd's output pitch / offset) -- x0 (already at ``size``) is the one copy."""
+    x0 = nhwc(x0)
+    n, c0, h, w = x0.shape
+    if (h, w) != (int(size[0]), int(size[1])):
+        raise RuntimeError("rtsds_amd.concat_resized: x0 must have the target size")
+    xs = [nhwc(x) for x in xs]
+    ct = c0 + sum(x.shape[1] for x in xs)
+    y = empty_nhwc(n, ct, h, w, x0.dtype, x0.device)
+    lib.rtsds_copy_channels(_P(x0), c0, 0, _P(y), ct, 0, n * h * w, c0, 0, dcode(x0), stream())
+    off = c0
+    for x in xs:
+        _, c, hi, wi = x.shape
+        ho, wo, sh, sw = upsample_geometry(x, size=size)
+        lib.rtsds_bilinear_fwd(_P(x), _P(y), n, hi, wi, c, ho, wo, sh, sw, ct, off, dcode(x), stream())
+        off += c
+    return y
+
+
+def ffm_head_eval(feature, w1, b1, w2, b2, w3, b3):
+    """Inference only: conv3(f * a + f) + b3 with a = sigmoid(conv2(relu(conv1(GAP(f)) + b1)) + b2)
+    -- FeatureFusionModule's attention tail and BiSeNet's final 1x1 conv (build_bisenet.py:75-80,
+    167) in one launch (rtsds_ffm_head_eval).  w*: [c, c, 1, 1] weights in the feature's dtype."""
+    f = nhwc(feature)
+    n, c, h, w = f.shape
+    out = empty_nhwc(n, c, h, w, f.dtype, f.device)
+    ws = [t.reshape(c, c).contiguous() for t in (w1, w2, w3)]
+    bs = [None if b is None else b.float().contiguous() for b in (b1, b2, b3)]
+    lib.rtsds_ffm_head_eval(_P(f), _P(ws[0]), _P(bs[0]), _P(ws[1]), _P(bs[1]), _P(ws[2]), _P(bs[2]), _P(out), n, h * w, c,
+                            dcode(f), stream())
+    return out
+
+
 def cat(xs, joins=None):
     """``joins``: per-input GradJoin (or None) for inputs that have other readers."""
     return CatFn.apply(joins, *xs)
@@ -666,7 +731,9 @@ class MaxPoolFn(torch.autograd.Function):
         n, c, h, w = x.shape
         ho, wo = pool_out(h, k, s, p, ceil_mode), pool_out(w, k, s, p, ceil_mode)
         y = empty_nhwc(n, c, ho, wo, x.dtype, x.device)
-        idx = torch.empty((n, ho, wo, c), dtype=torch.uint8, device=x.device)
+        # inference (no gradient): the argmax bytes are not written where the kernel allows it
+        need = ctx.needs_input_grad[0] or not (k == 3 and c % (8 if x.dtype == torch.bfloat16 else 4) == 0)
+        idx = torch.empty((n, ho, wo, c), dtype=torch.uint8, device=x.device) if need else None
         lib.rtsds_maxpool_fwd(_P(x), _P(y), _P(idx), n, h, w, c, ho, wo, k, s, p, dcode(x), stream())
         ctx.geo = (n, h, w, c, ho, wo, k, s, p)
         ctx.dtype = x.dtype
@@ -752,6 +819,8 @@ def bn_relu_maxpool(x, gamma, beta, running_mean, running_var, training, momentu
                     num_batches_tracked=None):
     st = getattr(x, "_rt_bn_stats", None) if training else None
     stats, nrb = st if st is not None else (None, None)
+    if training and running_mean is not None:
+        bump_params_epoch()  # running statistics change (raw-pointer write)
     return BnReluMaxPoolFn.apply(x, gamma, beta, running_mean, running_var, training, momentum, eps, stats, nrb,
                                  num_batches_tracked, p, ceil_mode)
 

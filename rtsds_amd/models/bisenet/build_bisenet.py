@@ -12,7 +12,7 @@ import torch
 from torch import nn
 
 from rtsds_amd import functional as F
-from rtsds_amd.nn import AdaptiveAvgPool2d, BatchNorm2d, Conv2d, ReLU, Sigmoid, conv_bn, grad_join, to_input
+from rtsds_amd.nn import AdaptiveAvgPool2d, BatchNorm2d, Conv2d, ReLU, Sigmoid, _shadow, conv_bn, to_input
 from rtsds_amd.runtime import BranchOut, branch_stream, branches_enabled
 
 from .build_contextpath import build_contextpath
@@ -57,8 +57,11 @@ class AttentionRefinementModule(torch.nn.Module):
         self.in_channels = in_channels
         self.avgpool = AdaptiveAvgPool2d(output_size=(1, 1))
 
-    def forward(self, input):
-        pooled = self.avgpool(input)
+    def forward(self, input, pooled=None):
+        """``pooled``: GAP(input) when the caller already has it (BiSeNet's ARM2 reads the
+        context path's tail, the same kernel on the same tensor)."""
+        if pooled is None:
+            pooled = self.avgpool(input)
         assert self.in_channels == pooled.size(1), \
             "in_channels and out_channels should all be {}".format(pooled.size(1))
         att = conv_bn(self.conv, self.bn, pooled, "sigmoid")
@@ -78,12 +81,16 @@ class FeatureFusionModule(torch.nn.Module):
         self.sigmoid = Sigmoid()
         self.avgpool = AdaptiveAvgPool2d(output_size=(1, 1))
 
-    def forward(self, input_1, input_2, joins=None):
+    def forward(self, input_1, input_2=None, joins=None):
         # input_2 may be the (cx1, cx2) pair itself: one concat pass instead of the
         # reference's nested cat (build_bisenet.py:153 then :72), same channel order.
-        # joins: GradJoin per concatenated input (functional.cat)
-        parts = [input_1, *input_2] if isinstance(input_2, (tuple, list)) else [input_1, input_2]
-        x = F.cat(parts, joins)
+        # joins: GradJoin per concatenated input (functional.cat).  input_2 None: input_1 is
+        # the concatenation already (BiSeNet's inference path writes it in place).
+        if input_2 is None:
+            x = input_1
+        else:
+            parts = [input_1, *input_2] if isinstance(input_2, (tuple, list)) else [input_1, input_2]
+            x = F.cat(parts, joins)
         assert self.in_channels == x.size(1), \
             "in_channels of ConvBlock should be {}".format(x.size(1))
         feature = self.convblock(x)
@@ -100,6 +107,9 @@ class BiSeNet(torch.nn.Module):
     # training: spatial path on runtime.branch_stream beside the context path (bs 8 train step
     # +2.5 %; at inference the fork / join edges cost more than the overlap gains)
     branch_parallel = True
+    # inference (eval, no autograd): resizes written into the fusion module's concatenated input
+    # and the attention tail + final 1x1 conv fused (False: the separate ops, for A/B tests)
+    inference_fusions = True
 
     def __init__(self, num_classes, context_path, with_interpolation=True):
         super().__init__()
@@ -159,21 +169,44 @@ class BiSeNet(torch.nn.Module):
             sx = self.saptial_path(x)
             f3, f4, tail = self.context_path(x)
         cx1 = self.attention_refinement_module1(f3)
-        cx2 = F.channel_scale(self.attention_refinement_module2(f4), tail)
+        # ARM2's global average pool is the tail itself (same kernel, same f4)
+        cx2 = F.channel_scale(self.attention_refinement_module2(f4, pooled=tail), tail)
         hw = sx.shape[-2:]
+        heads = []
+        if self.inference_fusions and not self.training and not torch.is_grad_enabled() and \
+                sx.shape[1] + cx1.shape[1] + cx2.shape[1] == self.feature_fusion_module.in_channels:
+            # inference: the two resizes write straight into the fusion module's concatenated
+            # input (no cat pass over them; the reference: interpolate, interpolate, cat)
+            cat = F.concat_resized(sx, (cx1, cx2), hw)
+            ffm = self.feature_fusion_module
+            if self.with_interpolation and ffm.conv1.out_channels == 19 and \
+                    (hw[0] * hw[1]) % (8 if sx.dtype == torch.bfloat16 else 4) == 0 and \
+                    all(m.kernel_size == (1, 1) and m.in_channels == m.out_channels == ffm.conv1.in_channels
+                        for m in (ffm.conv1, ffm.conv2, self.conv)):
+                # attention tail + final 1x1 conv as one launch (functional.ffm_head_eval)
+                feature = ffm.convblock(cat)
+                ws = [_shadow(m.weight, feature.dtype) for m in (ffm.conv1, ffm.conv2, self.conv)]
+                main = F.ffm_head_eval(feature, ws[0], ffm.conv1.bias, ws[1], ffm.conv2.bias, ws[2], self.conv.bias)
+                return [(main, F.upsample_geometry(main, scale_factor=8))]
+            result = ffm(cat)
+            if self.with_interpolation:
+                main = self.conv(result)
+                return [(main, F.upsample_geometry(main, scale_factor=8))]
+            return [(result, None)]
+        aux_on = self.training and not main_only
+        if aux_on:
+            # reference: supervision_i(interpolate(cx_i)) (build_bisenet.py:151-152, 156-157).  The
+            # 1x1 conv commutes with the bilinear resize (as the main head's, below), so each
+            # supervision conv runs on the un-resized map -- 1/4 (cx1) and 1/16 (cx2) of the
+            # pixels, without reading the resized 256 / 512-channel maps -- and its 19-channel
+            # output is resized instead; the loss then resizes it to full resolution as before.
+            full = input.shape[-2:]
+            s1 = F.interpolate_bilinear(self.supervision1(cx1), size=hw)
+            s2 = F.interpolate_bilinear(self.supervision2(cx2), size=hw)
+            aux = [(s1, F.upsample_geometry(s1, size=full)), (s2, F.upsample_geometry(s2, size=full))]
         cx1 = F.interpolate_bilinear(cx1, size=hw)
         cx2 = F.interpolate_bilinear(cx2, size=hw)
-        heads = []
-        aux_on = self.training and not main_only
         joins = None
-        if aux_on:
-            # cx1 / cx2 are read by the concat and by a supervision conv: their gradients
-            # meet in one buffer (nn.grad_join) instead of an autograd add
-            j1, j2 = grad_join(cx1, 2), grad_join(cx2, 2)
-            joins = (None, j1, j2)
-            full = input.shape[-2:]
-            s1, s2 = self.supervision1(cx1, join=j1), self.supervision2(cx2, join=j2)
-            aux = [(s1, F.upsample_geometry(s1, size=full)), (s2, F.upsample_geometry(s2, size=full))]
         result = self.feature_fusion_module(sx, (cx1, cx2), joins)
         if self.with_interpolation:
             # reference: conv(up8(result)) (build_bisenet.py:165-167).  A 1x1 conv mixes channels

@@ -26,7 +26,7 @@ import torch
 import torch.distributed as dist
 
 from ._lib import ConvDesc, lib
-from .runtime import collective, dp_world, stream
+from .runtime import bump_params_epoch, collective, dp_world, stream
 
 
 _ALLREDUCE = {"dtype": torch.float32}
@@ -299,6 +299,7 @@ class _FlatOptimizer(torch.optim.Optimizer):
     def step(self, closure=None):
         loss = closure() if closure is not None else None
         arenas = self._ensure()
+        bump_params_epoch()  # the update writes the arenas through raw pointers
         if self._finish is not None:
             self._finish()
             self._finish = None

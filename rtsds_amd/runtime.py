@@ -6,6 +6,7 @@
 """
 import contextlib
 import os
+import time
 
 import torch
 
@@ -64,6 +65,21 @@ def require_hip(*tensors):
         if t is not None and not t.is_cuda:
             raise RuntimeError("rtsds_amd: ops run only on HIP (MI355X) tensors; "
                                "there is no CPU fallback (move the model / data to 'cuda')")
+
+
+# Parameter epoch: advanced by every rtsds writer that updates parameters / BatchNorm running
+# statistics through raw device pointers (which torch's tensor versions do not see): the
+# optimizer step, a replayed training iteration, a train-mode BatchNorm forward.  Caches of
+# values derived from parameters (the eval-mode BatchNorm folds) are keyed on it.
+_epoch = [0]
+
+
+def bump_params_epoch():
+    _epoch[0] += 1
+
+
+def params_epoch():
+    return _epoch[0]
 
 
 CL = torch.channels_last
@@ -202,6 +218,69 @@ class BranchOut(torch.autograd.Function):
         return g, None, None
 
 
+# Submission of captured graphs.  hipGraphLaunch of a graph captured from several streams (the
+# branch streams) takes the runtime's multi-queue path and enqueues node by node: ~4.7 ms of
+# host time per BiSeNet bs-8 step (~330 nodes) -- hidden while the GPU needs 5.7 ms, but a
+# ceiling once the kernels get faster -- whereas a linear (single-stream) graph goes out as
+# one pre-recorded packet batch (~0.2 ms).  Measured on the bs-8 step (round 3,
+# profiles/r3_graph_submit.txt): multi-stream graph 5.67 ms wall / 4.7 ms host, the same
+# iteration captured serially 5.85 / 0.23, and the multi-stream capture replayed as per-stream
+# linear segment graphs joined by events (rtsds_graph_split, csrc/graph.hip) 6.11 / 0.41 -- each
+# segment launch and cross-queue wait costs ~20 us of GPU idle time.  GraphedStep therefore
+# captures both the branch-stream and the serial variant and keeps whichever runs faster
+# (submit="auto"); "split" remains selectable.
+SUBMIT = {"mode": "auto", "max_lanes": 4, "trial_calls": 3}
+
+
+def graph_lanes(graph):
+    """Stream chains of a captured graph (1 = linear)."""
+    import ctypes
+    from ._lib import load
+    n = load().rtsds_graph_lanes(ctypes.c_void_p(graph.raw_cuda_graph()), int(SUBMIT["max_lanes"]))
+    if n < 1:
+        raise RuntimeError(f"rtsds_amd: rtsds_graph_lanes failed (status {-n})")
+    return n
+
+
+class GraphRunner:
+    """Replays one captured torch.cuda.CUDAGraph(keep_graph=True) -- as lane-split linear
+    segments (rtsds_graph_split) when ``split`` and the capture forked streams, else the graph
+    itself.  Keeps the graph (and its memory pool) alive."""
+
+    def __init__(self, graph, split=False):
+        import ctypes
+        from ._lib import load
+        self.graph, self.handle, self.segments = graph, None, 1
+        self.lanes = graph_lanes(graph)
+        if split and self.lanes > 1:
+            lib = load()
+            h, ns, nl = ctypes.c_void_p(), ctypes.c_int(0), ctypes.c_int(0)
+            rc = lib.rtsds_graph_split(ctypes.c_void_p(graph.raw_cuda_graph()), int(SUBMIT["max_lanes"]),
+                                       ctypes.byref(h), ctypes.byref(ns), ctypes.byref(nl))
+            if rc == 0:
+                self.handle, self.segments = h, ns.value
+            elif rc != 2:  # RTSDS_ERR_UNSUPPORTED node type: replay the graph itself
+                raise RuntimeError(f"rtsds_amd: rtsds_graph_split failed (status {rc})")
+        if self.handle is None:
+            graph.instantiate()
+
+    def replay(self):
+        if self.handle is not None:
+            from ._lib import lib
+            lib.rtsds_graph_split_launch(self.handle, stream())
+        else:
+            self.graph.replay()
+
+    def __del__(self):
+        h, self.handle = getattr(self, "handle", None), None
+        if h is not None:
+            try:
+                from ._lib import load
+                load().rtsds_graph_split_destroy(h)
+            except Exception:  # interpreter shutdown
+                pass
+
+
 class GraphedForward:
     """hipGraph capture of a fixed-shape inference forward (torch.cuda.CUDAGraph is a hipGraph
     on ROCm): every rtsds kernel of ``module(x)`` is recorded once on a side stream and the
@@ -219,19 +298,34 @@ class GraphedForward:
             for _ in range(warmup):  # settle lazy allocations (bf16 shadows, workspaces)
                 module(self.static_in)
         torch.cuda.current_stream(x.device).wait_stream(side)
-        self.graph = torch.cuda.CUDAGraph()
-        with torch.no_grad(), torch.cuda.graph(self.graph, capture_error_mode=CAPTURE_MODE):
-            self.static_out = module(self.static_in)
+        self.graph = torch.cuda.CUDAGraph(keep_graph=True)
+        _fold_capture.append([])
+        try:
+            with torch.no_grad(), torch.cuda.graph(self.graph, capture_error_mode=CAPTURE_MODE):
+                self.static_out = module(self.static_in)
+        finally:
+            self.folds = _fold_capture.pop()
+        self.runner = GraphRunner(self.graph)
 
     def __call__(self, x):
         if x.shape != self.static_in.shape or x.dtype != self.static_in.dtype:
             raise RuntimeError("GraphedForward: input shape/dtype differs from the captured one")
         self.static_in.copy_(x)
-        self.graph.replay()
+        for refresh in self.folds:  # BatchNorm folds the graph reads (recomputed if stale)
+            refresh()
+        self.runner.replay()
         return self.static_out
 
 
 _capture = {"step": None}  # the GraphedStep currently capturing, if any
+# GraphedForward captures in progress: each collects the refresh callables of the cached
+# BatchNorm folds its graph reads (functional.conv_bn_eval)
+_fold_capture = []
+
+
+def register_fold(refresh):
+    if _fold_capture:
+        _fold_capture[-1].append(refresh)
 
 
 def collective(fn):
@@ -262,15 +356,23 @@ class GraphedStep:
     replay runs segment, collective, segment, ... -- so a data-parallel step is replayed too,
     with its RCCL calls issued eagerly between the graphs."""
 
-    def __init__(self, fn, optimizers, warmup=2):
+    def __init__(self, fn, optimizers, warmup=2, submit=None):
+        """``submit``: "auto" (default, SUBMIT["mode"]): capture the iteration with its branch
+        streams and, if it forked, a second time serially; the first trial_calls replays of each
+        are timed (host submission time and GPU time, HIP events) and the faster variant --
+        max(host, GPU) per step -- is kept.  Both compute bit-identical results, so the trial
+        replays are ordinary training steps.  "branches" / "serial" / "split": that variant only."""
         self.fn = fn
         self.optimizers = list(optimizers)
+        mode = submit or SUBMIT["mode"]
+        if mode not in ("auto", "branches", "serial", "split"):
+            raise ValueError(f"GraphedStep: unknown submit mode {mode!r}")
         for o in self.optimizers:
             o.set_graph_mode(True)
         cur = torch.cuda.current_stream()
         side = torch.cuda.Stream(device=cur.device)
         side.wait_stream(cur)
-        with torch.cuda.stream(side):
+        with torch.cuda.stream(side), (branches_serial() if mode == "serial" else contextlib.nullcontext()):
             for _ in range(warmup):
                 fn()
         cur.wait_stream(side)
@@ -279,21 +381,36 @@ class GraphedStep:
                 raise RuntimeError("GraphedStep: run one eager iteration before capturing")
             o.stage_hyper()  # allocates the device hyper buffer outside the capture
         torch.cuda.synchronize()
+        self._pool = torch.cuda.graph_pool_handle()  # shared by the variants (never run concurrently)
+        self.variants = []  # [(name, segments [(graph, collective)], runners, outputs)]
+        first = "serial" if mode == "serial" else ("split" if mode == "split" else "branches")
+        self._add_variant(first, fn, serial=first == "serial", split=first == "split")
+        if mode == "auto" and max(r.lanes for r, _ in self.variants[0][2]) > 1:
+            self._add_variant("serial", fn, serial=True, split=False)
+        self._use(0)
+        self._trial = [[] for _ in self.variants] if len(self.variants) > 1 else None
+        self._calls = 0
+        self.submit_choice = self.variants[0][0] if self._trial is None else None
+        self.submit_trials = {}
+        self.host_launch_s = 0.0  # host time spent submitting replays (bench.py)
+
+    def _add_variant(self, name, fn, serial, split):
+        cur = torch.cuda.current_stream()
         self.segments = []  # [(graph, collective run after it or None)]
-        self._pool = torch.cuda.graph_pool_handle()
         cap_stream = torch.cuda.Stream(device=cur.device)
+        cap_stream.wait_stream(cur)
         # the capture runs the optimizers' Python bookkeeping (step counters) without executing
         # a step: their counters are restored afterwards, also when the capture fails part-way
         saved = [o.steps_snapshot() for o in self.optimizers]
         for o in self.optimizers:
             o._capturing = True
         try:
-            with torch.cuda.stream(cap_stream):
-                self._graph = torch.cuda.CUDAGraph()
+            with torch.cuda.stream(cap_stream), (branches_serial() if serial else contextlib.nullcontext()):
+                self._graph = torch.cuda.CUDAGraph(keep_graph=True)
                 self._graph.capture_begin(pool=self._pool, capture_error_mode=CAPTURE_MODE)
                 _capture["step"] = self
                 try:
-                    self.outputs = fn()
+                    outputs = fn()
                 finally:
                     _capture["step"] = None
                     self._graph.capture_end()
@@ -303,20 +420,58 @@ class GraphedStep:
                 o._capturing = False
                 o.restore_steps(st)
         cur.wait_stream(cap_stream)
+        runners = [(GraphRunner(g, split=split), coll) for g, coll in self.segments]
+        self.variants.append((name, self.segments, runners, outputs))
+
+    def _use(self, i):
+        self.variant = self.variants[i][0]
+        self.segments, self.runners, self.outputs = self.variants[i][1], self.variants[i][2], self.variants[i][3]
         self.graph = self.segments[0][0]
 
     def _break(self, coll):
         self._graph.capture_end()
         self.segments.append((self._graph, coll))
-        self._graph = torch.cuda.CUDAGraph()
+        self._graph = torch.cuda.CUDAGraph(keep_graph=True)
         self._graph.capture_begin(pool=self._pool, capture_error_mode=CAPTURE_MODE)
 
     def __call__(self):
         for o in self.optimizers:
             o.stage_hyper()
             o.advance_steps()
-        for g, coll in self.segments:
-            g.replay()
+        bump_params_epoch()
+        trial = self._trial is not None
+        if trial:  # trial replays: trial_calls per variant, timed
+            vi = self._calls // int(SUBMIT["trial_calls"])
+            self._use(vi)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+        t0 = time.perf_counter()
+        for r, coll in self.runners:
+            r.replay()
             if coll is not None:
                 coll()
+        dt = time.perf_counter() - t0
+        self.host_launch_s += dt
+        if trial:
+            e1.record()
+            self._trial[vi].append((dt, e0, e1))
+            self._calls += 1
+            if self._calls == int(SUBMIT["trial_calls"]) * len(self.variants):
+                self._decide()
         return self.outputs
+
+    def _decide(self):
+        """Keep the variant with the smaller max(host submission, GPU) time per step (the first
+        trial replay of each is a warm-up)."""
+        torch.cuda.synchronize()
+        costs = []
+        for (name, *_), rec in zip(self.variants, self._trial):
+            use = rec[1:] if len(rec) > 1 else rec
+            host = 1e3 * sum(r[0] for r in use) / len(use)
+            gpu = sum(r[1].elapsed_time(r[2]) for r in use) / len(use)
+            self.submit_trials[name] = {"host_ms": round(host, 3), "gpu_ms": round(gpu, 3)}
+            costs.append(max(host, gpu))
+        best = min(range(len(costs)), key=costs.__getitem__)
+        self._use(best)
+        self.submit_choice = self.variants[best][0]
+        self._trial = None

@@ -336,12 +336,18 @@ def test_da2_epochs_match_reference_adversarial_train_2(golden, tmp_path, monkey
                                                     "DA2 update", floor=1e-2))
 
 
+@pytest.mark.parametrize("submit", ["auto", "branches", "serial", "split"])
 @pytest.mark.parametrize("da", [False, True])
-def test_graphed_step_equals_eager(da):
+def test_graphed_step_equals_eager(da, submit, monkeypatch):
     """runtime.GraphedStep: N replays of the captured iteration (poly-LR changing every step,
     Adam step counts advancing through the device hyper buffer) leave parameters, optimizer
-    state and BN buffers bit-identical to N eager iterations (seg step and DA iteration)."""
+    state and BN buffers bit-identical to N eager iterations (seg step and DA iteration), for
+    every submission variant: the multi-stream capture (branches), the serial capture, the
+    multi-stream capture replayed as lane-split linear segment graphs (rtsds_graph_split), and
+    "auto" (both captures; with trial_calls 2 the 4 replays run each variant twice)."""
+    from rtsds_amd import runtime
     from rtsds_amd.runtime import GraphedStep
+    monkeypatch.setitem(runtime.SUBMIT, "trial_calls", 2)
     from rtsds_amd.utils import poly_lr_scheduler
 
     def setup():
@@ -372,12 +378,23 @@ def test_graphed_step_equals_eager(da):
             for i in range(5):
                 poly_lr_scheduler(opt, 1e-3, i, 1, 10, 0.9)
                 if graphed and i == 1:  # step 0 is GraphedStep's eager warm-up
-                    run = GraphedStep(core, [opt, dopt] if da else [opt], warmup=0)
+                    run = GraphedStep(core, [opt, dopt] if da else [opt], warmup=0, submit=submit)
+                    names = [v[0] for v in run.variants]
+                    # branch streams fork: spatial path (seg), target forward / D phase (DA)
+                    assert names == {"auto": ["branches", "serial"], "branches": ["branches"],
+                                     "serial": ["serial"], "split": ["split"]}[submit], names
+                    for name, _, runners, _ in run.variants:
+                        lanes = max(r.lanes for r, _ in runners)
+                        assert lanes == 1 if name == "serial" else lanes > 1, (name, lanes)
+                    if submit == "split":
+                        assert sum(r.segments for r, _ in run.runners) > 1
                 if graphed and i == 0:
                     core_out = core()
                 else:
                     core_out = run()
             torch.cuda.synchronize()
+            if graphed:
+                assert run.submit_choice in names, run.submit_choice  # auto: decided after 2 + 2 trials
             states.append({k: v.detach().float().cpu().clone() for k, v in
                            list(net.state_dict().items()) + list(disc.state_dict().items())})
             states[-1]["_loss"] = core_out[0].float().cpu().clone()
@@ -760,3 +777,33 @@ def test_da_step_overlap_bit_identical(graphed):
     assert l0 == l1
     for k in s0:
         assert torch.equal(s0[k], s1[k]), k
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_bisenet_inference_fast_path_matches_general_path(dtype, monkeypatch):
+    """BiSeNet eval forward without autograd (inference: BN folded into the conv epilogues, the
+    context resizes written into the fusion module's concatenated input, the attention tail
+    and final 1x1 conv fused -- functional.concat_resized / ffm_head_eval) against (a) the same
+    no-autograd forward with those two fusions off (separate cat, GAP, pooled convs, channel
+    scale, 1x1 GEMM): within the fused kernel's own rounding, and (b) in fp32, the eval forward
+    with autograd enabled (no BN fold either)."""
+    torch.manual_seed(11)
+    net = BiSeNet(19, "resnet18").to(DEV).eval()
+    g = torch.Generator().manual_seed(12)
+    x = torch.randn(2, 3, 128, 256, generator=g).to(DEV) * 50
+    with rtsds_amd.precision(dtype):
+        with torch.no_grad():
+            fast = net(x).float()
+            monkeypatch.setattr(BiSeNet, "inference_fusions", False)
+            unfused = net(x).float()
+            monkeypatch.setattr(BiSeNet, "inference_fusions", True)
+        general = net(x).detach().float() if dtype == torch.float32 else None
+    torch.cuda.synchronize()
+    scale = unfused.abs().max().item()
+    err = (fast - unfused).abs().max().item() / scale
+    assert err < (1e-5 if dtype == torch.float32 else 1e-2), err
+    agree = (fast.argmax(1) == unfused.argmax(1)).float().mean().item()
+    assert agree > (0.999 if dtype == torch.float32 else 0.98), agree
+    if general is not None:
+        err = (fast - general).abs().max().item() / general.abs().max().item()
+        assert err < 1e-4, err
