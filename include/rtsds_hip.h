@@ -116,6 +116,24 @@ int rtsds_conv2d_dgrad_bnstats(const rtsds_conv_desc* d, const void* dy, const v
 size_t rtsds_conv2d_wgrad_workspace(const rtsds_conv_desc* d);
 int rtsds_conv2d_wgrad(const rtsds_conv_desc* d, const void* x, const void* dy, float* dw,
                        float* dbias, int accumulate, void* ws, size_t ws_bytes, void* stream);
+/* Deferred split-K reduction of a weight gradient.  rtsds_conv2d_wgrad_deferred launches every
+ * kernel of rtsds_conv2d_wgrad except the final reduction of the fp32 split slabs (which stay in
+ * ws) into dw, and describes that reduction in *pending (pending->nv == 0: nothing deferred --
+ * the call completed dw itself).  rtsds_split_reduce_many then performs up to n pending
+ * reductions in ONE launch (the backward pass's wgrads reduced together instead of one small
+ * launch each); descs must target distinct dw, and ws must stay allocated until it has run.  */
+typedef struct {
+  const float* slab;  /* [splits][k * kh * kw * cp] fp32 partials (in the wgrad's workspace) */
+  float* dw;          /* [k][kh][kw][c] fp32                                                   */
+  long slab_stride;   /* elements between splits                                              */
+  int nv;             /* float4 outputs: k * kh * kw * c / 4                                    */
+  int cv, cp;         /* c / 4; the slab's (padded) channel pitch                              */
+  int splits, accumulate;
+} rtsds_split_reduce_desc;
+int rtsds_conv2d_wgrad_deferred(const rtsds_conv_desc* d, const void* x, const void* dy, float* dw,
+                                float* dbias, int accumulate, void* ws, size_t ws_bytes,
+                                rtsds_split_reduce_desc* pending, void* stream);
+int rtsds_split_reduce_many(int n, const rtsds_split_reduce_desc* descs, void* stream);
 
 /* ---------------------------------------------------------------- batch norm (train/eval)
  * Replaces nn.BatchNorm2d at build_bisenet.py:13,39; torchvision ResNet bn*; deeplabv2.py:14-27,

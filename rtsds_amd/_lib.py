@@ -30,6 +30,12 @@ class ConvDesc(ctypes.Structure):
                                      "ph", "pw", "dh", "dw", "dtype")]
 
 
+class SplitReduceDesc(ctypes.Structure):
+    """rtsds_split_reduce_desc (include/rtsds_hip.h)."""
+    _fields_ = [("slab", c_void_p), ("dw", c_void_p), ("slab_stride", c_long), ("nv", c_int), ("cv", c_int),
+                ("cp", c_int), ("splits", c_int), ("accumulate", c_int)]
+
+
 P = c_void_p
 # name -> (restype, argtypes)
 SIGNATURES = {
@@ -47,6 +53,9 @@ SIGNATURES = {
     "rtsds_conv2d_dgrad_bnstats": (c_int, [ctypes.POINTER(ConvDesc), P, P, P, P, P, P, P, P, c_int, P, P, c_size_t, P]),
     "rtsds_conv2d_wgrad_workspace": (c_size_t, [ctypes.POINTER(ConvDesc)]),
     "rtsds_conv2d_wgrad": (c_int, [ctypes.POINTER(ConvDesc), P, P, P, P, c_int, P, c_size_t, P]),
+    "rtsds_conv2d_wgrad_deferred": (c_int, [ctypes.POINTER(ConvDesc), P, P, P, P, c_int, P, c_size_t,
+                                            ctypes.POINTER(SplitReduceDesc), P]),
+    "rtsds_split_reduce_many": (c_int, [c_int, ctypes.POINTER(SplitReduceDesc), P]),
     "rtsds_bn_workspace": (c_size_t, [c_long, c_int]),
     "rtsds_bn_fwd": (c_int, [P, P, P, c_long, c_int, P, P, P, P, P, P, P, c_float, c_float, c_int,
                              c_int, P, c_int, c_int, P, c_size_t, P]),

@@ -2378,8 +2378,88 @@ static void wgrad_launch(const ConvArgs& p, int bm, int bn, int splits, hipStrea
   }
 }
 
+static int wgrad_impl(const rtsds_conv_desc* d0, const void* x, const void* dy, float* dw, float* dbias, int accumulate,
+                      void* ws, size_t ws_bytes, rtsds_split_reduce_desc* pending, void* stream);
 extern "C" int rtsds_conv2d_wgrad(const rtsds_conv_desc* d0, const void* x, const void* dy, float* dw,
                                   float* dbias, int accumulate, void* ws, size_t ws_bytes, void* stream) {
+  return wgrad_impl(d0, x, dy, dw, dbias, accumulate, ws, ws_bytes, nullptr, stream);
+}
+extern "C" int rtsds_conv2d_wgrad_deferred(const rtsds_conv_desc* d0, const void* x, const void* dy, float* dw,
+                                           float* dbias, int accumulate, void* ws, size_t ws_bytes,
+                                           rtsds_split_reduce_desc* pending, void* stream) {
+  if (!pending) return RTSDS_ERR_SHAPE;
+  pending->nv = 0;
+  return wgrad_impl(d0, x, dy, dw, dbias, accumulate, ws, ws_bytes, pending, stream);
+}
+
+// Batched split-K reductions (rtsds_split_reduce_many): block b belongs to the descriptor whose
+// block range contains it; within it, split_reduce_kernel<4>'s arithmetic (4 split groups per
+// 64 outputs, summed in split order) -- bit-identical to the per-wgrad launch.
+static const int kReduceBatch = 16;
+struct ReduceBatch {
+  rtsds_split_reduce_desc d[kReduceBatch];
+  int blk0[kReduceBatch];
+  int n;
+};
+__global__ void __launch_bounds__(256) split_reduce_many_kernel(const ReduceBatch b) {
+  __shared__ float red[4][64][4];
+  int si = 0;
+  for (int i = 1; i < b.n; ++i)
+    if (b.blk0[i] <= (int)blockIdx.x) si = i;
+  const rtsds_split_reduce_desc& q = b.d[si];
+  const int lane = threadIdx.x & 63, sg = threadIdx.x >> 6;
+  const int i = ((int)blockIdx.x - b.blk0[si]) * 64 + lane;
+  const bool ok = i < q.nv;
+  const int rt = (ok ? i : 0) / q.cv;  // co * taps + tap
+  const long src = (long)rt * q.cp + (long)((ok ? i : 0) - rt * q.cv) * 4;
+  float s[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int g = sg; ok && g < q.splits; g += 32) {
+    float t[8][4];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const f32x4 v = *(const f32x4*)(q.slab + (long)min(g + 4 * u, q.splits - 1) * q.slab_stride + src);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) t[u][e] = v[e];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (g + 4 * u < q.splits)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) s[e] += t[u][e];
+  }
+#pragma unroll
+  for (int e = 0; e < 4; ++e) red[sg][lane][e] = s[e];
+  __syncthreads();
+  if (sg == 0 && ok) {
+    float* o = q.dw + (long)i * 4;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float t = (red[0][lane][e] + red[1][lane][e]) + (red[2][lane][e] + red[3][lane][e]);
+      o[e] = q.accumulate ? o[e] + t : t;
+    }
+  }
+}
+extern "C" int rtsds_split_reduce_many(int n, const rtsds_split_reduce_desc* descs, void* stream) {
+  if (n < 0 || (n && !descs)) return RTSDS_ERR_SHAPE;
+  for (int i0 = 0; i0 < n; i0 += kReduceBatch) {
+    ReduceBatch b;
+    b.n = 0;
+    int blocks = 0;
+    for (int i = i0; i < n && b.n < kReduceBatch; ++i) {
+      if (descs[i].nv <= 0) continue;
+      if (descs[i].cv <= 0 || descs[i].splits <= 0 || !descs[i].slab || !descs[i].dw) return RTSDS_ERR_SHAPE;
+      b.d[b.n] = descs[i];
+      b.blk0[b.n] = blocks;
+      blocks += (descs[i].nv + 63) / 64;
+      ++b.n;
+    }
+    if (b.n) hipLaunchKernelGGL(split_reduce_many_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, b);
+  }
+  return hipGetLastError() == hipSuccess ? RTSDS_OK : RTSDS_ERR_LAUNCH;
+}
+
+static int wgrad_impl(const rtsds_conv_desc* d0, const void* x, const void* dy, float* dw, float* dbias, int accumulate,
+                      void* ws, size_t ws_bytes, rtsds_split_reduce_desc* pending, void* stream) {
   int e = check_desc(d0);
   if (e) return e;
   const bool x_padded = (accumulate & RTSDS_INPUT_PADDED) != 0;
@@ -2444,7 +2524,16 @@ extern "C" int rtsds_conv2d_wgrad(const rtsds_conv_desc* d0, const void* x, cons
     const int V = d0->c % 4 == 0 ? 4 : 1, cv = d0->c / V;
     const int nv = d0->k * d0->kh * d0->kw * cv;
     const int blocks = std::min(8192, (nv + 63) / 64);
-    if (V == 4)
+    if (pending && V == 4) {  // the caller reduces it later, batched (rtsds_split_reduce_many)
+      pending->slab = (const float*)slab;
+      pending->dw = dw;
+      pending->slab_stride = p.split_stride;
+      pending->nv = nv;
+      pending->cv = cv;
+      pending->cp = pl.cp;
+      pending->splits = pl.splits;
+      pending->accumulate = accumulate ? 1 : 0;
+    } else if (V == 4)
       hipLaunchKernelGGL(split_reduce_kernel<4>, dim3(blocks), dim3(256), 0, st, (const float*)slab, dw, nv, cv, fastdiv_make(cv),
                          pl.cp, p.split_stride, pl.splits, accumulate);
     else

@@ -10,7 +10,7 @@ import ctypes
 import numpy as np
 import torch
 
-from ._lib import ACT_RELU, ACT_SIGMOID, INPUT_PADDED, WEIGHT_PACKED, ConvDesc, lib
+from ._lib import ACT_RELU, ACT_SIGMOID, INPUT_PADDED, WEIGHT_PACKED, ConvDesc, SplitReduceDesc, lib
 from .runtime import (CL, bump_params_epoch, collective, dcode, dp_world, empty_nhwc, nhwc, params_epoch,
                       register_fold, require_hip, side_enabled, side_fork, stream, workspace)
 
@@ -178,6 +178,59 @@ def _join_add(join, g):
     return join.put(g)
 
 
+# ----------------------------------------------------------------------------- deferred wgrad reduce
+# The split-K weight gradients of one backward pass leave their fp32 partial slabs in workspace
+# and are reduced into the optimizer's gradient arena together, by one rtsds_split_reduce_many
+# launch at the end of the backward (an autograd engine callback, so .grad is complete when
+# backward() returns) instead of one small launch per conv (~27 per BiSeNet step).  Same sums,
+# same order.  Off while bench.py event-times each conv (CONV_PROFILE).
+DEFER_WGRAD_REDUCE = True
+_deferred = []  # [(SplitReduceDesc, workspace tensor holding the slabs, stream of the wgrad)]
+
+
+def flush_wgrad_reduce():
+    """Run the pending split-K reductions (every deferral also queues this as an end-of-backward
+    callback; the first one of a backward pass does the work, optim.step() calls it too)."""
+    global _deferred
+    items, _deferred = _deferred, []
+    if not items:
+        return
+    cur = torch.cuda.current_stream(items[0][1].device)
+    for st in {it[2] for it in items}:  # wgrads issued on branch streams
+        if st != cur:
+            cur.wait_stream(st)
+    # one launch per run of distinct targets (a parameter reduced twice keeps its order)
+    batch, seen = [], set()
+    for desc, _ws, _st in items + [(None, None, None)]:
+        if desc is None or desc.dw in seen or len(batch) == 16:
+            if batch:
+                arr = (SplitReduceDesc * len(batch))(*batch)
+                lib.rtsds_split_reduce_many(len(batch), arr, cur.cuda_stream)
+            batch, seen = [], set()
+        if desc is not None:
+            batch.append(desc)
+            seen.add(desc.dw)
+    for _desc, ws, st in items:
+        if st != cur:
+            ws.record_stream(cur)
+
+
+def _wgrad_into_arena(d, x, g, sinks, xflag, ws):
+    """Weight gradient accumulated into the optimizer arena; its split-K reduction deferred to
+    the end of the backward pass when allowed."""
+    if DEFER_WGRAD_REDUCE and CONV_PROFILE is None and x.dtype == torch.bfloat16:
+        pend = SplitReduceDesc()
+        lib.rtsds_conv2d_wgrad_deferred(ctypes.byref(d), _P(x), _P(g), _P(sinks[0]), _P(sinks[1]), 1 | xflag,
+                                        _P(ws), ws.numel(), ctypes.byref(pend), stream())
+        if pend.nv > 0:
+            _deferred.append((pend, ws, torch.cuda.current_stream(ws.device)))
+            torch.autograd.Variable._execution_engine.queue_callback(flush_wgrad_reduce)
+        return
+    with _Timed(d, "wgrad"):
+        lib.rtsds_conv2d_wgrad(ctypes.byref(d), _P(x), _P(g), _P(sinks[0]), _P(sinks[1]), 1 | xflag,
+                               _P(ws), ws.numel(), stream())
+
+
 class ConvFn(torch.autograd.Function):
     """nn.Conv2d forward / backward (bias and LeakyReLU/ReLU epilogue optionally fused).
 
@@ -270,9 +323,7 @@ class ConvFn(torch.autograd.Function):
             sinks = _sinks(weight, bias if ctx.needs_input_grad[2] else None) if ctx.needs_input_grad[1] else None
             ws = workspace(lib.rtsds_conv2d_wgrad_workspace(ctypes.byref(d)), x.device)
             if sinks is not None:
-                with _Timed(d, "wgrad"):
-                    lib.rtsds_conv2d_wgrad(ctypes.byref(d), _P(x), _P(g), _P(sinks[0]), _P(sinks[1]), 1 | ctx.xflag,
-                                                  _P(ws), ws.numel(), stream())
+                _wgrad_into_arena(d, x, g, sinks, ctx.xflag, ws)
                 dw = None
                 db = None
             else:

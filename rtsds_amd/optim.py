@@ -298,6 +298,8 @@ class _FlatOptimizer(torch.optim.Optimizer):
     @torch.no_grad()
     def step(self, closure=None):
         loss = closure() if closure is not None else None
+        from .functional import flush_wgrad_reduce
+        flush_wgrad_reduce()  # normally done at the end of each backward already
         arenas = self._ensure()
         bump_params_epoch()  # the update writes the arenas through raw pointers
         if self._finish is not None:

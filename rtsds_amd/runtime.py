@@ -452,13 +452,14 @@ class GraphedStep:
                 coll()
         dt = time.perf_counter() - t0
         self.host_launch_s += dt
+        outputs = self.outputs  # of the variant just replayed (_decide may switch)
         if trial:
             e1.record()
             self._trial[vi].append((dt, e0, e1))
             self._calls += 1
             if self._calls == int(SUBMIT["trial_calls"]) * len(self.variants):
                 self._decide()
-        return self.outputs
+        return outputs
 
     def _decide(self):
         """Keep the variant with the smaller max(host submission, GPU) time per step (the first
