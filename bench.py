@@ -66,6 +66,8 @@ def parse():
     ap.add_argument("--da-unfused", action="store_true",
                     help="A/B: discriminator input through interpolate + softmax (no fused upsample_softmax)")
     ap.add_argument("--no-conv-profile", action="store_true", help="skip the event-timed roofline step")
+    ap.add_argument("--submit", default="auto", choices=["auto", "branches", "serial", "split"],
+                    help="graph submission variant (runtime.GraphedStep; auto = time both captures, keep the faster)")
     ap.add_argument("--graph", default="auto", choices=["auto", "on", "off"],
                     help="replay the iteration as hipGraph segments (auto = on; under data parallelism "
                          "the RCCL collectives run between the segments, runtime.GraphedStep)")
@@ -250,7 +252,7 @@ def main():
         # parallelism the collectives run between the graph segments
         from rtsds_amd.runtime import GraphedStep
         try:
-            graphed = GraphedStep(core, opts, warmup=1)
+            graphed = GraphedStep(core, opts, warmup=1, submit=args.submit)
         except Exception as e:  # keep the measurement alive on the eager path
             print(f"bench: hipGraph capture failed ({e!r}); timing eager iterations", file=sys.stderr)
             for o in opts:

@@ -673,25 +673,59 @@ class CatFn(torch.autograd.Function):
         return tuple(outs)
 
 
+class CatResizeFn(torch.autograd.Function):
+    """cat([x0] + [interpolate_bilinear(x, size) for x in xs], dim=1) (build_bisenet.py:151-153
+    and the FFM's cat, :72) with each resize written straight into its channel slice of the
+    output (rtsds_bilinear_fwd's output pitch / offset) and, backward, each resize's gradient
+    read straight from its slice of dy (rtsds_bilinear_bwd's input pitch / offset): neither the
+    resized maps nor their gradients exist on their own; x0 (already at ``size``) is the one
+    copy each way."""
+
+    @staticmethod
+    def forward(ctx, size, x0, *xs):
+        x0 = nhwc(x0)
+        n, c0, h, w = x0.shape
+        if (h, w) != (int(size[0]), int(size[1])):
+            raise RuntimeError("rtsds_amd.concat_resized: x0 must have the target size")
+        xs = [nhwc(x) for x in xs]
+        ct = c0 + sum(x.shape[1] for x in xs)
+        y = empty_nhwc(n, ct, h, w, x0.dtype, x0.device)
+        lib.rtsds_copy_channels(_P(x0), c0, 0, _P(y), ct, 0, n * h * w, c0, 0, dcode(x0), stream())
+        off, geos = c0, []
+        for x in xs:
+            _, c, hi, wi = x.shape
+            ho, wo, sh, sw = upsample_geometry(x, size=size)
+            lib.rtsds_bilinear_fwd(_P(x), _P(y), n, hi, wi, c, ho, wo, sh, sw, ct, off, dcode(x), stream())
+            geos.append((off, c, hi, wi, ho, wo, sh, sw))
+            off += c
+        ctx.meta = (n, c0, h, w, ct, geos)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        n, c0, h, w, ct, geos = ctx.meta
+        dy = nhwc(dy)
+        grads = [None, None]
+        if ctx.needs_input_grad[1]:
+            g0 = empty_nhwc(n, c0, h, w, dy.dtype, dy.device)
+            lib.rtsds_copy_channels(_P(dy), ct, 0, _P(g0), c0, 0, n * h * w, c0, 0, dcode(dy), stream())
+            grads[1] = g0
+        for k, (off, c, hi, wi, ho, wo, sh, sw) in enumerate(geos):
+            if not ctx.needs_input_grad[2 + k]:
+                grads.append(None)
+                continue
+            dx = empty_nhwc(n, c, hi, wi, dy.dtype, dy.device)
+            ws = workspace(lib.rtsds_bilinear_bwd_workspace(n, hi, wi, c, ho, wo), dy.device)
+            lib.rtsds_bilinear_bwd(_P(dy), _P(dx), n, hi, wi, c, ho, wo, sh, sw, ct, off, dcode(dy), _P(ws),
+                                   ws.numel(), stream())
+            grads.append(dx)
+        return tuple(grads)
+
+
 def concat_resized(x0, xs, size):
-    """Inference only (no autograd): cat([x0] + [interpolate_bilinear(x, size) for x in xs],
-    dim=1) with each resize written straight into its channel slice of the output
-    (rtsds_bilinear_fwd's output pitch / offset) -- x0 (already at ``size``) is the one copy."""
-    x0 = nhwc(x0)
-    n, c0, h, w = x0.shape
-    if (h, w) != (int(size[0]), int(size[1])):
-        raise RuntimeError("rtsds_amd.concat_resized: x0 must have the target size")
-    xs = [nhwc(x) for x in xs]
-    ct = c0 + sum(x.shape[1] for x in xs)
-    y = empty_nhwc(n, ct, h, w, x0.dtype, x0.device)
-    lib.rtsds_copy_channels(_P(x0), c0, 0, _P(y), ct, 0, n * h * w, c0, 0, dcode(x0), stream())
-    off = c0
-    for x in xs:
-        _, c, hi, wi = x.shape
-        ho, wo, sh, sw = upsample_geometry(x, size=size)
-        lib.rtsds_bilinear_fwd(_P(x), _P(y), n, hi, wi, c, ho, wo, sh, sw, ct, off, dcode(x), stream())
-        off += c
-    return y
+    """cat([x0] + [interpolate_bilinear(x, size) for x in xs], dim=1) without materialising the
+    resized maps (CatResizeFn)."""
+    return CatResizeFn.apply((int(size[0]), int(size[1])), x0, *xs)
 
 
 def ffm_head_eval(feature, w1, b1, w2, b2, w3, b3):

@@ -204,10 +204,10 @@ class BiSeNet(torch.nn.Module):
             s1 = F.interpolate_bilinear(self.supervision1(cx1), size=hw)
             s2 = F.interpolate_bilinear(self.supervision2(cx2), size=hw)
             aux = [(s1, F.upsample_geometry(s1, size=full)), (s2, F.upsample_geometry(s2, size=full))]
-        cx1 = F.interpolate_bilinear(cx1, size=hw)
-        cx2 = F.interpolate_bilinear(cx2, size=hw)
-        joins = None
-        result = self.feature_fusion_module(sx, (cx1, cx2), joins)
+        # the two resizes write straight into the fusion module's concatenated input and read
+        # their gradients straight from its gradient (functional.CatResizeFn; the reference:
+        # interpolate, interpolate, cat)
+        result = self.feature_fusion_module(F.concat_resized(sx, (cx1, cx2), hw))
         if self.with_interpolation:
             # reference: conv(up8(result)) (build_bisenet.py:165-167).  A 1x1 conv mixes channels
             # per pixel and bilinear resize mixes pixels per channel with weights summing to 1,

@@ -15,6 +15,7 @@ from torch import nn
 from rtsds_amd import functional as F
 from rtsds_amd.functional import BnBwdLink
 from rtsds_amd.nn import BatchNorm2d, Conv2d, MaxPool2d, ReLU, conv_bn, conv_bn_relu_maxpool, grad_join
+from rtsds_amd.runtime import grad_cut
 
 
 class BasicBlock(nn.Module):
@@ -127,7 +128,7 @@ class _ContextPath(nn.Module):
         t = self.layer2(self.layer1(t))
         if mid is not None:
             mid()
-        f3 = self.layer3(t)
+        f3 = grad_cut(self.layer3(t))  # data-parallel two-phase backward (runtime.grad_cut)
         f4 = self.layer4(f3)
         return f3, f4, F.global_avg_pool(f4)
 

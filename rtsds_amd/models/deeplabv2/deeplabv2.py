@@ -14,6 +14,7 @@ from rtsds_amd import functional as F
 from rtsds_amd.functional import BnBwdLink
 from rtsds_amd.nn import BatchNorm2d, Conv2d, MaxPool2d, ReLU, conv_bn, conv_bn_relu_maxpool, grad_join, to_input
 from rtsds_amd.nn import _shadow
+from rtsds_amd.runtime import grad_cut
 
 affine_par = True
 
@@ -110,7 +111,7 @@ class ResNetMulti(nn.Module):
         _, _, H, W = x.size()
         t = to_input(x)
         t = conv_bn_relu_maxpool(self.conv1, self.bn1, self.maxpool, t)
-        t = self.layer4(self.layer3(self.layer2(self.layer1(t))))
+        t = self.layer4(grad_cut(self.layer3(self.layer2(self.layer1(t)))))  # runtime.grad_cut
         t = self.layer6(t)
         return [(t, F.upsample_geometry(t, size=(H, W)))]
 

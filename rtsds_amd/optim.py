@@ -203,7 +203,8 @@ class _FlatOptimizer(torch.optim.Optimizer):
         self._hyper = None       # device fp32 [runs][3]
         self._ring = [[None, None] for _ in range(8)]  # pinned staging buffers + their copy events
         self._ring_pos = 0
-        self._finish = None      # pending early gradient all-reduce (start_grad_allreduce)
+        self._finish = []        # pending early gradient all-reduces (start_grad_allreduce)
+        self._reduced = None     # per arena: parameters whose all-reduce has been started
 
     # ------------------------------------------------------------------ arena
     def _ensure(self):
@@ -286,14 +287,41 @@ class _FlatOptimizer(torch.optim.Optimizer):
                         self._warned = True
                     a.rebind_grad(i)
 
+    @staticmethod
+    def _ranges(a, idx):
+        """Contiguous arena ranges [lo, hi) covering the parameters ``idx`` (sorted)."""
+        out = []
+        for i in idx:
+            lo, hi = a.offsets[i], a.offsets[i] + a.params[i].numel()
+            if out and out[-1][2] == i - 1:
+                out[-1] = (out[-1][0], hi, i)
+            else:
+                out.append((lo, hi, i))
+        return [(lo, hi) for lo, hi, _ in out]
+
     @torch.no_grad()
-    def start_grad_allreduce(self):
+    def start_grad_allreduce(self, partial=False):
         """Data parallelism: the gradients are final now -- start their all-reduce so it overlaps
-        the work enqueued before step(), which then only waits for it.  No-op at world 1."""
-        if self._finish is None and _OVERLAP["on"]:
-            arenas = self._ensure()
-            self._fix_grads(arenas)
-            self._finish = allreduce_start([a.gflat for a in arenas])
+        the work enqueued before step(), which then only waits for it.  ``partial``: only the
+        parameters that have received their gradients so far (a backward pass split at a cut,
+        train.seg_step: the later phase writes only the others), as contiguous arena ranges;
+        the rest follow at step() (or a later call).  No-op at world 1."""
+        if not _OVERLAP["on"] or dp_world() <= 1 or not (dist.is_available() and dist.is_initialized()):
+            return
+        arenas = self._ensure()
+        self._fix_grads(arenas)
+        if self._reduced is None:
+            self._reduced = [[False] * len(a.params) for a in arenas]
+        bufs = []
+        for a, red in zip(arenas, self._reduced):
+            idx = [i for i in range(len(a.params)) if not red[i] and (a.touched[i] or not partial)]
+            for i in idx:
+                red[i] = True
+            bufs += [a.gflat[lo:hi] for lo, hi in self._ranges(a, idx)]
+        if bufs:
+            fin = allreduce_start(bufs)
+            if fin is not None:
+                self._finish.append(fin)
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -302,9 +330,11 @@ class _FlatOptimizer(torch.optim.Optimizer):
         flush_wgrad_reduce()  # normally done at the end of each backward already
         arenas = self._ensure()
         bump_params_epoch()  # the update writes the arenas through raw pointers
-        if self._finish is not None:
-            self._finish()
-            self._finish = None
+        if self._finish:
+            self.start_grad_allreduce()  # whatever a partial start left
+            for fin in self._finish:
+                fin()
+            self._finish, self._reduced = [], None
             gscale = 1.0
         else:
             self._fix_grads(arenas)

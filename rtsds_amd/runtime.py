@@ -109,6 +109,40 @@ def workspace(nbytes, device):
     return torch.empty(max(int(nbytes), 16), dtype=torch.uint8, device=device)
 
 
+# ----------------------------------------------------------------------------- backward cuts
+# Data parallelism (train.seg_step): the backward pass runs in two phases split at a cut tensor
+# (the context path's layer-3 output), so that the all-reduce of the gradients finished in the
+# first phase (the late layers: ResNet layer4, attention / fusion modules, heads, spatial path --
+# ~75 % of BiSeNet-R18's parameters) is started from the host between the phases and overlaps
+# the second (layer3 .. stem).  A cut returns a detached leaf copy of its input for the
+# downstream consumers; phase 2 is torch.autograd.backward(cut inputs, their leaf gradients).
+_cuts = []
+
+
+@contextlib.contextmanager
+def collect_cuts(on=True):
+    """Models' grad_cut() calls inside the block record (tensor, detached leaf) pairs here."""
+    if not on:
+        yield None
+        return
+    lst = []
+    _cuts.append(lst)
+    try:
+        yield lst
+    finally:
+        _cuts.pop()
+
+
+def grad_cut(x):
+    """Identity, or -- inside collect_cuts() with autograd on -- a detached leaf copy of ``x``
+    whose gradient phase 1 of the backward accumulates."""
+    if not _cuts or not (torch.is_grad_enabled() and x.requires_grad):
+        return x
+    xd = x.detach().requires_grad_()
+    _cuts[-1].append((x, xd))
+    return xd
+
+
 # ----------------------------------------------------------------------------- side stream
 # Weight gradients run on a second HIP stream, concurrently with the data-gradient chain of
 # the backward pass (dgrad GEMMs, BatchNorm backward passes and the small reduction /

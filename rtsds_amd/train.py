@@ -12,7 +12,7 @@ import torch
 
 from . import functional as F
 from . import losses, utils
-from .runtime import branch_stream, branches_enabled, branches_serial, dp_world
+from .runtime import branch_stream, branches_enabled, branches_serial, collect_cuts, dp_world
 from .callbacks import Callback
 from .validation import val_GTA5
 
@@ -57,6 +57,17 @@ def _fused_heads(model, criterion, inputs):
     return ts, geo
 
 
+def _backward(loss, optimizer, cuts):
+    """loss.backward(); with cuts (runtime.grad_cut under data parallelism): phase 1 down to the
+    cut leaves, the all-reduce of the gradients complete so far started, then phase 2 through
+    the cut tensors -- same gradients (the cut leaves accumulate exactly what the cut tensors
+    would have received)."""
+    loss.backward()
+    if cuts:
+        optimizer.start_grad_allreduce(partial=True)
+        torch.autograd.backward([x for x, _ in cuts], [xd.grad for _, xd in cuts])
+
+
 def seg_step(model, criterion, optimizer, inputs, targets):
     """One train.train iteration body: zero_grad, forward, CE(main)+CE(aux1)+CE(aux2),
     backward, optimizer step, device-side pixel-accuracy count.  Returns device tensors
@@ -65,24 +76,30 @@ def seg_step(model, criterion, optimizer, inputs, targets):
     kernel (functional.upsample_cross_entropy) -- same losses and gradients, no
     full-resolution logits."""
     optimizer.zero_grad()
-    fused = _fused_heads(model, criterion, inputs)
+    # data parallelism: the backward runs in two phases split at the models' grad_cut tensor,
+    # and the all-reduce of the first phase's (late layers') gradients overlaps the second
+    split = dp_world() > 1 and hasattr(optimizer, "start_grad_allreduce")
+    with collect_cuts(split) as cuts:
+        fused = _fused_heads(model, criterion, inputs)
+        if fused is None:
+            outs = _unpack(model(inputs))
     if fused is not None and fused[1] is not None:
         correct = torch.zeros(1, dtype=torch.int64, device=fused[0][0].device)
         loss = F.upsample_cross_entropy(fused[0], targets, fused[1], criterion.ignore_index, correct)
-        loss.backward()
+        _backward(loss, optimizer, cuts)
         optimizer.step()
         return loss.detach(), correct
     if fused is not None:
         outs = list(fused[0]) + [None] * (3 - len(fused[0]))
         main_output, aux1, aux2 = outs[:3]
     else:
-        main_output, aux1, aux2 = _unpack(model(inputs))
+        main_output, aux1, aux2 = outs
     loss = criterion(main_output, targets)
     if aux1 is not None:
         loss = loss + criterion(aux1, targets)
     if aux2 is not None:
         loss = loss + criterion(aux2, targets)
-    loss.backward()
+    _backward(loss, optimizer, cuts)
     optimizer.step()
     correct = torch.zeros(1, dtype=torch.int64, device=main_output.device)
     F.argmax_channels(main_output.detach(), targets, correct, want_map=False)

@@ -16,7 +16,7 @@ trap "kill $hb" EXIT
 STEPS=6
 for wl in $wls; do
   o=gpurun_out/prof_${tag}_$wl; r=/tmp/prof_${tag}/$wl; mkdir -p $o $r
-  args="bench.py --workload $wl --steps 3 --warmup 1 --no-cpu-baseline --no-infer --no-conv-profile"
+  args="bench.py --workload $wl --steps 3 --warmup 1 --no-cpu-baseline --no-infer --no-conv-profile --submit branches"
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $r/kt -o run -- python3 $args > $o/log 2>&1
   timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $r/fetch -o run -- python3 $args >> $o/log 2>&1
   timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $r/write -o run -- python3 $args >> $o/log 2>&1
