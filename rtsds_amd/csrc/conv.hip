@@ -1726,12 +1726,18 @@ void hconv_fwd(const rtsds_conv_desc* d, const void* x, const void* w, const flo
 bool hconv_dgrad_ok(const rtsds_conv_desc* d);
 void hconv_dgrad(const rtsds_conv_desc* d, const void* dyp, int kp, const void* wt, void* dx, int accumulate, hipStream_t st);
 bool pw_ok(const rtsds_conv_desc* d);
+// Direct MFMA conv for the 3-channel stride-2 image convs (imgconv.hip).
+bool imgconv_ok(const rtsds_conv_desc* d);
+int imgconv_tiles(const rtsds_conv_desc* d);
+void imgconv_fwd(const rtsds_conv_desc* d, const void* x4, const void* w, const float* bias, const float* scale, void* y,
+                 int act, float* stats, hipStream_t st);
 void pw_dgrad(const rtsds_conv_desc* d, const void* dy, const void* w, void* dx, int accum, hipStream_t st);
 
 // Number of M tiles (= BatchNorm partial-statistics rows) the forward launch of d uses.
 extern "C" int rtsds_conv2d_fwd_stats_tiles(const rtsds_conv_desc* d) {
   if (pooled_1x1(d)) return 1;
   if (hconv_ok(d)) return hconv_tiles(d);
+  if (imgconv_ok(d)) return imgconv_tiles(d);
   int bm, bn;
   const long M = (long)d->n * d->ho * d->wo;
   const long K = sp_path(d) ? 0 : (long)d->kh * d->kw * pad_c(d->c, d->dtype);  // rtsds_conv2d_fwd's p.K
@@ -1857,6 +1863,12 @@ extern "C" int rtsds_conv2d_fwd(const rtsds_conv_desc* d0, const void* x, const 
     hconv_fwd(d0, x, w, bias, nullptr, y, act & 0xff, bn_stats, st);
     return hipGetLastError() == hipSuccess ? RTSDS_OK : RTSDS_ERR_LAUNCH;
   }
+  if (imgconv_ok(d0) && !(act & RTSDS_ACCUMULATE)) {
+    if (bn_stats && (act & 0xff)) return RTSDS_ERR_UNSUPPORTED;
+    if (!x_padded) sp_pad4(d0, x, ws, st);
+    imgconv_fwd(d0, x_padded ? x : ws, w, bias, nullptr, y, act & 0xff, bn_stats, st);
+    return hipGetLastError() == hipSuccess ? RTSDS_OK : RTSDS_ERR_LAUNCH;
+  }
   rtsds_conv_desc d;
   fwd_prepare(d0, x, w, ws, d, st, x_padded);
   ConvArgs p = make_args(&d);
@@ -1898,6 +1910,11 @@ extern "C" int rtsds_conv2d_fwd_bn(const rtsds_conv_desc* d0, const void* x, con
   hipStream_t st = (hipStream_t)stream;
   if (hconv_ok(d0) && !res) {
     hconv_fwd(d0, x, w, shift, scale, y, act & 0xff, nullptr, st);
+    return hipGetLastError() == hipSuccess ? RTSDS_OK : RTSDS_ERR_LAUNCH;
+  }
+  if (imgconv_ok(d0) && !res) {
+    if (!x_padded) sp_pad4(d0, x, ws, st);
+    imgconv_fwd(d0, x_padded ? x : ws, w, shift, scale, y, act & 0xff, nullptr, st);
     return hipGetLastError() == hipSuccess ? RTSDS_OK : RTSDS_ERR_LAUNCH;
   }
   rtsds_conv_desc d;
@@ -2149,7 +2166,8 @@ static bool dgrad_hconv(const rtsds_conv_desc* d, int kp);
 static DgradSplit dgrad_split(const rtsds_conv_desc* d, int kp);
 // M tiles of the data-gradient GEMM when its epilogue can emit the BatchNorm backward
 // statistics (bf16, stride 1, plain GEMM path: not the pooled / narrow-1x1 / halo / split-K
-// routes, vector epilogue), else 0
+// routes, vector epilogue), else 0.  (The stride-2 parity-phase launch could carry them too:
+// measured for the spatial path's BatchNorms, the epilogue cost what the statistics pass saved.)
 extern "C" int rtsds_conv2d_dgrad_bnstats_tiles(const rtsds_conv_desc* d) {
   if (check_desc(d) || d->dtype != RTSDS_BF16 || d->sh != 1 || d->sw != 1 || d->c % 8 != 0) return 0;
   if (pooled_1x1(d) || pw_ok(d)) return 0;
@@ -2157,7 +2175,7 @@ extern "C" int rtsds_conv2d_dgrad_bnstats_tiles(const rtsds_conv_desc* d) {
   if (dgrad_hconv(d, kp) || dgrad_split(d, kp).splits > 1) return 0;
   int bm, bn;
   const long M = (long)d->n * d->h * d->w;
-  pick_tile(M, d->c, true, bm, bn, false);
+  pick_tile(M, d->c, true, bm, bn, false, (long)d->kh * d->kw * kp);  // dispatch_align's choice
   if (256 % (bn / 8) != 0) return 0;
   return (int)((M + bm - 1) / bm);
 }

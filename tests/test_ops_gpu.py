@@ -874,3 +874,38 @@ def test_dgrad_packs_in_training_bit_identical():
         F.set_dgrad_packs(True)
     for k in states[0]:
         assert torch.equal(states[0][k], states[1][k]), k
+
+
+@pytest.mark.parametrize("kh,pad,bias", [(7, 3, False), (3, 1, True)])
+@pytest.mark.parametrize("hw", [(38, 150), (64, 256)])
+def test_image_conv_direct(kh, pad, bias, hw):
+    """The 3-channel stride-2 image convs (imgconv.hip: stem 7x7 s2 p3, spatial-path 3x3 s2 p1)
+    at output sizes that do / do not divide the 4 x 64 tile: forward vs ATen fp64, the
+    train-mode ConvBlock with the BatchNorm statistics from the conv epilogue (output and
+    running statistics), and the eval-mode folded conv + BN + ReLU."""
+    from rtsds_amd import nn as rnn
+    h, w = hw
+    g = torch.Generator().manual_seed(kh * 100 + h)
+    x = (torch.randn(2, 3, h, w, generator=g, dtype=torch.float64) * 40).bfloat16().double()
+    conv = rnn.Conv2d(3, 64, kh, stride=2, padding=pad, bias=bias).to(DEV)
+    bn = rnn.BatchNorm2d(64).to(DEV)
+    with torch.no_grad():
+        conv.weight.copy_((torch.randn(64, 3, kh, kh, generator=g) / (3 * kh * kh) ** 0.5).bfloat16().float())
+        if bias:
+            conv.bias.copy_(torch.randn(64, generator=g))
+    wr = conv.weight.detach().double().cpu()
+    br = conv.bias.detach().double().cpu() if bias else None
+    y0 = TF.conv2d(x, wr, br, 2, pad)
+    y = F.conv2d(_dev(x, torch.bfloat16), conv.weight, conv.bias, _shadow(conv.weight, torch.bfloat16), (2, 2),
+                 (pad, pad), (1, 1), 0)
+    _close(y, y0, torch.bfloat16, "conv")
+    yb = rnn.conv_bn(conv, bn, _dev(x, torch.bfloat16), "relu")
+    _close(yb, TF.relu(TF.batch_norm(y0, None, None, None, None, True, 0.1, 1e-5)), torch.bfloat16, "conv+bn+relu")
+    _close(bn.running_mean, 0.1 * y0.mean(dim=(0, 2, 3)), torch.bfloat16, "running_mean")
+    _close(bn.running_var, 0.9 + 0.1 * y0.var(dim=(0, 2, 3)), torch.bfloat16, "running_var")
+    conv.eval()
+    bn.eval()
+    with torch.no_grad():
+        ye = rnn.conv_bn(conv, bn, _dev(x, torch.bfloat16), "relu")
+    rm, rv = bn.running_mean.double().cpu(), bn.running_var.double().cpu()
+    _close(ye, TF.relu(TF.batch_norm(y0, rm, rv, None, None, False, 0.1, 1e-5)), torch.bfloat16, "eval fold")
