@@ -293,12 +293,14 @@ RT_DEV void bn_act_grad(float* g, const T* y, const float* xv, const float* sc, 
 // names r.  The dY of the BatchNorm never exists in memory.
 template <typename T>
 struct GradDirect {
+  static constexpr bool kDirect = true;
   const T* dy;
   int c;
   template <int VEC> RT_DEV void load(long r, int ch0, float* g, int cvalid) const { load_vec<T, VEC>(dy + r * c + ch0, g, cvalid); }
 };
 template <typename T>
 struct GradPool {
+  static constexpr bool kDirect = false;
   const T* dyp;
   const uint8_t* idx;
   int c, h, w, ho, wo, p;
@@ -346,12 +348,14 @@ RT_DEV void bn_bwd_coef(int ch0, int c, const float* gamma, const float* beta, c
 
 // Backward pass 1: part[(ch*RB+rb)*2 + {0,1}] = (sum g, sum g*(x-mean)) with g = dy*act'(y).
 // HAS_Y: the activation mask comes from y (residual BNs); otherwise from x (no y registers).
+// gout (HAS_Y): g = dy * act'(y) is also stored (the residual branch's gradient, and the apply
+// pass's input instead of dy and y).
 template <typename T, int VEC, bool HAS_Y, class GS>
 __global__ void __launch_bounds__(256) bn_bwd_stats_kernel(const GS gs, const T* __restrict__ x,
                                                             const T* __restrict__ y, const float* __restrict__ gamma,
                                                             const float* __restrict__ beta, const float* __restrict__ mean,
                                                             const float* __restrict__ sinv, float* __restrict__ part,
-                                                            long rows, int c, int act) {
+                                                            long rows, int c, int act, T* __restrict__ gout) {
   __shared__ float red[2][256][VEC];
   const int cbase = blockIdx.y * 256 * VEC;
   const int cl = min(c - cbase, 256 * VEC);
@@ -391,6 +395,7 @@ __global__ void __launch_bounds__(256) bn_bwd_stats_kernel(const GS gs, const T*
             g[u][j] *= HAS_Y ? act_grad(yv[HAS_Y ? u : 0][j], act)
                              : (fmaf(xv[u][j], sc[j], sh[j]) > 0.f ? 1.f : (act == RTSDS_ACT_LEAKY ? 0.2f : 0.f));
         }
+        if (HAS_Y && gout && r + u * step < rows) store_vec<T, VEC>(gout + (r + u * step) * c + ch0, g[u], c - ch0);
 #pragma unroll
         for (int j = 0; j < VEC; ++j) {
           sg[j] += g[u][j];
@@ -639,18 +644,26 @@ static void bn_bwd_launch(const GS& gs, const void* x, const void* y, void* dx, 
                           int act, int accumulate, const BnWs& w, hipStream_t st, const float* pre = nullptr, int pre_nrb = 0) {
   int rb = bn_rb(rows, c, VEC);
   const float* part = w.part;
+  // residual BatchNorm + ReLU with both gradients wanted: the statistics pass stores
+  // g = dy * relu'(y) as dres, and the apply pass reads g and x (not dy, y) -- one full read
+  // less; g is exactly dy or 0, so the arithmetic is unchanged
+  const bool g_out = !pre && y && act == RTSDS_ACT_RELU && dres && dx && GS::kDirect;
   if (pre) {  // statistics already produced by the consumer conv's data-gradient epilogue
     part = pre;
     rb = pre_nrb;
   } else if (y && act)
     hipLaunchKernelGGL((bn_bwd_stats_kernel<T, VEC, true, GS>), dim3(rb, rt_cdiv(c, 256 * VEC)), dim3(256), 0, st, gs, (const T*)x,
-                       (const T*)y, gamma, beta, smean, sinv, w.part, rows, c, act);
+                       (const T*)y, gamma, beta, smean, sinv, w.part, rows, c, act, g_out ? (T*)dres : (T*)nullptr);
   else
     hipLaunchKernelGGL((bn_bwd_stats_kernel<T, VEC, false, GS>), dim3(rb, rt_cdiv(c, 256 * VEC)), dim3(256), 0, st, gs, (const T*)x,
-                       (const T*)y, gamma, beta, smean, sinv, w.part, rows, c, act);
+                       (const T*)y, gamma, beta, smean, sinv, w.part, rows, c, act, (T*)nullptr);
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(c), dim3(256), 0, st, part, rb, c, rows, gamma, beta, smean, sinv,
                      dgamma, dbeta, w.coef, training, accumulate);
-  if (dx || dres) {
+  if (g_out) {
+    const GradDirect<T> gg{(const T*)dres, c};
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<T, VEC, GradDirect<T>>), dim3(bn_apply_rb(rows, c, VEC), rt_cdiv(c, 256 * VEC)), dim3(256),
+                       0, st, gg, (const T*)x, (const T*)nullptr, (T*)dx, (T*)nullptr, w.coef, rows, c, 0);
+  } else if (dx || dres) {
     hipLaunchKernelGGL((bn_bwd_apply_kernel<T, VEC, GS>), dim3(bn_apply_rb(rows, c, VEC), rt_cdiv(c, 256 * VEC)), dim3(256), 0, st,
                        gs, (const T*)x, (const T*)y, (T*)dx, (T*)dres, w.coef, rows, c, act);
   }

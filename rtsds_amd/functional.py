@@ -586,7 +586,7 @@ def pack_input(x, dtype):
     Differentiable when ``x`` requires grad (discriminator / UpSampler inputs): the gradient
     goes back as the NHWC tensor cast to x's dtype (same logical NCHW shape)."""
     require_hip(x)
-    if x.dtype == dtype and x.dim() == 4 and x.is_contiguous(memory_format=CL) and x.shape[1] > 1:
+    if x.dtype == dtype and x.dim() == 4 and (x.is_contiguous(memory_format=CL) and x.shape[1] > 1 or is_padded_input(x)):
         return x
     if x.requires_grad and torch.is_grad_enabled():
         return PackInputFn.apply(x, dtype)
@@ -602,6 +602,23 @@ class PackInputFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         return cast(nhwc(dy), ctx.xdtype), None
+
+
+def pack_input_into(x, y):
+    """pack_input(x, y.dtype) written into the existing packed tensor ``y`` (same shape): a
+    captured graph's input buffer refilled with one pass over x."""
+    require_hip(x)
+    xf = (x if x.dtype == torch.float32 else cast(x, torch.float32)).contiguous()
+    n, c, h, w = xf.shape
+    if tuple(y.shape) != (n, c, h, w):
+        raise RuntimeError("rtsds_amd.pack_input_into: shape mismatch")
+    if is_padded_input(y):
+        lib.rtsds_nchw_to_nhwc_pad(_P(xf), _P(y), n, c, h, w, y._rt_cpad, 0 if y.dtype == torch.float32 else 1, stream())
+    elif y.is_contiguous(memory_format=CL):
+        lib.rtsds_nchw_to_nhwc(_P(xf), _P(y), n, c, h, w, 0 if y.dtype == torch.float32 else 1, stream())
+    else:
+        raise RuntimeError("rtsds_amd.pack_input_into: y is not a packed input")
+    return y
 
 
 def _pack(x, dtype):

@@ -110,6 +110,8 @@ class BiSeNet(torch.nn.Module):
     # inference (eval, no autograd): resizes written into the fusion module's concatenated input
     # and the attention tail + final 1x1 conv fused (False: the separate ops, for A/B tests)
     inference_fusions = True
+    # forward() starts with nn.to_input: runtime.GraphedForward may capture from the packed input
+    accepts_packed_input = True
 
     def __init__(self, num_classes, context_path, with_interpolation=True):
         super().__init__()

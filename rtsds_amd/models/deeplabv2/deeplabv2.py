@@ -74,6 +74,9 @@ class ClassifierModule(nn.Module):
 
 
 class ResNetMulti(nn.Module):
+    # forward() starts with nn.to_input: runtime.GraphedForward may capture from the packed input
+    accepts_packed_input = True
+
     def __init__(self, block, layers, num_classes):
         self.inplanes = 64
         super(ResNetMulti, self).__init__()

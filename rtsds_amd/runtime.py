@@ -323,9 +323,24 @@ class GraphedForward:
     new batch into the captured input buffer and return the captured output buffer (valid
     until the next replay)."""
 
-    def __init__(self, module, x, warmup=2):
+    def __init__(self, module, x, warmup=2, packed=None):
+        """``packed``: the module's forward starts with ``nn.to_input`` (the reference-layout
+        NCHW fp32 batch -> the packed compute-dtype input): the graph is captured from the packed
+        tensor and each replay packs the new batch straight into it (one pass over the batch
+        instead of a copy into a captured fp32 buffer plus the pack).  Default: on when the
+        module says so (``accepts_packed_input``)."""
         self.module = module
-        self.static_in = x.detach().clone()
+        if packed is None:
+            packed = bool(getattr(module, "accepts_packed_input", False)) and x.dtype == torch.float32
+        self.packed = packed
+        if packed:
+            from .functional import pack_input
+            self.in_shape, self.in_dtype = tuple(x.shape), x.dtype
+            self.static_in = pack_input(x.detach(), compute_dtype())
+            if self.static_in.data_ptr() == x.data_ptr():
+                self.static_in = self.static_in.clone()
+        else:
+            self.static_in = x.detach().clone()
         side = torch.cuda.Stream(device=x.device)
         side.wait_stream(torch.cuda.current_stream(x.device))
         with torch.no_grad(), torch.cuda.stream(side):
@@ -342,9 +357,15 @@ class GraphedForward:
         self.runner = GraphRunner(self.graph)
 
     def __call__(self, x):
-        if x.shape != self.static_in.shape or x.dtype != self.static_in.dtype:
-            raise RuntimeError("GraphedForward: input shape/dtype differs from the captured one")
-        self.static_in.copy_(x)
+        if self.packed:
+            if tuple(x.shape) != self.in_shape or x.dtype != self.in_dtype:
+                raise RuntimeError("GraphedForward: input shape/dtype differs from the captured one")
+            from .functional import pack_input_into
+            pack_input_into(x, self.static_in)
+        else:
+            if x.shape != self.static_in.shape or x.dtype != self.static_in.dtype:
+                raise RuntimeError("GraphedForward: input shape/dtype differs from the captured one")
+            self.static_in.copy_(x)
         for refresh in self.folds:  # BatchNorm folds the graph reads (recomputed if stale)
             refresh()
         self.runner.replay()
