@@ -346,7 +346,10 @@ RT_DEV void bn_bwd_coef(int ch0, int c, const float* gamma, const float* beta, c
   }
 }
 
-// Backward pass 1: part[(ch*RB+rb)*2 + {0,1}] = (sum g, sum g*(x-mean)) with g = dy*act'(y).
+// Backward pass 1: part[(rb*c+ch)*2 + {0,1}] = (sum g, sum g*(x-mean)) with g = dy*act'(y) --
+// row-block-major, so each block's partials leave as contiguous stores (channel-major rows
+// scattered 8-B stores RB*c*8 bytes apart: 16 MB of them for 1024 channels).  Merged by
+// bn_bwd_finalize_rb_kernel.
 // HAS_Y: the activation mask comes from y (residual BNs); otherwise from x (no y registers).
 // gout (HAS_Y): g = dy * act'(y) is also stored (the residual branch's gradient, and the apply
 // pass's input instead of dy and y).
@@ -369,7 +372,10 @@ __global__ void __launch_bounds__(256) bn_bwd_stats_kernel(const GS gs, const T*
   if (active) {
     bn_bwd_coef<VEC>(ch0, c, gamma, beta, mean, sinv, mu, sc, sh);
     const long step = (long)gridDim.x * L.rpi;
-    constexpr int U = 2;  // rows in flight per thread (loads issued before any use)
+#ifndef BN_STATS_U
+#define BN_STATS_U 2
+#endif
+    constexpr int U = BN_STATS_U;  // rows in flight per thread (loads issued before any use)
     for (long r = (long)blockIdx.x * L.rpi + rg; r < rows; r += U * step) {
       float g[U][VEC], xv[U][VEC], yv[HAS_Y ? U : 1][VEC];
 #pragma unroll
@@ -427,7 +433,7 @@ __global__ void __launch_bounds__(256) bn_bwd_stats_kernel(const GS gs, const T*
         const float a = (red[0][tid][j] + red[0][64 + tid][j]) + (red[0][128 + tid][j] + red[0][192 + tid][j]);
         const float b = (red[1][tid][j] + red[1][64 + tid][j]) + (red[1][128 + tid][j] + red[1][192 + tid][j]);
         if (ch0 + j < c) {
-          *(float2*)(part + ((long)(ch0 + j) * gridDim.x + blockIdx.x) * 2) = make_float2(a, b);
+          *(float2*)(part + ((long)blockIdx.x * c + ch0 + j) * 2) = make_float2(a, b);
         }
       }
     }
@@ -445,7 +451,7 @@ __global__ void __launch_bounds__(256) bn_bwd_stats_kernel(const GS gs, const T*
         b += red[1][gi * L.tpr + cv][j];
       }
       if (ch0 + j < c) {
-        *(float2*)(part + ((long)(ch0 + j) * gridDim.x + blockIdx.x) * 2) = make_float2(a, b);
+        *(float2*)(part + ((long)blockIdx.x * c + ch0 + j) * 2) = make_float2(a, b);
       }
     }
   }
@@ -480,6 +486,52 @@ __global__ void __launch_bounds__(256) bn_bwd_finalize_kernel(const float* __res
   if (threadIdx.x != 0) return;
   sg = (wr[0][0] + wr[1][0]) + (wr[2][0] + wr[3][0]);
   sgx = (wr[0][1] + wr[1][1]) + (wr[2][1] + wr[3][1]);
+  const float inv = sinv[ch], g = gamma ? gamma[ch] : 1.f;
+  if (dgamma) dgamma[ch] = accumulate ? dgamma[ch] + sgx * inv : sgx * inv;
+  if (dbeta) dbeta[ch] = accumulate ? dbeta[ch] + sg : sg;
+  const float a = g * inv;
+  const float invn = 1.f / (float)rows;
+  coef[ch] = a;
+  coef[c + ch] = training ? -a * inv * inv * sgx * invn : 0.f;
+  coef[2 * c + ch] = training ? -a * sg * invn : 0.f;
+  coef[3 * c + ch] = smean[ch];
+  bn_coef(g, beta ? beta[ch] : 0.f, smean[ch], inv, coef[4 * c + ch], coef[5 * c + ch]);
+}
+
+// Backward pass 2 for the row-block-major partials of bn_bwd_stats_kernel: 16 channels per
+// block, lane q (0..15) of a channel sums row blocks q, q + 16, ... (8 in flight, 128-B rows of
+// 16 channels per load group), the 16 lane sums added in a fixed tree order; coefficients as
+// bn_bwd_finalize_kernel.
+__global__ void __launch_bounds__(256) bn_bwd_finalize_rb_kernel(const float* __restrict__ part, int nrb, int c, long rows,
+                                                                  const float* gamma, const float* beta, const float* smean,
+                                                                  const float* sinv, float* dgamma, float* dbeta, float* coef,
+                                                                  int training, int accumulate) {
+  __shared__ float wr[16][16][2];
+  const int cl = threadIdx.x & 15, q = threadIdx.x >> 4, ch = blockIdx.x * 16 + cl;
+  const int chc = min(ch, c - 1);
+  float sg = 0.f, sgx = 0.f;
+  for (int b0 = q; b0 < nrb; b0 += 16 * 8) {
+    float2 pv[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int b = min(b0 + 16 * u, nrb - 1);  // clamped: unconditional
+      pv[u] = *(const float2*)(part + ((long)b * c + chc) * 2);
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (b0 + 16 * u < nrb) { sg += pv[u].x; sgx += pv[u].y; }
+  }
+  wr[q][cl][0] = sg;
+  wr[q][cl][1] = sgx;
+  __syncthreads();
+  if (q != 0 || ch >= c) return;
+  float t0[8], t1[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) { t0[i] = wr[2 * i][cl][0] + wr[2 * i + 1][cl][0]; t1[i] = wr[2 * i][cl][1] + wr[2 * i + 1][cl][1]; }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) { t0[i] = t0[2 * i] + t0[2 * i + 1]; t1[i] = t1[2 * i] + t1[2 * i + 1]; }
+  sg = (t0[0] + t0[1]) + (t0[2] + t0[3]);
+  sgx = (t1[0] + t1[1]) + (t1[2] + t1[3]);
   const float inv = sinv[ch], g = gamma ? gamma[ch] : 1.f;
   if (dgamma) dgamma[ch] = accumulate ? dgamma[ch] + sgx * inv : sgx * inv;
   if (dbeta) dbeta[ch] = accumulate ? dbeta[ch] + sg : sg;
@@ -638,11 +690,27 @@ extern "C" int rtsds_bn_fwd(const void* x, const void* res, void* y, long rows, 
   return hipGetLastError() == hipSuccess ? RTSDS_OK : RTSDS_ERR_LAUNCH;
 }
 
+#ifndef BN_BWD_RB_MAX
+#define BN_BWD_RB_MAX 512
+#endif
+#ifndef BN_BWD_RB_DIV
+#define BN_BWD_RB_DIV 8
+#endif
+// Row blocks of the backward statistics pass (row-block-major partials, merged 16 lanes per
+// channel by bn_bwd_finalize_rb_kernel).  At most 512 (tools/ab_bn2.sh, stats pass: 33,540 x
+// 1024 58.8 -> 29.2 us, 262,144 x 128 41.3 -> 27.7 us, 262,144 x 64 17.6 -> 15.6 us against 2048
+// channel-major row blocks; finalize unchanged at ~5 us).
+static int bn_bwd_rb(long rows, int c, int vec) {
+  const long need = bn_need(rows, c, vec);
+  long rb = std::min<long>(need, BN_BWD_RB_MAX);
+  rb = std::max<long>(1, std::min<long>(rb, (need + BN_BWD_RB_DIV - 1) / BN_BWD_RB_DIV));
+  return (int)rb;
+}
 template <typename T, int VEC, class GS>
 static void bn_bwd_launch(const GS& gs, const void* x, const void* y, void* dx, void* dres, float* dgamma, float* dbeta,
                           long rows, int c, const float* gamma, const float* beta, const float* smean, const float* sinv, int training,
                           int act, int accumulate, const BnWs& w, hipStream_t st, const float* pre = nullptr, int pre_nrb = 0) {
-  int rb = bn_rb(rows, c, VEC);
+  int rb = bn_bwd_rb(rows, c, VEC);
   const float* part = w.part;
   // residual BatchNorm + ReLU with both gradients wanted: the statistics pass stores
   // g = dy * relu'(y) as dres, and the apply pass reads g and x (not dy, y) -- one full read
@@ -657,8 +725,12 @@ static void bn_bwd_launch(const GS& gs, const void* x, const void* y, void* dx, 
   else
     hipLaunchKernelGGL((bn_bwd_stats_kernel<T, VEC, false, GS>), dim3(rb, rt_cdiv(c, 256 * VEC)), dim3(256), 0, st, gs, (const T*)x,
                        (const T*)y, gamma, beta, smean, sinv, w.part, rows, c, act, (T*)nullptr);
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(c), dim3(256), 0, st, part, rb, c, rows, gamma, beta, smean, sinv,
-                     dgamma, dbeta, w.coef, training, accumulate);
+  if (pre)  // channel-major [c][tile][2] partials of the data-gradient epilogue
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(c), dim3(256), 0, st, part, rb, c, rows, gamma, beta, smean, sinv,
+                       dgamma, dbeta, w.coef, training, accumulate);
+  else
+    hipLaunchKernelGGL(bn_bwd_finalize_rb_kernel, dim3(rt_cdiv(c, 16)), dim3(256), 0, st, part, rb, c, rows, gamma, beta, smean,
+                       sinv, dgamma, dbeta, w.coef, training, accumulate);
   if (g_out) {
     const GradDirect<T> gg{(const T*)dres, c};
     hipLaunchKernelGGL((bn_bwd_apply_kernel<T, VEC, GradDirect<T>>), dim3(bn_apply_rb(rows, c, VEC), rt_cdiv(c, 256 * VEC)), dim3(256),
