@@ -183,7 +183,7 @@ template <typename T> RT_DEV typename VecT<T>::v16 vzero() {
 //       swizzled unpadded image above, the next K-tile's DMA in flight across the barrier
 //       (counted vmcnt, raw s_barrier); 0 = register-staged double buffer.
 template <typename T, int MODE, int BM, int BN, int BK, int WM, int WN, int ALA, int ALB, int GL>
-__global__ void __launch_bounds__(256) conv_gemm_kernel(const ConvArgs P0) {
+__global__ void __launch_bounds__(256, (BM == 160 && GL) ? 2 : 1) conv_gemm_kernel(const ConvArgs P0) {
   ConvArgs P = P0;
   if (MODE == MODE_DGRAD && P0.nph > 1) {
     const ConvArgs::Phase& q = P0.phs[blockIdx.z];
@@ -947,19 +947,36 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(const ConvArgs P0) {
         }
         // the BatchNorm input chunks this thread folds into the statistics, loaded up front (all
         // in flight across the LDS staging): read after each chunk's store they serialised
-        // behind it (the compiler cannot reorder them past the possibly-aliasing store)
+        // behind it (the compiler cannot reorder them past the possibly-aliasing store).  The
+        // 160-row tiles (10 chunks per thread) preload half of them (registers: 2 groups per
+        // CU) and the other half as one batch after the first half's stores.
         constexpr int NIT = (BM * CPR + 255) / 256;
-        constexpr int NXP = MODE == MODE_DGRAD ? NIT : 1;
+        constexpr int NPL = NIT > 8 ? (NIT + 1) / 2 : NIT;
+        constexpr int NXP = MODE == MODE_DGRAD ? NPL : 1;
         V16 xpre[NXP];
+        const bool pmask = MODE == MODE_DGRAD && has_mask;  // (mask and accumulate exclusive)
+        const bool ppre_on = pmask || P.accum;
+        V16 ppre[NPL];
+        auto chunk_ok = [&](int it, long& o) {
+          const int c = tid + it * 256;
+          const int row = c / CPR, cc = c - row * CPR;
+          const int gm = m0 + row, gn = n0 + cc * V;
+          const bool ok = c < BM * CPR && gm < P.M && gn < P.N;
+          o = ok ? out_row(gm) * P.N + gn : 0;
+          return ok;
+        };
+        auto load_x = [&](int it, V16& xr) {
+          long o;
+          if (chunk_ok(it, o)) xr = *(const V16*)((const T*)P.bnb_x + o);
+        };
+        auto load_p = [&](int it, V16& pr) {
+          long o;
+          if (chunk_ok(it, o)) pr = pmask ? *(const V16*)((const T*)P.mask + o) : *(const V16*)(out + o);
+        };
         if constexpr (MODE == MODE_DGRAD) {
           if (bnb) {
 #pragma unroll
-            for (int it = 0; it < NIT; ++it) {
-              const int c = tid + it * 256;
-              const int row = c / CPR, cc = c - row * CPR;
-              const int gm = m0 + row, gn = n0 + cc * V;
-              if (c < BM * CPR && gm < P.M && gn < P.N) xpre[it] = *(const V16*)((const T*)P.bnb_x + out_row(gm) * P.N + gn);
-            }
+            for (int it = 0; it < NPL; ++it) load_x(it, xpre[it]);
           }
         }
         __syncthreads();
@@ -979,26 +996,14 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(const ConvArgs P0) {
         }
         // the mask / accumulate operand chunks, loaded before the staging barrier (all in
         // flight, the accumulators dead by now); read after each chunk's store they serialised
-        const bool pmask = MODE == MODE_DGRAD && has_mask;  // (mask and accumulate exclusive)
-        const bool ppre_on = pmask || P.accum;
-        V16 ppre[NIT];
         if (ppre_on) {
 #pragma unroll
-          for (int it = 0; it < NIT; ++it) {
-            const int c = tid + it * 256;
-            const int row = c / CPR, cc = c - row * CPR;
-            const int gm = m0 + row, gn = n0 + cc * V;
-            if (c < BM * CPR && gm < P.M && gn < P.N) {
-              const long o = out_row(gm) * P.N + gn;
-              ppre[it] = pmask ? *(const V16*)((const T*)P.mask + o) : *(const V16*)(out + o);
-            }
-          }
+          for (int it = 0; it < NPL; ++it) load_p(it, ppre[it]);
         }
         __syncthreads();
-#pragma unroll
-        for (int it = 0; it < NIT; ++it) {
+        auto process = [&](int it, const V16& pp, const V16& xr) {
           const int c = tid + it * 256;
-          if (c >= BM * CPR) break;
+          if (c >= BM * CPR) return;
           const int row = c / CPR, cc = c - row * CPR;
           const int gm = m0 + row, gn = n0 + cc * V;
           if (gm < P.M && gn < P.N) {
@@ -1014,12 +1019,12 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(const ConvArgs P0) {
                 for (int q = 0; q < V; ++q) f[q] += to_f(r[q]);
               }
               if (has_mask) {  // (accumulate is refused together with a mask)
-                const V16 r = pmask ? ppre[it] : *(const V16*)((const T*)P.mask + o);
+                const V16 r = pmask ? pp : *(const V16*)((const T*)P.mask + o);
 #pragma unroll
                 for (int q = 0; q < V; ++q) f[q] = mask_f(f[q], to_f(r[q]));
               }
               if (P.accum) {
-                const V16 r = pmask ? *(const V16*)(out + o) : ppre[it];
+                const V16 r = pmask ? *(const V16*)(out + o) : pp;
 #pragma unroll
                 for (int q = 0; q < V; ++q) f[q] += to_f(r[q]);
               }
@@ -1028,7 +1033,6 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(const ConvArgs P0) {
             }
             *(V16*)(out + o) = v;
             if (MODE == MODE_DGRAD && bnb) {
-              const V16 xr = xpre[MODE == MODE_DGRAD ? it : 0];
 #pragma unroll
               for (int q = 0; q < V; ++q) {
                 const float xv = to_f(xr[q]);
@@ -1039,6 +1043,19 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(const ConvArgs P0) {
               }
             }
           }
+        };
+#pragma unroll
+        for (int it = 0; it < NPL; ++it) process(it, ppre[it], xpre[MODE == MODE_DGRAD ? it : 0]);
+        if constexpr (NPL < NIT) {
+#pragma unroll
+          for (int k = 0; k < NIT - NPL; ++k) {
+            if constexpr (MODE == MODE_DGRAD) {
+              if (bnb) load_x(NPL + k, xpre[k]);
+            }
+            if (ppre_on) load_p(NPL + k, ppre[k]);
+          }
+#pragma unroll
+          for (int k = 0; k < NIT - NPL; ++k) process(NPL + k, ppre[k], xpre[MODE == MODE_DGRAD ? k : 0]);
         }
         if (bnb) {
           // threads tid = cc + CPR * k share chunk cc: sum their partials in a fixed order
@@ -1365,7 +1382,7 @@ static void launch(const ConvArgs& p, int splits, hipStream_t st) {
 // workgroups on the 256 CUs.  bf16: 128x128 (or 160x128, see below) / 128x64 / 256x32 (19- and
 // 1-channel outputs), falling back to 64x64 / 128x32 for small-M layers (ResNet layer4, pooled
 // vectors).
-static void pick_tile(long M, int N, bool b16, int& bm, int& bn, bool fwd = false, long K = 0) {
+static void pick_tile(long M, int N, bool b16, int& bm, int& bn, bool fwd = false, long K = 0, bool m160 = false) {
   auto blocks = [&](int a, int b) { return ((M + a - 1) / a) * (long)((N + b - 1) / b); };
   if (b16) {
     // short reductions (K <= 512: 1-8 K-steps, DeepLab's layer1-3 1x1 convs) cannot hide the
@@ -1385,7 +1402,7 @@ static void pick_tile(long M, int N, bool b16, int& bm, int& bn, bool fwd = fals
       // 128 (2 rounds, the second 3 % full) vs 420 of 160 (1 round)
       bn = 128;
       const long r128 = (blocks(128, 128) + 511) / 512, r160 = (blocks(160, 128) + 511) / 512;
-      bm = fwd && r160 * 160 < r128 * 128 ? 160 : 128;
+      bm = (fwd || m160) && r160 * 160 < r128 * 128 ? 160 : 128;
     }
     else if (blocks(128, 64) >= 384) { bm = 128; bn = 64; }
     else { bm = 64; bn = 64; }
@@ -1417,13 +1434,13 @@ static void launch_al(const ConvArgs& p, int cr, hipStream_t st, int splits = 1)
 template <typename T, int MODE>
 static void dispatch_align(const ConvArgs& p, int cr, hipStream_t st, int splits = 1) {
   int bm, bn;
-  pick_tile(p.M, p.N, sizeof(T) == 2, bm, bn, MODE == MODE_FWD, p.K);
+  pick_tile(p.M, p.N, sizeof(T) == 2, bm, bn, MODE == MODE_FWD, p.K, MODE == MODE_DGRAD);
   if constexpr (sizeof(T) == 2) {
     if (bn == 32 && bm == 256) launch_al<T, MODE, 256, 32, 32, 4, 1>(p, cr, st, splits);
     else if (bn == 32) launch_al<T, MODE, 128, 32, 32, 4, 1>(p, cr, st, splits);
     else if (bn == 64 && bm == 128) launch_al<T, MODE, 128, 64, 32, 2, 2>(p, cr, st);
     else if (bn == 64) launch_al<T, MODE, 64, 64, 64, 2, 2>(p, cr, st);
-    else if (MODE == MODE_FWD && bm == 160) launch_al<T, MODE_FWD, 160, 128, 64, 2, 2>(p, cr, st);
+    else if (MODE != MODE_WGRAD && bm == 160) launch_al<T, MODE, 160, 128, 64, 2, 2>(p, cr, st);
     else launch_al<T, MODE, 128, 128, 64, 2, 2>(p, cr, st);
   } else {
     if (bn == 32) launch_al<T, MODE, 128, 32, 16, 4, 1>(p, cr, st);
@@ -2175,7 +2192,7 @@ extern "C" int rtsds_conv2d_dgrad_bnstats_tiles(const rtsds_conv_desc* d) {
   if (dgrad_hconv(d, kp) || dgrad_split(d, kp).splits > 1) return 0;
   int bm, bn;
   const long M = (long)d->n * d->h * d->w;
-  pick_tile(M, d->c, true, bm, bn, false, (long)d->kh * d->kw * kp);  // dispatch_align's choice
+  pick_tile(M, d->c, true, bm, bn, false, (long)d->kh * d->kw * kp, true);  // dispatch_align's choice
   if (256 % (bn / 8) != 0) return 0;
   return (int)((M + bm - 1) / bm);
 }
