@@ -79,6 +79,15 @@ int rtsds_conv2d_fwd(const rtsds_conv_desc* d, const void* x, const void* w, con
 int rtsds_conv2d_fwd_bn(const rtsds_conv_desc* d, const void* x, const void* w, const float* scale,
                         const float* shift, const void* res, void* y, int act, void* ws, size_t ws_bytes,
                         void* stream);
+/* Inference stem: eval conv + BatchNorm(running stats) + act + MaxPool2d(3, 2, pool_pad) in one
+ * launch (torchvision ResNet conv1 -> bn1 -> relu -> maxpool, deeplabv2.py:106-110): y is the
+ * pooled [n][hp][wp][k] NHWC output (hp / wp from the caller: floor or ceil mode); windows
+ * skip positions outside the conv output.  Equal to rtsds_conv2d_fwd_bn + rtsds_maxpool_fwd.
+ * RTSDS_ERR_UNSUPPORTED outside the 3-channel 7x7 stride-2 image conv with 64 outputs (bf16).
+ * Same workspace as rtsds_conv2d_fwd.                                                       */
+int rtsds_conv2d_fwd_bn_maxpool(const rtsds_conv_desc* d, const void* x, const void* w, const float* scale,
+                                const float* shift, void* y, int act, int hp, int wp, int pool_pad, void* ws,
+                                size_t ws_bytes, void* stream);
 /* dx (+)= conv_transpose(dy, w) (accumulate != 0: dx += ...).  Needs ws >=
  * rtsds_conv2d_dgrad_workspace(d).  Strides 1 and 2 only.                               */
 size_t rtsds_conv2d_dgrad_workspace(const rtsds_conv_desc* d);

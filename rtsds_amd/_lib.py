@@ -44,6 +44,8 @@ SIGNATURES = {
     "rtsds_conv2d_fwd_stats_tiles": (c_int, [ctypes.POINTER(ConvDesc)]),
     "rtsds_conv2d_fwd": (c_int, [ctypes.POINTER(ConvDesc), P, P, P, P, c_int, P, P, c_size_t, P]),
     "rtsds_conv2d_fwd_bn": (c_int, [ctypes.POINTER(ConvDesc), P, P, P, P, P, P, c_int, P, c_size_t, P]),
+    "rtsds_conv2d_fwd_bn_maxpool": (c_int, [ctypes.POINTER(ConvDesc), P, P, P, P, P, c_int, c_int, c_int, c_int, P,
+                                            c_size_t, P]),
     "rtsds_conv2d_dgrad_workspace": (c_size_t, [ctypes.POINTER(ConvDesc)]),
     "rtsds_conv2d_dgrad_pack_bytes": (c_size_t, [ctypes.POINTER(ConvDesc)]),
     "rtsds_conv2d_dgrad_pack_many": (c_int, [c_int, ctypes.POINTER(ConvDesc), P, P, P]),

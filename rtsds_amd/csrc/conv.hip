@@ -1745,6 +1745,9 @@ void hconv_dgrad(const rtsds_conv_desc* d, const void* dyp, int kp, const void* 
 bool pw_ok(const rtsds_conv_desc* d);
 // Direct MFMA conv for the 3-channel stride-2 image convs (imgconv.hip).
 bool imgconv_ok(const rtsds_conv_desc* d);
+bool imgconv_pool_ok(const rtsds_conv_desc* d, int hp, int wp);
+void imgconv_pool_fwd(const rtsds_conv_desc* d, const void* x4, const void* w, const float* shift, const float* scale, void* y,
+                      int act, int hp, int wp, int pp, hipStream_t st);
 int imgconv_tiles(const rtsds_conv_desc* d);
 void imgconv_fwd(const rtsds_conv_desc* d, const void* x4, const void* w, const float* bias, const float* scale, void* y,
                  int act, float* stats, hipStream_t st);
@@ -1944,6 +1947,23 @@ extern "C" int rtsds_conv2d_fwd_bn(const rtsds_conv_desc* d0, const void* x, con
   p.K = d.kh * d.kw * d.c;
   if (d.dtype == RTSDS_BF16) dispatch_align<bf16, MODE_FWD>(p, d.c, st);
   else dispatch_align<float, MODE_FWD>(p, d.c, st);
+  return hipGetLastError() == hipSuccess ? RTSDS_OK : RTSDS_ERR_LAUNCH;
+}
+
+extern "C" int rtsds_conv2d_fwd_bn_maxpool(const rtsds_conv_desc* d0, const void* x, const void* w, const float* scale,
+                                           const float* shift, void* y, int act, int hp, int wp, int pool_pad, void* ws,
+                                           size_t ws_bytes, void* stream) {
+  if (!scale || !shift || (act & RTSDS_ACCUMULATE)) return RTSDS_ERR_UNSUPPORTED;
+  int e = check_desc(d0);
+  if (e) return e;
+  if (!imgconv_pool_ok(d0, hp, wp) || pool_pad < 0 || pool_pad > 1) return RTSDS_ERR_UNSUPPORTED;
+  // the windows must cover the pooled grid: hp <= ceil((ho + 2 pad - 3) / 2) + 1
+  if (hp > (d0->ho + 2 * pool_pad - 3 + 1) / 2 + 1 || wp > (d0->wo + 2 * pool_pad - 3 + 1) / 2 + 1) return RTSDS_ERR_SHAPE;
+  if (ws_bytes < rtsds_conv2d_fwd_workspace(d0)) return RTSDS_ERR_WORKSPACE;
+  const bool x_padded = (act & RTSDS_INPUT_PADDED) != 0;
+  hipStream_t st = (hipStream_t)stream;
+  if (!x_padded) sp_pad4(d0, x, ws, st);
+  imgconv_pool_fwd(d0, x_padded ? x : ws, w, shift, scale, y, act & 0xff, hp, wp, pool_pad, st);
   return hipGetLastError() == hipSuccess ? RTSDS_OK : RTSDS_ERR_LAUNCH;
 }
 

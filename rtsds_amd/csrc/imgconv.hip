@@ -21,9 +21,10 @@
 //  * K order (row tap, superpixel, 8 elements) in 32-deep MFMA steps, identical to the
 //    superpixel GEMM's BK = 32 K-steps, so the accumulators match it bit for bit;
 //  * epilogue: bias or eval-BN scale / shift, activation, the following BatchNorm's per-tile
-//    (count, mean, M2) from the fp32 values (each wave owns whole channels: no LDS reduction),
-//    and the bf16 tile staged through LDS and written as 16-B row chunks (8 KB contiguous per
-//    output row segment).
+//    (count, mean, M2) from the fp32 values, and 8-B stores of 4 channels per pixel straight
+//    from the (transposed) accumulators.
+// Inference also has a variant with the stem's 3x3 stride-2 max pool in the epilogue
+// (imgconv_pool_kernel): the full-resolution activation is never written.
 #include "common.h"
 
 template <int N> RT_DEV void wait_vmcnt_img() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
@@ -297,6 +298,197 @@ __global__ void __launch_bounds__(256, (KH == 7 || WP != 1) ? 2 : 3) imgconv_fwd
   }
 }
 
+// ---- conv + eval BatchNorm (folded scale / shift) + activation + MaxPool2d(3, 2, pp) (the
+// ResNet stem at inference: build_contextpath.py via torchvision resnet; deeplabv2.py:106-110,
+// ceil mode).  A tile is PH pooled rows x 31 pooled columns: conv rows 2 po0 - pp .. + 2 PH and
+// 64 conv columns from 2 pc0 - pp (the 31 windows need 63 of them), (2 PH + 1) x 4 MFMA pixel
+// groups per wave (4 waves x 16 channels).  Each conv value is rounded to bf16 exactly as the conv kernel stores
+// it; the window maximum is taken vertically in registers and horizontally across lanes
+// (ds_bpermute), conv positions outside the conv output are skipped (padding / ceil-mode
+// windows), so the result equals imgconv_fwd_kernel followed by maxpool_fwd_k3 bit for bit.
+namespace {
+constexpr int kPW = 31;  // pooled columns per tile
+}
+struct ImgPoolArgs {
+  const bf16* x4;
+  const bf16* wt;
+  const float* shift;
+  const float* scale;
+  bf16* y;             // [n][hp][wp][64]
+  int n, h, w, ho, wo, ph, pw, act;
+  int hp, wp, pp;      // pooled output size, pool padding
+  int tiles, per;
+};
+template <int KH, int KW, int PH>
+__global__ void __launch_bounds__(256, 2) imgconv_pool_kernel(const ImgPoolArgs P) {
+  constexpr int KWP = (KW + 1) / 2, NQ = KH * KWP, KS = (NQ + 3) / 4;
+  constexpr int CR = 2 * PH + 1, NG = 4 * CR;  // conv rows, pixel groups per tile
+  constexpr int NR = 2 * (CR - 1) + KH;      // input rows of the CR conv rows (stride 2)
+  constexpr int NC = 64 + KWP - 1;
+  constexpr int NP = NR * NC, NI = (NP + 63) / 64, NIW = (NI + 3) / 4;
+  constexpr int W_EL = kCo * KH * KW * 3;
+  constexpr int NWI = (W_EL * 2 + 1023) / 1024, NWIW = (NWI + 3) / 4;
+  constexpr int A_BYTES = NI * 1024;
+  constexpr int NST = 4 * PH;                // output store instructions per wave and tile
+  __shared__ __attribute__((aligned(16))) unsigned char lds[NWI * 1024 + 2 * A_BYTES];
+  unsigned char* const abuf = lds + NWI * 1024;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  int bid;
+  {
+    const int nwg = gridDim.x, b = blockIdx.x;
+    const int xcd = b & 7, q = nwg >> 3, r = nwg & 7;
+    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
+  }
+  const int t0 = bid * P.per, t1 = min(P.tiles, t0 + P.per);
+  const int tw_n = (P.wp + kPW - 1) / kPW, th_n = (P.hp + PH - 1) / PH;
+  const int spw = P.w >> 1, pwp = (P.pw + 1) >> 1;
+  const rsrc_t rx = make_rsrc(P.x4, P.n * P.h * P.w * 8);
+  const rsrc_t ry = make_rsrc(P.y, P.n * P.hp * P.wp * kCo * 2);
+  auto tile_xy = [&](int t, int& img, int& po, int& pc0) {  // po: the tile's first pooled row
+    img = t / (th_n * tw_n);
+    const int rem = t - img * th_n * tw_n, tr = rem / tw_n;
+    po = tr * PH;
+    pc0 = (rem - tr * tw_n) * kPW;
+  };
+  auto issue = [&](int t, int b) {
+    int img, po, pc0;
+    tile_xy(t, img, po, pc0);
+    const int cr0 = 2 * po - P.pp, cc0 = 2 * pc0 - P.pp;
+    const int ih0 = 2 * cr0 - P.ph, j0 = cc0 - pwp;
+#pragma unroll
+    for (int i = 0; i < NIW; ++i) {
+      const int ins = wave + 4 * i;
+      if (ins < NI) {
+        const int piece = ins * 64 + lane;
+        const int row = piece / NC, col = piece - row * NC;
+        const int ih = ih0 + row, j = j0 + col;
+        const bool ok = piece < NP && (unsigned)ih < (unsigned)P.h && (unsigned)j < (unsigned)spw;
+        buf_lds16(rx, abuf + b * A_BYTES + ins * 1024, ok ? ((img * P.h + ih) * spw + j) * 16 : (int)0x80000000, 0);
+      }
+    }
+  };
+  const rsrc_t rw = make_rsrc(P.wt, W_EL * 2);
+#pragma unroll
+  for (int i = 0; i < NWIW; ++i) {
+    const int ins = wave + 4 * i;
+    if (ins < NWI) buf_lds16(rw, lds + ins * 1024, (ins * 64 + lane) * 16, 0);
+  }
+  if (t0 < t1) issue(t0, 0);
+  const int fr = lane & 15, fc = lane >> 4;
+  const int nb = wave * 16 + 4 * fc;         // this lane's output channels nb .. nb + 3
+  float bv[4], sv[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    bv[e] = P.shift ? P.shift[nb + e] : 0.f;
+    sv[e] = P.scale ? P.scale[nb + e] : 1.f;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  const bf16* ws = (const bf16*)lds;
+  bf16x8 fw[KS];
+  int koff[KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    const int q = 4 * ks + fc;
+    const int r = q / KWP, p = q - r * KWP;
+    const int n = wave * 16 + fr;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int s = 2 * p - 1 + (e >> 2), ch = e & 3;
+      bf16 v = (bf16)0.f;
+      if (q < NQ && ch < 3 && s >= 0 && s < KW) v = ws[((n * KH + r) * KW + s) * 3 + ch];
+      fw[ks][e] = v;
+    }
+    const int qq = q < NQ ? q : 0;
+    koff[ks] = ((qq / KWP) * NC + (qq % KWP) + fr) * 16;
+  }
+  auto act_f = [&](float t) {
+    if (P.act == RTSDS_ACT_RELU) return fmaxf(t, 0.f);
+    if (P.act == RTSDS_ACT_LEAKY) return t > 0.f ? t : 0.2f * t;
+    if (P.act == RTSDS_ACT_SIGMOID) return 1.f / (1.f + expf(-t));
+    return t;
+  };
+  // window maximum with maxpool_fwd_k3's rule (a NaN wins)
+  auto mx = [](float best, float f) { return (f > best || (f != f && best == best)) ? f : best; };
+
+  for (int t = t0; t < t1; ++t) {
+    const int b = (t - t0) & 1;
+    if (t > t0) wait_vmcnt_img<NST>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (t + 1 < t1) issue(t + 1, b ^ 1);
+    int img, po, pc0;
+    tile_xy(t, img, po, pc0);
+    const int cr0 = 2 * po - P.pp, cc0 = 2 * pc0 - P.pp;
+
+    // NG pixel groups: conv row g / 4, columns 16 (g % 4) + (lane & 15)
+    f32x4 acc[NG];
+#pragma unroll
+    for (int g = 0; g < NG; ++g) acc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const unsigned char* ab = abuf + b * A_BYTES;
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+      const int goff = ((2 * (g >> 2)) * NC + (g & 3) * 16) * 16;
+      bf16x8 fa[KS];
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) fa[ks] = *(const bf16x8*)(ab + koff[ks] + goff);
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[ks], fa[ks], acc[g], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int pr = 0; pr < PH; ++pr) {
+      // vertical maxima of the bf16-rounded conv outputs (invalid conv positions skipped)
+      float vm[4][4];
+#pragma unroll
+      for (int cg = 0; cg < 4; ++cg) {
+        const int cc = cc0 + cg * 16 + fr;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) vm[cg][e] = -INFINITY;
+        bool any = false;
+#pragma unroll
+        for (int tr = 0; tr < 3; ++tr) {
+          const int cr = cr0 + 2 * pr + tr;
+          if ((unsigned)cr < (unsigned)P.ho && (unsigned)cc < (unsigned)P.wo) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const float v = (float)(bf16)act_f(fmaf(acc[(2 * pr + tr) * 4 + cg][e], sv[e], bv[e]));
+              vm[cg][e] = any ? mx(vm[cg][e], v) : v;
+            }
+            any = true;
+          }
+        }
+      }
+      // horizontal: pooled column j = 8 cg + fr / 2 (even lanes) covers local conv columns
+      // fr, fr + 1, fr + 2 of group cg (fr + 2 = 16: lane 0 of group cg + 1)
+#pragma unroll
+      for (int cg = 0; cg < 4; ++cg) {
+        const int l1 = (lane & ~15) | ((fr + 1) & 15), l2 = (lane & ~15) | ((fr + 2) & 15);
+        float o[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float a1 = __shfl(vm[cg][e], l1, 64);
+          const float a2s = __shfl(vm[cg][e], l2, 64), a2n = __shfl(vm[cg < 3 ? cg + 1 : cg][e], l2, 64);
+          const float a2 = fr + 2 < 16 ? a2s : a2n;  // (the selection is the reader's)
+          // window order: left column, then middle, then right (skip -inf = no valid position)
+          float best = vm[cg][e];
+          best = a1 == -INFINITY ? best : (best == -INFINITY ? a1 : mx(best, a1));
+          best = a2 == -INFINITY ? best : (best == -INFINITY ? a2 : mx(best, a2));
+          o[e] = best;
+        }
+        const int pc = pc0 + cg * 8 + (fr >> 1), pry = po + pr;
+        const bool ok = (fr & 1) == 0 && cg * 8 + (fr >> 1) < kPW && pry < P.hp && pc < P.wp;
+        bf16x4 ov;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) ov[e] = (bf16)o[e];
+        store8(ry, ov, ok ? (((img * P.hp + pry) * P.wp + pc) * kCo + nb) * 2 : (int)0x80000000);
+      }
+    }
+  }
+}
+
 // ---- host -------------------------------------------------------------------------------
 // The superpixel geometry of conv.hip's sp_path with 64 output channels and a 7x7 or 3x3 kernel.
 bool imgconv_ok(const rtsds_conv_desc* d) {
@@ -347,4 +539,31 @@ void imgconv_fwd(const rtsds_conv_desc* d, const void* x4, const void* w, const 
   if (d->kh == 7) hipLaunchKernelGGL((imgconv_fwd_kernel<7, 7, 2>), dim3(grid), dim3(256), 0, st, a);
   else if (stats) hipLaunchKernelGGL((imgconv_fwd_kernel<3, 3, 1>), dim3(grid), dim3(256), 0, st, a);
   else hipLaunchKernelGGL((imgconv_fwd_kernel<3, 3, 2>), dim3(grid), dim3(256), 0, st, a);
+}
+
+// Pooled stem at inference (imgconv_pool_kernel): conv + folded BN + act + MaxPool2d(3, 2, pp).
+bool imgconv_pool_ok(const rtsds_conv_desc* d, int hp, int wp) {
+  return imgconv_ok(d) && d->kh == 7 && hp > 0 && wp > 0 && (long)d->n * hp * wp * kCo * 2 < (1L << 31);
+}
+void imgconv_pool_fwd(const rtsds_conv_desc* d, const void* x4, const void* w, const float* shift, const float* scale, void* y,
+                      int act, int hp, int wp, int pp, hipStream_t st) {
+  ImgPoolArgs a;
+  a.x4 = (const bf16*)x4; a.wt = (const bf16*)w; a.shift = shift; a.scale = scale; a.y = (bf16*)y;
+  a.n = d->n; a.h = d->h; a.w = d->w; a.ho = d->ho; a.wo = d->wo; a.ph = d->ph; a.pw = d->pw; a.act = act;
+  a.hp = hp; a.wp = wp; a.pp = pp;
+// 2 pooled rows per tile (tools/ab_pool.sh, bs 8 1024x512: 106 us vs 111 at 1 row, 155 at 3 with
+// one group per CU; the separate folded conv + pool take 59 + 63 us)
+#ifndef IMG_POOL_PH
+#define IMG_POOL_PH 2
+#endif
+  a.tiles = d->n * rt_cdiv(hp, IMG_POOL_PH) * rt_cdiv(wp, kPW);
+  static int occ = 0, cus = 0;
+  if (!occ && (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)imgconv_pool_kernel<7, 7, IMG_POOL_PH>, 256, 0) != hipSuccess ||
+               occ < 1))
+    occ = 1;
+  if (!cus && (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0) != hipSuccess || cus < 1)) cus = 256;
+  const int slots = cus * occ;
+  a.per = (a.tiles + slots - 1) / slots;
+  const int grid = (a.tiles + a.per - 1) / a.per;
+  hipLaunchKernelGGL((imgconv_pool_kernel<7, 7, IMG_POOL_PH>), dim3(grid), dim3(256), 0, st, a);
 }

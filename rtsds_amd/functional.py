@@ -413,6 +413,34 @@ def conv_bn_eval(x, weight, bias, wq, stride, padding, dilation, gamma, beta, ru
     return y
 
 
+def conv_bn_maxpool_eval(x, weight, bias, wq, stride, padding, dilation, gamma, beta, running_mean, running_var, eps,
+                         act, pool_k, pool_s, pool_p, ceil_mode):
+    """Inference stem: pool(act(bn(conv(x)))) with the BN folded and the 3x3 stride-2 pool in
+    the conv's epilogue (rtsds_conv2d_fwd_bn_maxpool; the full-resolution activation is never
+    written).  None where that route does not apply (the caller runs the separate ops)."""
+    require_hip(x, weight)
+    if pool_k != 3 or pool_s != 2 or x.dtype != torch.bfloat16:
+        return None
+    k, _, kh, kw = weight.shape
+    flag = INPUT_PADDED if hasattr(x, "_rt_cpad") and \
+        is_padded_input(x, _conv_desc(x, k, kh, kw, stride, padding, dilation)) else 0
+    if not flag:
+        x = nhwc(x)
+    d = _conv_desc(x, k, kh, kw, stride, padding, dilation)
+    hp, wp = pool_out(d.ho, 3, 2, pool_p, ceil_mode), pool_out(d.wo, 3, 2, pool_p, ceil_mode)
+    ss = _bn_fold(gamma, beta, running_mean, running_var, bias, eps, k)
+    y = empty_nhwc(d.n, k, hp, wp, x.dtype, x.device)
+    ws = workspace(lib.rtsds_conv2d_fwd_workspace(ctypes.byref(d)), x.device)
+    try:
+        lib.rtsds_conv2d_fwd_bn_maxpool(ctypes.byref(d), _P(x), _P(wq), _P(ss), ss.data_ptr() + 4 * k, _P(y),
+                                        act | flag, hp, wp, pool_p, _P(ws), ws.numel(), stream())
+    except RuntimeError as e:
+        if "unsupported" in str(e):  # not the stem geometry: the separate ops
+            return None
+        raise
+    return y
+
+
 class ConvSumFn(torch.autograd.Function):
     """sum_i conv_i(x) + bias_i over convs sharing x and output shape (ASPP,
     deeplabv2.py:62-66): one output buffer accumulated in the GEMM epilogue; the backward

@@ -148,8 +148,8 @@ def conv_bn(conv, bn, x, act=None, residual=None, join=None, res_join=None, in_l
 def conv_bn_relu_maxpool(conv, bn, pool, x):
     """pool(relu(bn(conv(x)))) -- the ResNet stem.  Train-mode (batch statistics) bf16 with a
     3x3 stride-2 pool: the BN apply, ReLU and pool run as one pass (functional.bn_relu_maxpool,
-    statistics from the conv epilogue); otherwise the separate ops (eval: BN folded into the
-    conv, then the pool)."""
+    statistics from the conv epilogue); inference: conv + folded BN + ReLU + pool in one launch
+    (bf16 image stem); otherwise the separate ops."""
     use_batch = bn.training or not bn.track_running_stats
     k = pool.kernel_size if isinstance(pool.kernel_size, int) else pool.kernel_size[0]
     s = pool.stride if isinstance(pool.stride, int) else pool.stride[0]
@@ -163,6 +163,13 @@ def conv_bn_relu_maxpool(conv, bn, pool, x):
             nbt = bn.num_batches_tracked if (bn.training and bn.track_running_stats) else None
             return F.bn_relu_maxpool(y, bn.weight, bn.bias, rm, rv, True, bn.momentum, bn.eps, p, pool.ceil_mode, nbt)
         return pool(bn(y, act="relu"))
+    if not use_batch and bn.momentum is not None and _no_grad_needed(conv, bn, x, None) and k == 3 and s == 2:
+        # inference: the pool runs in the folded conv's epilogue (rtsds_conv2d_fwd_bn_maxpool)
+        y = F.conv_bn_maxpool_eval(x, conv.weight, conv.bias, _shadow(conv.weight, x.dtype), conv.stride, conv.padding,
+                                   conv.dilation, bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.eps,
+                                   ACT["relu"], k, s, p, pool.ceil_mode)
+        if y is not None:
+            return y
     return pool(conv_bn(conv, bn, x, "relu"))
 
 

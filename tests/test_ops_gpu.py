@@ -909,3 +909,36 @@ def test_image_conv_direct(kh, pad, bias, hw):
         ye = rnn.conv_bn(conv, bn, _dev(x, torch.bfloat16), "relu")
     rm, rv = bn.running_mean.double().cpu(), bn.running_var.double().cpu()
     _close(ye, TF.relu(TF.batch_norm(y0, rm, rv, None, None, False, 0.1, 1e-5)), torch.bfloat16, "eval fold")
+
+
+@pytest.mark.parametrize("hw,ceil", [((64, 96), False), ((38, 150), False), ((38, 150), True), ((70, 134), True)])
+def test_stem_conv_bn_maxpool_eval_fused(hw, ceil):
+    """Inference stem (imgconv_pool_kernel: conv 7x7 s2 + folded BN + ReLU + MaxPool 3/2/1 in one
+    launch) equals the folded conv followed by the pool bit for bit, incl. ceil mode and tiles
+    past the output edge; and the module path (nn.conv_bn_relu_maxpool) takes it."""
+    from rtsds_amd import nn as rnn
+    h, w = hw
+    g = torch.Generator().manual_seed(h + w)
+    x = F.pack_input((torch.randn(2, 3, h, w, generator=g) * 40).to(DEV), torch.bfloat16)
+    conv = rnn.Conv2d(3, 64, 7, stride=2, padding=3, bias=False).to(DEV)
+    bn = rnn.BatchNorm2d(64).to(DEV)
+    pool = rnn.MaxPool2d(3, 2, 1, ceil_mode=ceil)
+    with torch.no_grad():
+        conv.weight.copy_(torch.randn(64, 3, 7, 7, generator=g) / 12)
+        bn.running_mean.copy_(torch.randn(64, generator=g))
+        bn.running_var.copy_(0.5 + torch.rand(64, generator=g))
+        bn.weight.copy_(torch.randn(64, generator=g))
+        bn.bias.copy_(torch.randn(64, generator=g))
+    conv.eval()
+    bn.eval()
+    with torch.no_grad():
+        wq = _shadow(conv.weight, torch.bfloat16)
+        fused = F.conv_bn_maxpool_eval(x, conv.weight, None, wq, (2, 2), (3, 3), (1, 1), bn.weight, bn.bias,
+                                       bn.running_mean, bn.running_var, bn.eps, 1, 3, 2, 1, ceil)
+        y = F.conv_bn_eval(x, conv.weight, None, wq, (2, 2), (3, 3), (1, 1), bn.weight, bn.bias, bn.running_mean,
+                           bn.running_var, bn.eps, 1)
+        ref = F.max_pool2d(y, 3, 2, 1, ceil)
+        mod = rnn.conv_bn_relu_maxpool(conv, bn, pool, x)
+    assert fused is not None and fused.shape == ref.shape, (None if fused is None else fused.shape, ref.shape)
+    assert torch.equal(fused.float(), ref.float())
+    assert torch.equal(mod.float(), ref.float())

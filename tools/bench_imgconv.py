@@ -44,3 +44,21 @@ for kh, pad in ((7, 3), (3, 1)):
         us = e0.elapsed_time(e1) * 1e3 / iters
         mb = (x.numel() // 3 * 4 * 2 + y.numel() * 2) / 1e6
         print(f"k{kh} {name:15s} {us:7.1f} us  {mb / us:6.2f} TB/s (input + output {mb:.0f} MB)", flush=True)
+# the inference stem with the pool in its epilogue (rtsds_conv2d_fwd_bn_maxpool), bs / size as above
+wt = (torch.randn(64, 3, 7, 7, device=dev) * 0.05).to(torch.bfloat16).contiguous(memory_format=CL)
+d = F._conv_desc(x, 64, 7, 7, (2, 2), (3, 3), (1, 1))
+hp, wp = F.pool_out(d.ho, 3, 2, 1, False), F.pool_out(d.wo, 3, 2, 1, False)
+yp = torch.empty(n, 64, hp, wp, device=dev, dtype=torch.bfloat16).contiguous(memory_format=CL)
+ss = torch.rand(128, device=dev)
+ws = workspace(lib.rtsds_conv2d_fwd_workspace(ctypes.byref(d)), x.device)
+fn = lambda: lib.rtsds_conv2d_fwd_bn_maxpool(ctypes.byref(d), P(x), P(wt), P(ss), ss.data_ptr() + 256, P(yp),  # noqa: E731
+                                             1 | INPUT_PADDED, hp, wp, 1, P(ws), ws.numel(), st)
+for _ in range(5):
+    fn()
+e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+e0.record()
+for _ in range(iters):
+    fn()
+e1.record()
+torch.cuda.synchronize()
+print(f"k7 eval stem+pool  {e0.elapsed_time(e1) * 1e3 / iters:7.1f} us", flush=True)
