@@ -70,6 +70,27 @@ RT_DEV void bil_src(int o, float scale, int in, int& i0, int& i1, float& l0, flo
   l0 = 1.f - l1;
 }
 
+// Smallest output index o in [0, out] whose top tap i0(o) >= target (i0 is non-decreasing in o).
+RT_DEV int bil_first_ge(int target, float s, int in, int out) {
+  if (target <= 0) return 0;
+  if (target >= in) return out;
+  int o = (int)floorf(((float)target + 0.5f) / s - 0.5f);
+  o = max(0, min(out, o));
+  int i0, i1;
+  float l0, l1;
+  while (o > 0) {
+    bil_src(o - 1, s, in, i0, i1, l0, l1);
+    if (i0 < target) break;
+    --o;
+  }
+  while (o < out) {
+    bil_src(o, s, in, i0, i1, l0, l1);
+    if (i0 >= target) break;
+    ++o;
+  }
+  return o;
+}
+
 // Blend of the 4 taps (p00 = (h0,w0), p01 = (h0,w1), p10 = (h1,w0), p11 = (h1,w1)): width
 // inner, height outer (the association of ATen's separable upsample_bilinear2d), explicit fma
 // order -- the fused upsample+CE computes the identical expression from per-column

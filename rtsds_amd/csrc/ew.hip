@@ -893,6 +893,82 @@ __global__ void __launch_bounds__(256) bilinear_fwd_rows_kernel(const T* __restr
   }
 }
 
+// The same resize for upsampling, one workgroup per (image, source row h0, column chunk): every
+// output row whose top tap is h0 blends the same two horizontal blends t0 / t1 (bil_mix's inner
+// terms), so each thread computes them once for its J output vectors of the chunk, keeps them in
+// registers and writes all of the group's rows (~ the scale factor of them) as
+// fmaf(lh1, t1, lh0 * t0) -- bil_mix bit for bit, at 2 VALU ops per element instead of ~12 and
+// 4 LDS reads per element per group instead of per row.
+template <typename T, int J>
+__global__ void __launch_bounds__(256) bilinear_fwd_rowgroup_kernel(const T* __restrict__ x, T* __restrict__ y, int hi, int wi, int c,
+                                                                     int ho, int wo, float sh, float sw, int nchunk, FastDiv f_c) {
+  typedef typename VecT<T>::v16 V16;
+  constexpr int V = VecT<T>::N;
+  extern __shared__ float rows[];  // [2][wi * c]
+  const int grp = blockIdx.x / nchunk, chunk = blockIdx.x - grp * nchunk;
+  const int img = grp / hi, h0 = grp - img * hi;
+  const int oa = bil_first_ge(h0, sh, hi, ho), ob = bil_first_ge(h0 + 1, sh, hi, ho);
+  if (oa >= ob) return;  // no output row starts at h0 (downsampling): whole workgroup
+  const int h1 = h0 + (h0 < hi - 1 ? 1 : 0);
+  const int rl = wi * c;
+  const T* r0 = x + ((long)img * hi + h0) * rl;
+  const T* r1 = x + ((long)img * hi + h1) * rl;
+  for (int e = threadIdx.x; e < rl; e += 256) {
+    rows[e] = to_f(r0[e]);
+    rows[rl + e] = to_f(r1[e]);
+  }
+  __syncthreads();
+  const int nv = wo * c / V;  // (wo * c) % V == 0 (host)
+  const int v0 = (int)((long)nv * chunk / nchunk), v1 = (int)((long)nv * (chunk + 1) / nchunk);
+  float t0[J][V], t1[J][V];
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    const int v = v0 + threadIdx.x + 256 * j;
+    if (v >= v1) break;
+    const int e = v * V;
+    int ow = (int)fdiv((uint32_t)e, f_c), ch = e - ow * c;
+    int w0, w1;
+    float lw0, lw1;
+    bil_src(ow, sw, wi, w0, w1, lw0, lw1);
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+      if (ch == c) {
+        ch = 0;
+        ++ow;
+        bil_src(ow, sw, wi, w0, w1, lw0, lw1);
+      }
+      const float* a = rows + w0 * c + ch;
+      const float* b = rows + w1 * c + ch;
+      t0[j][k] = fmaf(lw1, b[0], lw0 * a[0]);
+      t1[j][k] = fmaf(lw1, b[rl], lw0 * a[rl]);
+      ++ch;
+    }
+  }
+  for (int oh = oa; oh < ob; ++oh) {
+    int i0, i1;
+    float lh0, lh1;
+    bil_src(oh, sh, hi, i0, i1, lh0, lh1);
+    T* yo = y + ((long)img * ho + oh) * wo * c;
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+      const int v = v0 + threadIdx.x + 256 * j;
+      if (v >= v1) break;
+      V16 r;
+#pragma unroll
+      for (int k = 0; k < V; ++k) r[k] = from_f<T>(fmaf(lh1, t1[j][k], lh0 * t0[j][k]));
+      *(V16*)(yo + (long)v * V) = r;
+    }
+  }
+}
+
+#ifndef BIL_ROWGROUP
+#define BIL_ROWGROUP 1
+#endif
+static const bool kBilRowGroup = BIL_ROWGROUP;
+#ifndef BIL_J
+#define BIL_J 2  // output vectors per thread and column chunk (2, 3, 4, 6 measured: 2 best)
+#endif
+
 // Backward, separable gather (deterministic, no atomics): input index i along one axis
 // receives from outputs o with i0(o) == i (weight l0) or i1(o) == i (weight l1); those o lie
 // in [(i-0.5)/s - 0.5, (i+1.5)/s - 0.5], widened by one and tested exactly with bil_src.
@@ -1049,7 +1125,16 @@ extern "C" int rtsds_bilinear_fwd(const void* x, void* y, int n, int hi, int wi,
     const long pix = (long)n * ho * wo;
     if (c % V == 0 && y_ld % V == 0 && y_off % V == 0)
       hipLaunchKernelGGL((bilinear_fwd_kernel<T, 0>), dim3(ew_blocks(pix * (c / V))), dim3(256), 0, st, (const T*)x, (T*)y, n, hi, wi, c, ho, wo, scale_h, scale_w, y_ld, y_off);
-    else if (c >= V && y_ld == c && y_off == 0 && (wo * c) % V == 0 && 2L * wi * c * 4 <= 64 * 1024)
+    else if (c >= V && y_ld == c && y_off == 0 && (wo * c) % V == 0 && 2L * wi * c * 4 <= 64 * 1024 && ho >= hi && kBilRowGroup) {
+      // column chunks: <= 256 * kJ vectors each, and enough workgroups to fill the chip
+      constexpr int kJ = BIL_J;
+      const int nv = wo * c / V;
+      int nchunk = std::max((nv + 256 * kJ - 1) / (256 * kJ), (1024 + n * hi - 1) / (n * hi));
+      nchunk = std::min(nchunk, std::max(1, nv / 64));
+      nchunk = std::max(nchunk, (nv + 256 * kJ - 1) / (256 * kJ));
+      hipLaunchKernelGGL((bilinear_fwd_rowgroup_kernel<T, kJ>), dim3(n * hi * nchunk), dim3(256), 2 * wi * c * 4, st, (const T*)x,
+                         (T*)y, hi, wi, c, ho, wo, scale_h, scale_w, nchunk, fastdiv_make(c));
+    } else if (c >= V && y_ld == c && y_off == 0 && (wo * c) % V == 0 && 2L * wi * c * 4 <= 64 * 1024)
       hipLaunchKernelGGL((bilinear_fwd_rows_kernel<T>), dim3(n * ho), dim3(256), 2 * wi * c * 4, st, (const T*)x, (T*)y, hi, wi, c, ho,
                          wo, scale_h, scale_w, fastdiv_make(c));
     else if (c <= 64)

@@ -52,27 +52,6 @@ struct UpceArgs {
   int nheads, ignore, want_grad;
 };
 
-// Smallest o in [0, out] with i0(o) >= target (i0 is non-decreasing in o).
-RT_DEV int upce_first_ge(int target, float s, int in, int out) {
-  if (target <= 0) return 0;
-  if (target >= in) return out;
-  int o = (int)floorf(((float)target + 0.5f) / s - 0.5f);
-  o = max(0, min(out, o));
-  int i0, i1;
-  float l0, l1;
-  while (o > 0) {
-    bil_src(o - 1, s, in, i0, i1, l0, l1);
-    if (i0 < target) break;
-    --o;
-  }
-  while (o < out) {
-    bil_src(o, s, in, i0, i1, l0, l1);
-    if (i0 >= target) break;
-    ++o;
-  }
-  return o;
-}
-
 RT_DEV float upce_block_sum(float v, float* red) {
   v = wave_sum(v);
   __syncthreads();
@@ -105,9 +84,9 @@ __global__ void __launch_bounds__(256, 3) upce_fwd_kernel(UpceArgs a) {
   const int tr = tt / q.ntc, tc = tt - tr * q.ntc;
   const int r0 = tr * TH, c0 = tc * TW;
   const int rows_l = min(TH + 1, q.hl - r0), cols_l = min(TW1, q.wl - c0);
-  const int y_lo = upce_first_ge(r0, q.sh, q.hl, q.H), y_hi = upce_first_ge(r0 + TH, q.sh, q.hl, q.H);
-  const int x_lo = upce_first_ge(c0, q.sw, q.wl, q.W);
-  const int x_hi = upce_first_ge(c0 + TW, q.sw, q.wl, q.W);
+  const int y_lo = bil_first_ge(r0, q.sh, q.hl, q.H), y_hi = bil_first_ge(r0 + TH, q.sh, q.hl, q.H);
+  const int x_lo = bil_first_ge(c0, q.sw, q.wl, q.W);
+  const int x_hi = bil_first_ge(c0 + TW, q.sw, q.wl, q.W);
   const int Wt = min(x_hi - x_lo, q.wmax);
   const int tile_el = (TH + 1) * TW1 * C;  // gradient-partial layout (compact classes)
   const int rowp = TW1 * CP, ltile = (TH + 1) * rowp;
@@ -252,7 +231,7 @@ __global__ void __launch_bounds__(256, 3) upce_fwd_kernel(UpceArgs a) {
     int li = 0;
     for (int ya = y_lo; ya < y_lo + Ht; ++li) {
       const int gi = r0 + li;
-      const int yb = min(upce_first_ge(gi + 1, q.sh, q.hl, q.H), y_lo + Ht);
+      const int yb = min(bil_first_ge(gi + 1, q.sh, q.hl, q.H), y_lo + Ht);
       const bool same = gi + 1 >= q.hl;  // bottom clamp: i1 == i0, both taps on row li
       hblend(li, H0);
       hblend(same ? li : li + 1, H1);

@@ -344,6 +344,34 @@ def test_bilinear(geo, dt):
 
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("geo", [((8, 16), None, 8), ((13, 17), (97, 129), None), ((64, 128), (512, 1024), None),
+                                 ((9, 9), (9, 9), None), ((7, 5), (20, 31), None)])
+def test_bilinear_narrow_channels(geo, dt):
+    """19-class logits (channel count not a 16-B multiple): the row-group upsample kernel
+    (bilinear_fwd_rowgroup_kernel) vs torch fp64, and bit-identical to the generic per-element
+    path evaluating the same bil_mix expression (an output pitch forces that path)."""
+    (hi, wi), size, sf = geo
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(2, 19, hi, wi, generator=g, dtype=torch.float64) * 3
+    if dt == torch.bfloat16:
+        x = x.bfloat16().double()
+    yr = TF.interpolate(x, size=size, scale_factor=sf, mode="bilinear")
+    xd = _dev(x, dt)
+    geo_ = F.upsample_geometry(xd, size=size, scale_factor=sf)
+    y = F.interpolate_geometry(xd, geo_)
+    _close(y, yr, dt, "y", 1e-5 if dt == torch.float32 else 1e-2)
+    from rtsds_amd._lib import lib
+    from rtsds_amd.functional import _P
+    from rtsds_amd.runtime import stream
+    ho, wo = yr.shape[2], yr.shape[3]
+    wide = torch.zeros(2, ho, wo, 24, device=DEV, dtype=dt)
+    lib.rtsds_bilinear_fwd(_P(xd), _P(wide), 2, hi, wi, 19, ho, wo, float(geo_[2]), float(geo_[3]), 24, 0,
+                           0 if dt == torch.float32 else 1, stream())
+    torch.cuda.synchronize()
+    assert torch.equal(y.permute(0, 2, 3, 1), wide[..., :19])
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 def test_gap_chscale_cat_act(dt):
     g = torch.Generator().manual_seed(4)
     x = torch.randn(3, 24, 7, 9, generator=g, dtype=torch.float64)
