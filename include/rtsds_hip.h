@@ -264,6 +264,14 @@ int rtsds_chscale_bwd(const void* dy, const void* x, const void* a, void* dx, vo
  * of a wider NHWC tensor: pixel pitch *_ld (0 = c), channel offset *_off.               */
 int rtsds_bilinear_fwd(const void* x, void* y, int n, int hi, int wi, int c, int ho, int wo,
                        float scale_h, float scale_w, int y_ld, int y_off, int dtype, void* stream);
+/* Inference: rtsds_bilinear_fwd of (x * s1) * s2 (s1 / s2: optional [n][c] channel scales in the
+ * activation dtype, each product rounded to it as rtsds_chscale_fwd mode 0 stores it) -- the
+ * attention refinement's channel scales (build_bisenet.py:52-53, 157-159) folded into the
+ * eval forward's resize.  Upsampling (ho >= hi) with c, y_ld, y_off multiples of a 16-B vector
+ * only; RTSDS_ERR_UNSUPPORTED otherwise (the caller scales and resizes separately).      */
+int rtsds_bilinear_fwd_scaled(const void* x, const void* s1, const void* s2, void* y, int n, int hi, int wi,
+                              int c, int ho, int wo, float scale_h, float scale_w, int y_ld, int y_off,
+                              int dtype, void* stream);
 /* Backward = separable two-pass gather (W then H) through an fp32 workspace of
  * rtsds_bilinear_bwd_workspace() bytes; deterministic (no atomics).                      */
 size_t rtsds_bilinear_bwd_workspace(int n, int hi, int wi, int c, int ho, int wo);

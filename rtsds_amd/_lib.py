@@ -89,6 +89,7 @@ SIGNATURES = {
     "rtsds_chscale_fwd": (c_int, [P, P, P, c_int, c_long, c_int, c_int, c_int, P]),
     "rtsds_chscale_bwd": (c_int, [P, P, P, P, P, c_int, c_long, c_int, c_int, c_int, P, c_size_t, P]),
     "rtsds_bilinear_fwd": (c_int, [P, P] + [c_int] * 6 + [c_float, c_float, c_int, c_int, c_int, P]),
+    "rtsds_bilinear_fwd_scaled": (c_int, [P, P, P, P] + [c_int] * 6 + [c_float, c_float, c_int, c_int, c_int, P]),
     "rtsds_bilinear_bwd_workspace": (c_size_t, [c_int] * 6),
     "rtsds_bilinear_bwd": (c_int, [P, P] + [c_int] * 6 + [c_float, c_float, c_int, c_int, c_int, P, c_size_t, P]),
     "rtsds_softmax_fwd": (c_int, [P, c_long, c_long, c_long, P, c_int, c_int, c_long, c_int, c_int, P]),

@@ -844,6 +844,61 @@ __global__ void bilinear_fwd_kernel(const T* __restrict__ x, T* __restrict__ y, 
   }
 }
 
+// Upsampling with 16-B channel vectors (the context-path resizes into the FFM concat): one thread
+// per (image, source row h0, output column, channel vector) loads the 4 taps once, forms bil_mix's
+// two horizontal blends and writes every output row whose top tap is h0 (bit-identical to MODE 0;
+// the taps are gathered once per source row instead of once per output row).  s1 / s2 (optional,
+// [n][c]): channel scales applied to each tap first, rounded to T after each as the stored
+// rtsds_chscale_fwd outputs would be (BiSeNet's attention refinement, build_bisenet.py:42-53,
+// 157-159, folded into the eval forward's resize: bit-identical to scale, scale, resize).
+template <typename T>
+__global__ void bilinear_fwd_group_vec_kernel(const T* __restrict__ x, T* __restrict__ y, int n, int hi, int wi, int c, int ho,
+                                              int wo, float sh, float sw, int yld, int yoff, const T* __restrict__ s1,
+                                              const T* __restrict__ s2) {
+  constexpr int V = VecT<T>::N;
+  typedef typename VecT<T>::v16 V16;
+  // grid (column-vector blocks, n * hi): the source row and its output rows are block-uniform
+  const int cpp = c / V;
+  const int img = blockIdx.y / hi, h0 = blockIdx.y - img * hi;
+  const int oa = bil_first_ge(h0, sh, hi, ho), ob = bil_first_ge(h0 + 1, sh, hi, ho);
+  const int h1 = h0 + (h0 < hi - 1 ? 1 : 0);
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (oa >= ob || i >= wo * cpp) return;
+  {
+    const int ow = i / cpp, chunk = i - ow * cpp;
+    int w0, w1;
+    float lw0, lw1;
+    bil_src(ow, sw, wi, w0, w1, lw0, lw1);
+    const T* b = x + (long)img * hi * wi * c + chunk * V;
+    const V16 a = *(const V16*)(b + ((long)h0 * wi + w0) * c), bb = *(const V16*)(b + ((long)h0 * wi + w1) * c);
+    const V16 cc = *(const V16*)(b + ((long)h1 * wi + w0) * c), dd = *(const V16*)(b + ((long)h1 * wi + w1) * c);
+    V16 k1, k2;
+    if (s1) k1 = *(const V16*)(s1 + (long)img * c + chunk * V);
+    if (s2) k2 = *(const V16*)(s2 + (long)img * c + chunk * V);
+    auto tap = [&](T v, int j) {
+      float f = to_f(v);
+      if (s1) f = to_f(from_f<T>(f * to_f(k1[j])));
+      if (s2) f = to_f(from_f<T>(f * to_f(k2[j])));
+      return f;
+    };
+    float t0[V], t1[V];
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+      t0[j] = fmaf(lw1, tap(bb[j], j), lw0 * tap(a[j], j));
+      t1[j] = fmaf(lw1, tap(dd[j], j), lw0 * tap(cc[j], j));
+    }
+    for (int oh = oa; oh < ob; ++oh) {
+      int i0, i1;
+      float lh0, lh1;
+      bil_src(oh, sh, hi, i0, i1, lh0, lh1);
+      V16 r;
+#pragma unroll
+      for (int j = 0; j < V; ++j) r[j] = from_f<T>(fmaf(lh1, t1[j], lh0 * t0[j]));
+      *(V16*)(y + (((long)img * ho + oh) * wo + ow) * yld + yoff + chunk * V) = r;
+    }
+  }
+}
+
 // Narrow channel counts that are not a 16-B multiple (the 19-class logits of the eval forward's
 // final x8 resize, build_bisenet.py:165-166): one workgroup per output row.  The row's two source
 // rows are staged in LDS as fp32 (coalesced), then every thread writes whole 16-B vectors of the
@@ -1123,7 +1178,12 @@ extern "C" int rtsds_bilinear_fwd(const void* x, void* y, int n, int hi, int wi,
   DISPATCH_T(dtype, {
     constexpr int V = VecT<T>::N;
     const long pix = (long)n * ho * wo;
-    if (c % V == 0 && y_ld % V == 0 && y_off % V == 0)
+    // grouped taps pay off from ~3 output rows per source row (x2: 24 vs 17 us at 256 ch, x4:
+    // 26 vs 28 us, tools/ab_bilinear.sh)
+    if (c % V == 0 && y_ld % V == 0 && y_off % V == 0 && ho >= 3 * hi && kBilRowGroup)
+      hipLaunchKernelGGL((bilinear_fwd_group_vec_kernel<T>), dim3(rt_cdiv(wo * (c / V), 256), n * hi), dim3(256), 0, st,
+                         (const T*)x, (T*)y, n, hi, wi, c, ho, wo, scale_h, scale_w, y_ld, y_off, nullptr, nullptr);
+    else if (c % V == 0 && y_ld % V == 0 && y_off % V == 0)
       hipLaunchKernelGGL((bilinear_fwd_kernel<T, 0>), dim3(ew_blocks(pix * (c / V))), dim3(256), 0, st, (const T*)x, (T*)y, n, hi, wi, c, ho, wo, scale_h, scale_w, y_ld, y_off);
     else if (c >= V && y_ld == c && y_off == 0 && (wo * c) % V == 0 && 2L * wi * c * 4 <= 64 * 1024 && ho >= hi && kBilRowGroup) {
       // column chunks: <= 256 * kJ vectors each, and enough workgroups to fill the chip
@@ -1141,6 +1201,20 @@ extern "C" int rtsds_bilinear_fwd(const void* x, void* y, int n, int hi, int wi,
       hipLaunchKernelGGL((bilinear_fwd_kernel<T, 1>), dim3(ew_blocks(pix)), dim3(256), 0, st, (const T*)x, (T*)y, n, hi, wi, c, ho, wo, scale_h, scale_w, y_ld, y_off);
     else
       hipLaunchKernelGGL((bilinear_fwd_kernel<T, 2>), dim3(ew_blocks(pix * c)), dim3(256), 0, st, (const T*)x, (T*)y, n, hi, wi, c, ho, wo, scale_h, scale_w, y_ld, y_off);
+  });
+  RET_LAUNCH();
+}
+extern "C" int rtsds_bilinear_fwd_scaled(const void* x, const void* s1, const void* s2, void* y, int n, int hi, int wi, int c, int ho,
+                                         int wo, float scale_h, float scale_w, int y_ld, int y_off, int dtype, void* stream) {
+  const long total = (long)n * ho * wo * c;
+  if (total <= 0 || hi <= 0 || wi <= 0) return RTSDS_ERR_SHAPE;
+  if (y_ld <= 0) y_ld = c;
+  hipStream_t st = (hipStream_t)stream;
+  DISPATCH_T(dtype, {
+    constexpr int V = VecT<T>::N;
+    if (!(c % V == 0 && y_ld % V == 0 && y_off % V == 0 && ho >= hi)) return RTSDS_ERR_UNSUPPORTED;
+    hipLaunchKernelGGL((bilinear_fwd_group_vec_kernel<T>), dim3(rt_cdiv(wo * (c / V), 256), n * hi), dim3(256), 0, st,
+                       (const T*)x, (T*)y, n, hi, wi, c, ho, wo, scale_h, scale_w, y_ld, y_off, (const T*)s1, (const T*)s2);
   });
   RET_LAUNCH();
 }

@@ -773,6 +773,37 @@ def concat_resized(x0, xs, size):
     return CatResizeFn.apply((int(size[0]), int(size[1])), x0, *xs)
 
 
+def concat_resized_scaled_eval(x0, parts, size):
+    """Inference only: concat_resized(x0, [channel_scale(...channel_scale(x, s1)..., sk) for
+    (x, (s1, ...)) in parts], size) with the (at most two) channel scales applied to the resize's
+    taps (rtsds_bilinear_fwd_scaled; bit-identical to the separate ops).  None when a part's
+    geometry is outside the fused kernel (the caller then runs the separate ops)."""
+    x0 = nhwc(x0)
+    n, c0, h, w = x0.shape
+    ps = []
+    for x, scales in parts:
+        x = nhwc(x)
+        if len(scales) > 2 or x.shape[-2] > h or x.shape[-1] > w:
+            return None
+        ss = [(s if s.dtype == x.dtype else cast(s, x.dtype)).contiguous() for s in scales]
+        ps.append((x, ss + [None] * (2 - len(ss))))
+    ct = c0 + sum(x.shape[1] for x, _ in ps)
+    y = empty_nhwc(n, ct, h, w, x0.dtype, x0.device)
+    off = c0
+    for x, (s1, s2) in ps:
+        _, c, hi, wi = x.shape
+        ho, wo, sh, sw = upsample_geometry(x, size=size)
+        try:
+            lib.rtsds_bilinear_fwd_scaled(_P(x), _P(s1), _P(s2), _P(y), n, hi, wi, c, ho, wo, sh, sw, ct, off, dcode(x), stream())
+        except RuntimeError as e:
+            if "unsupported" in str(e):
+                return None
+            raise
+        off += c
+    lib.rtsds_copy_channels(_P(x0), c0, 0, _P(y), ct, 0, n * h * w, c0, 0, dcode(x0), stream())
+    return y
+
+
 def ffm_head_eval(feature, w1, b1, w2, b2, w3, b3):
     """Inference only: conv3(f * a + f) + b3 with a = sigmoid(conv2(relu(conv1(GAP(f)) + b1)) + b2)
     -- FeatureFusionModule's attention tail and BiSeNet's final 1x1 conv (build_bisenet.py:75-80,

@@ -57,15 +57,18 @@ class AttentionRefinementModule(torch.nn.Module):
         self.in_channels = in_channels
         self.avgpool = AdaptiveAvgPool2d(output_size=(1, 1))
 
-    def forward(self, input, pooled=None):
-        """``pooled``: GAP(input) when the caller already has it (BiSeNet's ARM2 reads the
-        context path's tail, the same kernel on the same tensor)."""
+    def attention(self, input, pooled=None):
+        """sigmoid(BN(conv(GAP(input)))) [N, C, 1, 1]; ``pooled``: GAP(input) when the caller
+        already has it (BiSeNet's ARM2 reads the context path's tail, the same kernel on the
+        same tensor)."""
         if pooled is None:
             pooled = self.avgpool(input)
         assert self.in_channels == pooled.size(1), \
             "in_channels and out_channels should all be {}".format(pooled.size(1))
-        att = conv_bn(self.conv, self.bn, pooled, "sigmoid")
-        return F.channel_scale(input, att)
+        return conv_bn(self.conv, self.bn, pooled, "sigmoid")
+
+    def forward(self, input, pooled=None):
+        return F.channel_scale(input, self.attention(input, pooled))
 
 
 class FeatureFusionModule(torch.nn.Module):
@@ -170,16 +173,25 @@ class BiSeNet(torch.nn.Module):
         else:
             sx = self.saptial_path(x)
             f3, f4, tail = self.context_path(x)
-        cx1 = self.attention_refinement_module1(f3)
-        # ARM2's global average pool is the tail itself (same kernel, same f4)
-        cx2 = F.channel_scale(self.attention_refinement_module2(f4, pooled=tail), tail)
         hw = sx.shape[-2:]
         heads = []
-        if self.inference_fusions and not self.training and not torch.is_grad_enabled() and \
-                sx.shape[1] + cx1.shape[1] + cx2.shape[1] == self.feature_fusion_module.in_channels:
-            # inference: the two resizes write straight into the fusion module's concatenated
-            # input (no cat pass over them; the reference: interpolate, interpolate, cat)
-            cat = F.concat_resized(sx, (cx1, cx2), hw)
+        cat = None
+        infer = self.inference_fusions and not self.training and not torch.is_grad_enabled() and \
+            sx.shape[1] + f3.shape[1] + f4.shape[1] == self.feature_fusion_module.in_channels
+        if infer:
+            # inference: the attention refinements' channel scales and the two resizes write
+            # straight into the fusion module's concatenated input (the reference: scale, scale,
+            # interpolate, interpolate, cat); ARM2's global average pool is the tail itself
+            att1 = self.attention_refinement_module1.attention(f3)
+            att2 = self.attention_refinement_module2.attention(f4, pooled=tail)
+            cat = F.concat_resized_scaled_eval(sx, ((f3, (att1,)), (f4, (att2, tail))), hw)
+        if cat is None:
+            cx1 = self.attention_refinement_module1(f3)
+            # ARM2's global average pool is the tail itself (same kernel, same f4)
+            cx2 = F.channel_scale(self.attention_refinement_module2(f4, pooled=tail), tail)
+        if infer:
+            if cat is None:  # a geometry outside the fused resize
+                cat = F.concat_resized(sx, (cx1, cx2), hw)
             ffm = self.feature_fusion_module
             if self.with_interpolation and ffm.conv1.out_channels == 19 and \
                     (hw[0] * hw[1]) % (8 if sx.dtype == torch.bfloat16 else 4) == 0 and \

@@ -372,6 +372,52 @@ def test_bilinear_narrow_channels(geo, dt):
 
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("geo", [((16, 32), (32, 64)), ((8, 16), (32, 64)), ((13, 17), (50, 61)), ((9, 9), (9, 9))])
+def test_bilinear_grouped_vectors(geo, dt):
+    """Upsampling with 16-B channel vectors (bilinear_fwd_group_vec_kernel: taps gathered once per
+    source row, all output rows of the group written from registers) vs torch fp64, into a
+    pitched channel slice as the FFM concat uses it (output pitch 48, offset 16)."""
+    from rtsds_amd._lib import lib
+    from rtsds_amd.functional import _P
+    from rtsds_amd.runtime import stream
+    (hi, wi), (ho, wo) = geo
+    g = torch.Generator().manual_seed(6)
+    x = torch.randn(2, 32, hi, wi, generator=g, dtype=torch.float64)
+    if dt == torch.bfloat16:
+        x = x.bfloat16().double()
+    yr = TF.interpolate(x, size=(ho, wo), mode="bilinear")
+    xd = _dev(x, dt)
+    y = F.interpolate_bilinear(xd, size=(ho, wo))
+    _close(y, yr, dt, "y", 1e-5 if dt == torch.float32 else 1e-2)
+    cat = torch.zeros(2, ho, wo, 48, device=DEV, dtype=dt)
+    assert lib.rtsds_bilinear_fwd(_P(xd), _P(cat), 2, hi, wi, 32, ho, wo, hi / ho, wi / wo, 48, 16,
+                                  0 if dt == torch.float32 else 1, stream()) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(y.permute(0, 2, 3, 1), cat[..., 16:])
+    assert not cat[..., :16].any()
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_concat_resized_scaled_eval(dt):
+    """BiSeNet eval: ARM channel scales folded into the resize taps (rtsds_bilinear_fwd_scaled)
+    == channel_scale, channel_scale, concat_resized, bit for bit."""
+    g = torch.Generator().manual_seed(8)
+    sx = _dev(torch.randn(2, 16, 32, 64, generator=g), dt)
+    f3 = _dev(torch.randn(2, 32, 16, 32, generator=g), dt)
+    f4 = _dev(torch.randn(2, 64, 8, 16, generator=g), dt)
+    a1, a2, t = (torch.rand(2, c, 1, 1, generator=g).to(DEV, dt) for c in (32, 64, 64))
+    with torch.no_grad():
+        ref = F.concat_resized(sx, (F.channel_scale(f3, a1), F.channel_scale(F.channel_scale(f4, a2), t)), (32, 64))
+        got = F.concat_resized_scaled_eval(sx, ((f3, (a1,)), (f4, (a2, t))), (32, 64))
+    assert got is not None
+    assert torch.equal(got, ref)
+    # a downsampling part is outside the fused kernel: None, the caller runs the separate ops
+    big = _dev(torch.randn(2, 32, 64, 128, generator=g), dt)
+    with torch.no_grad():
+        assert F.concat_resized_scaled_eval(sx, ((big, (a1,)),), (32, 64)) is None
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 def test_gap_chscale_cat_act(dt):
     g = torch.Generator().manual_seed(4)
     x = torch.randn(3, 24, 7, 9, generator=g, dtype=torch.float64)

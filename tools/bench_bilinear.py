@@ -30,5 +30,22 @@ for dt in (torch.bfloat16, torch.float32):
     # non-integer scale, ragged sizes
     x2 = torch.randn(2, 19, 13, 17, generator=g).to(dev, dt).contiguous(memory_format=torch.channels_last)
     out[str(dt) + "_ragged"] = F.interpolate_geometry(x2, F.upsample_geometry(x2, size=(97, 129))).cpu()
+# the context-path resizes of the eval forward (16-B channel vectors, x2 and x4 to 1/8 resolution)
+for c, hi, wi in ((256, 32, 64), (512, 16, 32)):
+    for dt in (torch.bfloat16,):
+        x = torch.randn(8, c, hi, wi, generator=g).to(dev, dt).contiguous(memory_format=torch.channels_last)
+        geo = F.upsample_geometry(x, size=(64, 128))
+        y = F.interpolate_geometry(x, geo)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(50):
+            F.interpolate_geometry(x, geo)
+        e1.record()
+        torch.cuda.synchronize()
+        print(f"{str(dt):16s} {c}ch {hi}x{wi} -> 64x128 bs8: {e0.elapsed_time(e1) / 50 * 1e3:.1f} us")
+        out[f"{dt}_{c}"] = y.cpu()
+        x2 = torch.randn(2, c, 13, 17, generator=g).to(dev, dt).contiguous(memory_format=torch.channels_last)
+        out[f"{dt}_{c}_ragged"] = F.interpolate_geometry(x2, F.upsample_geometry(x2, size=(50, 61))).cpu()
 if len(sys.argv) > 1:
     torch.save(out, sys.argv[1])
