@@ -825,6 +825,23 @@ def test_upsample_softmax_fused(dt, geo):
     assert torch.equal(xd.grad, x2.grad)
 
 
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("shape", [(2, 3, 64, 96), (3, 3, 7, 9), (1, 2, 4, 5)])
+def test_nchw_to_nhwc_pad(shape, dt):
+    """rtsds_nchw_to_nhwc_pad: NCHW fp32 -> NHWC with a 4-channel pitch, pad channels zero (the
+    4-pixel vector kernel for planes of a multiple of 4 pixels, the per-pixel one otherwise)."""
+    from rtsds_amd._lib import lib
+    from rtsds_amd.functional import _P
+    from rtsds_amd.runtime import stream
+    n, c, h, w = shape
+    x = (torch.randn(shape, generator=torch.Generator().manual_seed(3)) * 30).to(DEV)
+    y = torch.full((n, h, w, 4), 7.0, device=DEV, dtype=dt)
+    assert lib.rtsds_nchw_to_nhwc_pad(_P(x), _P(y), n, c, h, w, 4, 0 if dt == torch.float32 else 1, stream()) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(y[..., :c], x.permute(0, 2, 3, 1).to(dt))
+    assert not y[..., c:].any()
+
+
 @pytest.mark.parametrize("kh,pad", [(7, 3), (3, 1)])
 def test_padded_image_input_bit_identical(kh, pad):
     """pack_input writes a 3-channel bf16 image with the 4-channel pitch of the superpixel
