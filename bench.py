@@ -33,6 +33,11 @@ sys.path.insert(0, ROOT)
 
 MFMA_BF16_PEAK_TFLOPS = 2500.0   # MI355X dense bf16 (MI355X_MICROARCH.md)
 NC = 19
+# north_star's inference roofline: BiSeNet-R18 eval forward at 1024x512 is
+# 51.26 GFLOP per image; at bs 8 the per-layer roofline sum_i max(flop_i / 2.5 PF, bytes_i /
+# 8 TB/s) is t_roof = 0.266 ms (conv traffic >= 1.72 GB), the MFMA-only time 0.164 ms
+INFER_GFLOP_PER_IMG = 51.26
+INFER_T_ROOF_MS_BS8 = 0.266
 # default timed steps per workload: >= ~2.4 s of timed work at the round-2 step times, so the
 # driver's own wall clock and GPU-busy sampler can corroborate the measured window
 DEFAULT_STEPS = {"bisenet-seg": 400, "bisenet-da": 160, "deeplab-seg": 70, "deeplab-da": 40}
@@ -352,6 +357,35 @@ def main():
                     net(xb)
                 torch.cuda.synchronize()
                 infer[f"inference_fps_bs{bs}_eager"] = round(bs * (k // 5) * world / (time.perf_counter() - t1), 2)
+                if bs == 8 and dtype == torch.bfloat16:
+                    # north_star's headline: fraction of the MFMA roofline of the bs-8 forward
+                    # (whole forward, graph replay), plus the event-timed conv family of one
+                    # eager eval forward queued behind a GPU spacer (as the train roofline)
+                    fps = infer["inference_fps_bs8"] / world
+                    t_ms = 1000.0 * bs / fps
+                    spacer = torch.randn(8192, 8192, device=dev, dtype=torch.bfloat16)
+                    for _ in range(20):
+                        torch.mm(spacer, spacer)
+                    F.CONV_PROFILE = []
+                    net(xb)
+                    torch.cuda.synchronize()
+                    irecs, F.CONV_PROFILE = F.CONV_PROFILE, None
+                    del spacer
+                    ims = sum(r[0].elapsed_time(r[1]) for r in irecs)
+                    ifl = sum(r[2] for r in irecs)
+                    infer["inference_roofline"] = {
+                        "batch": bs, "gflop_per_image": INFER_GFLOP_PER_IMG, "ms_per_batch": round(t_ms, 4),
+                        "mfma_achieved_tflops": round(INFER_GFLOP_PER_IMG * bs / t_ms, 2),
+                        "peak_tflops": MFMA_BF16_PEAK_TFLOPS,
+                        "mfma_frac": round(INFER_GFLOP_PER_IMG * bs / t_ms / MFMA_BF16_PEAK_TFLOPS, 4),
+                        "t_roof_ms": INFER_T_ROOF_MS_BS8,
+                        "roofline_frac": round(INFER_T_ROOF_MS_BS8 / t_ms, 4),
+                        "conv_family_ms": round(ims, 4), "conv_family_gflop": round(ifl / 1e9, 2),
+                        "conv_family_frac": round(ifl / (ims * 1e-3) / 1e12 / MFMA_BF16_PEAK_TFLOPS, 4) if ims else None,
+                        "conv_launches": len(irecs),
+                        "note": "mfma_frac = 51.26 GFLOP/img x FPS / 2.5 PF; roofline_frac = t_roof / t_measured "
+                                "(SURVEY.md 8(d)); conv_family_* from HIP events around each conv call of one "
+                                "eager eval forward"}
                 del fwd
         net.train()
 

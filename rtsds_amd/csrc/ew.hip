@@ -92,7 +92,9 @@ extern "C" int rtsds_nchw_to_nhwc_pad(const float* x, void* y, int n, int c, int
   const long px = (long)n * h * w;
   if (px <= 0 || c <= 0 || pitch != 4 || c > pitch) return RTSDS_ERR_UNSUPPORTED;
   const long hw = (long)h * w;
-  if (hw % 4 == 0 && hw / 4 < INT_MAX && n <= 65535) {
+  // 16-B vector loads / stores: only for 16-B aligned bases (a view with a storage offset
+  // that is not a multiple of 4 floats takes the per-pixel kernel)
+  if (hw % 4 == 0 && hw / 4 < INT_MAX && n <= 65535 && (((uintptr_t)x | (uintptr_t)y) & 15) == 0) {
     const int hw4 = (int)(hw / 4);
     DISPATCH_T(dtype, hipLaunchKernelGGL((nchw_to_nhwc_pad4_x4_kernel<T>), dim3(std::min(rt_cdiv(hw4, 256), 4096), n), dim3(256), 0,
                                          (hipStream_t)stream, x, (T*)y, c, hw4));

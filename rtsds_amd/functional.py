@@ -432,8 +432,9 @@ def conv_bn_maxpool_eval(x, weight, bias, wq, stride, padding, dilation, gamma, 
     y = empty_nhwc(d.n, k, hp, wp, x.dtype, x.device)
     ws = workspace(lib.rtsds_conv2d_fwd_workspace(ctypes.byref(d)), x.device)
     try:
-        lib.rtsds_conv2d_fwd_bn_maxpool(ctypes.byref(d), _P(x), _P(wq), _P(ss), ss.data_ptr() + 4 * k, _P(y),
-                                        act | flag, hp, wp, pool_p, _P(ws), ws.numel(), stream())
+        with _Timed(d, "fwd"):
+            lib.rtsds_conv2d_fwd_bn_maxpool(ctypes.byref(d), _P(x), _P(wq), _P(ss), ss.data_ptr() + 4 * k, _P(y),
+                                            act | flag, hp, wp, pool_p, _P(ws), ws.numel(), stream())
     except RuntimeError as e:
         if "unsupported" in str(e):  # not the stem geometry: the separate ops
             return None

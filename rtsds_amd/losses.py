@@ -25,9 +25,13 @@ class CrossEntropyLoss(nn.Module):
 class BCEWithLogitsLoss(nn.Module):
     """Mean of the logistic loss.  Under data parallelism the mean runs over every rank's
     elements.  D's logits have a data-independent size, so the global element count is
-    all-reduced once per local size and cached: the ranks see the same sequence of local batch
-    sizes (DistributedSampler pads its shards to equal length, synthetic loaders are equal),
-    so they miss the cache together.  Unequal shards still get the exact weighted mean."""
+    all-reduced once per local size and cached.  The cache miss is a collective, so every rank
+    must miss on the same calls: each rank's sequence of local sizes must be fixed from the
+    first iteration on -- equal shards (DistributedSampler pads its shards to equal length,
+    synthetic loaders are equal, main.py's loaders drop_last) or unequal but fixed shards
+    (those get the exact weighted mean).  A rank that meets a new local size while another
+    rank hits its cache would desynchronise the collectives; the per-rank cache keys are
+    therefore checked for agreement on every miss."""
 
     def __init__(self, reduction="mean"):
         super().__init__()
@@ -48,7 +52,13 @@ class BCEWithLogitsLoss(nn.Module):
         if total is None:
             if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
                 raise RuntimeError("rtsds_amd.BCEWithLogitsLoss: run an eager iteration before graph capture")
-            cnt = torch.full((1,), float(n), dtype=torch.float64, device=input.device)
+            # [local count, 1, number of cached sizes]: the second slot counts the ranks taking
+            # part, the third must agree (all ranks miss together on the same call)
+            cnt = torch.tensor([float(n), 1.0, float(len(self._global))], dtype=torch.float64, device=input.device)
             dist.all_reduce(cnt)  # eager, outside any graph capture: warm-up iterations fill the cache
-            total = self._global[(n, dp_world())] = float(cnt.item())
+            w = dp_world()
+            if int(cnt[1].item()) != w or float(cnt[2].item()) != w * len(self._global):
+                raise RuntimeError("rtsds_amd.BCEWithLogitsLoss: ranks disagree on the global element count "
+                                   "cache (local batch sizes must follow the same pattern on every rank)")
+            total = self._global[(n, w)] = float(cnt[0].item())
         return loss * (n / total)

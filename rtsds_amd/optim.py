@@ -123,6 +123,9 @@ class _Arena:
         self.shadow = torch.empty(total, dtype=torch.bfloat16, device=dev)
         self.steps = [0] * len(params)
         self.touched = [False] * len(params)
+        # per parameter: its gradient's all-reduce has been started (optimizer.start_grad_allreduce
+        # with partial=True); a later gradient write would be missing from the reduced sum
+        self.reduced = None
         self.dpacks = []  # conv weights whose packed dgrad copy this arena refreshes (functional._dgrad_weight)
         with torch.no_grad():
             for i, p in enumerate(params):
@@ -143,8 +146,15 @@ class _Arena:
 
     def _hook(self, i):
         def mark(_p):
+            self._check_open(i)
             self.touched[i] = True
         return mark
+
+    def _check_open(self, i):
+        if self.reduced is not None and self.reduced[i]:
+            raise RuntimeError(f"rtsds_amd.optim: a gradient of parameter {i} ({tuple(self.params[i].shape)}) arrived "
+                               "after its all-reduce started (start_grad_allreduce(partial=True)): the backward cut "
+                               "must separate the parameters of the two phases")
 
     def repack(self):
         """Refresh the packed data-gradient copies of the registered conv weights from the bf16
@@ -165,6 +175,7 @@ class _Arena:
         as having received a gradient this step); None if .grad left the arena."""
         if not self.grad_ptr_ok(i):
             return None
+        self._check_open(i)
         self.touched[i] = True
         return self.params[i].grad
 
@@ -312,6 +323,8 @@ class _FlatOptimizer(torch.optim.Optimizer):
         self._fix_grads(arenas)
         if self._reduced is None:
             self._reduced = [[False] * len(a.params) for a in arenas]
+            for a, red in zip(arenas, self._reduced):
+                a.reduced = red
         bufs = []
         for a, red in zip(arenas, self._reduced):
             idx = [i for i in range(len(a.params)) if not red[i] and (a.touched[i] or not partial)]
@@ -335,6 +348,8 @@ class _FlatOptimizer(torch.optim.Optimizer):
             for fin in self._finish:
                 fin()
             self._finish, self._reduced = [], None
+            for a in arenas:
+                a.reduced = None
             gscale = 1.0
         else:
             self._fix_grads(arenas)

@@ -544,6 +544,11 @@ class GraphedStep:
             best = names.index("branches")
         else:
             best = min(range(len(costs)), key=costs.__getitem__)
-        self._use(best)
-        self.submit_choice = self.variants[best][0]
+        # drop the variants not chosen: their graphs, split-replay clones and the captured
+        # collectives' closures (with a reduced-precision wire, an arena-sized copy each)
+        # would otherwise stay referenced for the whole run ("split" keeps the branch
+        # capture's graphs through its own segment list)
+        self.variants = [self.variants[best]]
+        self._use(0)
+        self.submit_choice = self.variants[0][0]
         self._trial = None

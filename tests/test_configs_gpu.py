@@ -23,6 +23,11 @@ bench times.  Here:
   mode at 1024x512 bs4, plus its bf16 training iteration; a DeepLab-generator DA iteration
   vs the oracle's da_step; the configs[3] / configs[4] DA iterations by size-independent
   properties (fused == unfused loss, hipGraph replay == eager).
+* the measured inference path (bench.py inference_fps_*: no-grad eval forward, BatchNorm
+  folded, fused FFM tail, GraphedForward replay): in fp32 mode at 2 x 3 x 512 x 1024 vs the
+  oracle's eval forward (1e-3 x max|logit|, argmax at safe pixels), and the bench's bf16
+  workload at 8 x 3 x 512 x 1024 vs fp32 mode, bounded by a control that applies bf16's
+  perturbations (rounded weights, input and block outputs) in fp32 arithmetic.
 """
 import math
 
@@ -277,6 +282,111 @@ def test_bisenet_bench_step_bf16_vs_fp32():
     assert fro <= max(5e-2, 3 * fro_c), (fro, fro_c)
     assert agree >= min(0.97, 1 - 3 * (1 - agree_c)), (agree, agree_c)
     assert sign >= min(0.95, 1 - 3 * (1 - sign_c)), (sign, sign_c)
+
+
+# ----------------------------------------------------------------------------- BiSeNet inference
+@pytest.fixture(scope="module")
+def eval_state():
+    """Recipe weights (seed 1) with realistic BatchNorm running statistics: one train-mode
+    forward of the CPU oracle on a 2 x 3 x 512 x 1024 batch with momentum 1 (running = that
+    batch's statistics, unbiased variance as torch), so the eval forward's BatchNorm folds
+    actually normalise.  Returns (oracle in eval mode, state_dict)."""
+    ref = _load(om.BiSeNet(NC, "resnet18"), 1).train()
+    bns = [m for m in ref.modules() if isinstance(m, torch.nn.BatchNorm2d)]
+    for m in bns:
+        m.momentum = 1.0
+    torch.set_num_threads(min(16, torch.get_num_threads()))
+    with torch.no_grad():
+        ref(synthetic_images(2, 512, 1024, seed=50))
+    for m in bns:
+        m.momentum = 0.1
+    return ref.eval(), {k: v.clone() for k, v in ref.state_dict().items()}
+
+
+def _eval_net(sd):
+    net = BiSeNet(NC, "resnet18")
+    net.load_state_dict(sd)
+    return net.to(DEV).eval()
+
+
+def _graphed_eval(net, x, dtype):
+    """The measured inference path (bench.py inference_fps_*): no autograd, BatchNorm folded
+    into the conv epilogues, fused FFM tail, replayed as one hipGraph (runtime.GraphedForward,
+    the batch packed straight into the captured input)."""
+    from rtsds_amd.runtime import GraphedForward
+    with rtsds_amd.precision(dtype), torch.no_grad():
+        fwd = GraphedForward(net, x)
+        fwd(x)
+        out = fwd(x).float().clone()
+    torch.cuda.synchronize()
+    del fwd
+    return out
+
+
+def test_bisenet_1024x512_fp32_eval_fast_path_matches_oracle(eval_state):
+    """The inference fast path (GraphedForward replay of the no-grad eval forward) in fp32 mode
+    at 2 x 3 x 512 x 1024 vs the oracle's eval forward (build_bisenet.py:141-172, eval branch)
+    on the same weights and running statistics: logits within 1e-3 x max|logit|, argmax
+    identical wherever the oracle's top-2 margin exceeds 1e-3 x max|logit|."""
+    ref, sd = eval_state
+    x = synthetic_images(2, 512, 1024, seed=42)
+    with torch.no_grad():
+        want = ref(x).double()
+    got = _graphed_eval(_eval_net(sd), x.to(DEV), torch.float32).double().cpu()
+    err = ((got - want).abs().max() / want.abs().max()).item()
+    top2 = want.topk(2, dim=1).values
+    safe = (top2[:, 0] - top2[:, 1]) > 1e-3 * want.abs().max()
+    mism = ((got.argmax(1) != want.argmax(1)) & safe).sum().item()
+    print(f"fp32 eval fast path vs oracle: max rel err {err:.2e}, argmax mismatches {mism} "
+          f"at safe pixels ({float(safe.float().mean()):.4f} safe)")
+    assert err < 1e-3, err
+    assert mism == 0 and safe.float().mean() > 0.95, (mism, float(safe.float().mean()))
+
+
+def _block_rounding(net):
+    """fp32-mode forward hooks rounding every ConvBlock / BasicBlock output to bf16 (where bf16
+    mode stores its block outputs)."""
+    cp = net.context_path
+    mods = [getattr(net.saptial_path, f"convblock{i}") for i in (1, 2, 3)]
+    mods += [blk for li in (1, 2, 3, 4) for blk in getattr(cp, f"layer{li}")]
+    return [m.register_forward_hook(lambda mod, args, o: o.to(torch.bfloat16).float()) for m in mods]
+
+
+def test_bisenet_bench_inference_bf16_vs_fp32(eval_state):
+    """The bench's inference workload (inference_fps_bs8: 8 x 3 x 512 x 1024, bf16, graphed eval
+    forward) vs the same graphed forward in fp32 mode, which the previous test pins to the
+    oracle.
+
+    Every block is bf16-accurate on its own (tools/diag/infer_bf16.py, teacher-forced: 0.26-0.42 %
+    relative Frobenius per ConvBlock / BasicBlock, i.e. one or two bf16 roundings), but this
+    random-weight network amplifies perturbations ~14x end to end (an fp32 run on the
+    bf16-rounded input alone moves the logits 2.7 %), so the bound is calibrated by a CONTROL
+    that applies bf16's perturbations in fp32 arithmetic: conv weights rounded to bf16 (bf16
+    mode reads the rounded weight shadow), the input rounded, every block output rounded.
+    Required: logits' relative Frobenius error <= max(2 %, 1.5x the control's) and argmax
+    agreement >= 1 - 1.5x the control's disagreement; logits finite."""
+    _, sd = eval_state
+    net = _eval_net(sd)
+    x, _ = _batch(8, 512, 1024, 42)
+    r32 = _graphed_eval(net, x, torch.float32)
+    r16 = _graphed_eval(net, x, torch.bfloat16)
+    del net
+    ctl = _eval_net({k: (v.to(torch.bfloat16).float() if v.dim() == 4 else v) for k, v in sd.items()})
+    hooks = _block_rounding(ctl)
+    with rtsds_amd.precision(torch.float32), torch.no_grad():
+        rctl = ctl(x.to(torch.bfloat16).float()).float()
+    for h in hooks:
+        h.remove()
+
+    def cmp(a, b):
+        return (((a - b).norm() / b.norm()).item(), (a.argmax(1) == b.argmax(1)).float().mean().item())
+    fro_c, agree_c = cmp(rctl, r32)
+    fro, agree = cmp(r16, r32)
+    print(f"bench inference bf16 vs fp32: logits fro {fro:.4f} (control {fro_c:.4f}); argmax {agree:.4f} "
+          f"(control {agree_c:.4f})")
+    assert torch.isfinite(r16).all()
+    assert fro <= max(2e-2, 1.5 * fro_c), (fro, fro_c)
+    assert agree >= 1 - 1.5 * (1 - agree_c), (agree, agree_c)
 
 
 # ----------------------------------------------------------------------------- DeepLabV2

@@ -160,6 +160,117 @@ def _da_worker(rank, world, port, out):
         dist.destroy_process_group()
 
 
+def _wire_worker(rank, world, port, out):
+    """The same sharded DA iteration twice, with the gradient all-reduce on an fp32 wire and on
+    an fp16 wire (BASELINE configs[4]: "fp16+fp32 grad all-reduce").  Saves, per rank, the local
+    gradients handed to the all-reduce (recorded by wrapping optim.allreduce_start /
+    allreduce_flat), the reduced gradients (the arenas keep them after step()) and the updated
+    parameters."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    import torch.distributed as dist
+    import rtsds_amd
+    from rtsds_amd import losses, optim
+    from rtsds_amd.train import da_step
+    dist.init_process_group("gloo")
+    rec = []
+
+    def spy(orig):
+        def f(bufs):
+            rec.extend((b.data_ptr(), b.detach().clone()) for b in bufs)
+            return orig(bufs)
+        return f
+    optim.allreduce_start = spy(optim.allreduce_start)
+    optim.allreduce_flat = spy(optim.allreduce_flat)
+
+    def flat(opt, local):
+        parts = []
+        for a in opt.arenas():
+            if not local:
+                parts.append(a.gflat.cpu())
+                continue
+            loc, base = torch.zeros_like(a.gflat), a.gflat.data_ptr()
+            for ptr, v in rec:
+                off = (ptr - base) // 4
+                if 0 <= off < a.total:
+                    loc[off:off + v.numel()] = v
+            parts.append(loc.cpu())
+        return torch.cat(parts)
+    try:
+        x, y, xt = _da_data()
+        lo, hi = SHARDS[rank]
+        res = {}
+        for wire in ("fp32", "fp16"):
+            optim.set_allreduce_dtype(torch.float32 if wire == "fp32" else torch.float16)
+            rec.clear()
+            with rtsds_amd.precision(torch.float32):
+                g, d = _models()
+                og = optim.Adam(g.parameters(), lr=1e-4)
+                od = optim.Adam(d.parameters(), lr=1e-4, weight_decay=1e-4)
+                da_step(g, d, og, od, losses.CrossEntropyLoss(ignore_index=19), losses.BCEWithLogitsLoss(),
+                        x[lo:hi].to(DEV), y[lo:hi].to(DEV), xt[lo:hi].to(DEV), 0.1, 2)
+                torch.cuda.synchronize()
+            res[wire] = {"local_g": flat(og, True), "local_d": flat(od, True),
+                         "grad_g": flat(og, False), "grad_d": flat(od, False),
+                         "g": {k: v.detach().cpu() for k, v in g.named_parameters()},
+                         "d": {k: v.detach().cpu() for k, v in d.named_parameters()}}
+            del g, d, og, od
+        optim.set_allreduce_dtype(torch.float32)
+        torch.save(res, out + f".{rank}")
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_da_step_fp16_wire_allreduce(tmp_path):
+    """configs[4]'s fp16 gradient all-reduce on real gradients: the sharded DA iteration (2 ranks,
+    shards of 2 and 3 images) with G's and D's flat gradients summed as float16 vs as float32.
+    (a) The reduced gradients equal a host emulation of the wire from the ranks' local gradients
+    bit for bit: fp32 wire l0 + l1; fp16 wire fp16(fp16(l0) + fp16(l1)) (two addends: one
+    correctly rounded sum in any order), and no element overflows.  (b) The Adam updates: an
+    fp16-rounded gradient keeps its sign unless it underflows, so every update stays within
+    Adam's first-step bound 2.05 lr of the fp32-wire one, and >= 97 % of G's and D's elements
+    move identically to 1e-6."""
+    out = str(tmp_path / "wire.pt")
+    ctx = mp.get_context("spawn")
+    port = _port()
+    procs = [ctx.Process(target=_wire_worker, args=(r, 2, port, out)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=300)
+        assert p.exitcode == 0
+    got = [torch.load(out + f".{r}", weights_only=True) for r in range(2)]
+    for wire in ("fp32", "fp16"):
+        for nm in ("g", "d"):
+            l0, l1 = got[0][wire]["local_" + nm], got[1][wire]["local_" + nm]
+            red = got[0][wire]["grad_" + nm]
+            assert torch.equal(red, got[1][wire]["grad_" + nm]), (wire, nm, "ranks differ")
+            if wire == "fp32":
+                want = l0 + l1
+            else:
+                want = (l0.half().float() + l1.half().float()).half().float()
+            assert torch.isfinite(red).all(), (wire, nm)
+            bad = int((red != want).sum())
+            print(f"{wire} wire, {nm}: max |g| {float(red.abs().max()):.3e}, "
+                  f"{bad} / {red.numel()} elements differ from the host emulation")
+            assert bad == 0, (wire, nm, bad)
+    r32, r16 = got[0]["fp32"], got[0]["fp16"]
+    dg = (r16["grad_g"] - r32["grad_g"]).abs().max().item()
+    print(f"G gradient, fp16 vs fp32 wire: max |diff| {dg:.3e}")
+    lr = 1e-4
+    for name in ("g", "d"):
+        n = same = 0
+        worst = 0.0
+        for k in r32[name]:
+            dlt = (r16[name][k] - r32[name][k]).abs()
+            n += dlt.numel()
+            same += int((dlt <= 1e-6).sum())
+            worst = max(worst, float(dlt.max()))
+        print(f"{name}: fp16-wire update vs fp32-wire: worst {worst:.3e}, identical {same / n:.5f}")
+        assert worst <= 2.05 * lr, (name, worst)
+        assert same >= 0.97 * n, (name, same, n)
+
+
 def _gathered_da_step(g, d, og, od, x, y, xt, lam, it):
     """adversarial_train's iteration (train.py:174-275) under nn.DataParallel on the gathered
     batch: every module runs per replica on its shard (per-replica BatchNorm statistics), the
