@@ -41,6 +41,7 @@ def install_stubs():
     tr.functional = trf
     tvio = types.ModuleType("torchvision.io")
     tvio.read_image = lambda *a, **k: None
+    tvio.ImageReadMode = types.SimpleNamespace(RGB="RGB", UNCHANGED="UNCHANGED", GRAY="GRAY")
     tv.transforms, tv.io = tr, tvio
     fv = types.ModuleType("fvcore")
     fvnn = types.ModuleType("fvcore.nn")
@@ -110,6 +111,8 @@ def main():
     import train as ref_train
 
     if only:
+        if "inputs" in only:
+            make_inputs()
         if "da2" in only:
             make_da2(ref_train, BiSeNet, TinyDomainDiscriminator)
         if "extras" in only:
@@ -307,6 +310,65 @@ def make_da2(ref_train, BiSeNet, TinyDomainDiscriminator):
     meta["g_running_mean_sum"] = {k: float(v.double().sum()) for k, v in g.state_dict().items()
                                   if k.endswith("running_mean")}
     save("da2_c1", arrays, meta)
+
+
+def make_inputs():
+    """The reference's input-pipeline code that needs no torchvision kernel, run on synthetic
+    data: GTA5.__decode_label__ (datasets/gta5.py:111-119, colour map :10-46) on a colour image
+    holding every colour of the map (ignore classes, the car / license-plate and pole /
+    polegroup shared colours), near-miss and random colours; IntRangeTransformer(0, 19)
+    (utils.py:67-75) on int64 and float label values; CityScapes.__merge_ids__
+    (datasets/cityscapes.py:31-50) and GTA5.__make_dataset__ (datasets/gta5.py:85-100) on
+    synthetic file lists (their order as a glob could return it)."""
+    from datasets.cityscapes import CityScapes
+    from datasets.gta5 import GTA5, cityscape_color_map, cityscape_color_map_df
+    from utils import IntRangeTransformer
+    g = torch.Generator().manual_seed(7)
+    pal = [tuple(int(c) for c in v[1]) for v in cityscape_color_map.values()]
+    train = [tuple(int(c) for c in cityscape_color_map_df.loc[cityscape_color_map_df[0] == i].iloc[0, 1])
+             for i in range(19)]
+    for col in train:  # one channel off by one: no match
+        pal.append((min(col[0] + 1, 255), col[1], col[2]))
+        pal.append((col[0], max(col[1] - 1, 0), col[2]))
+    pal += [tuple(int(c) for c in torch.randint(0, 256, (3,), generator=g)) for _ in range(24)]
+    pal = torch.tensor(pal, dtype=torch.long)
+    h, w = 48, 80
+    idx = torch.randint(0, len(pal), (h, w), generator=g)
+    idx.view(-1)[:len(pal)] = torch.arange(len(pal))  # every palette colour at least once
+    label = pal[idx].permute(2, 0, 1).contiguous()  # [3, H, W] long, as read_image(...).long()
+    ids = GTA5.__decode_label__(None, label, cityscape_color_map_df)
+    arrays = {"gta5_rgb": label.permute(1, 2, 0).to(torch.uint8).numpy(),
+              "gta5_ids": ids[0].to(torch.uint8).numpy()}
+    meta = {"gta5_palette": pal.tolist(), "gta5_ids_shape": list(ids.shape)}
+    clamp = IntRangeTransformer(min_val=0, max_val=19)
+    li = torch.randint(-40, 300, (1, 32, 48), generator=g)
+    lf = torch.randn(1, 32, 48, generator=g) * 40 + 9
+    arrays.update({"int_range_in_long": li.numpy().astype(np.int32), "int_range_out_long": clamp(li).numpy().astype(np.int32),
+                   "int_range_in_float": lf.numpy(), "int_range_out_float": clamp(lf).numpy().astype(np.int32)})
+    # Cityscapes id merge: images and gtFine annotations (colour, instance and label-id maps)
+    cities = {"aachen": ["000000_000019", "000001_000019"], "bochum": ["000000_000313"],
+              "zurich": ["000121_000019", "000007_000019"]}
+    imgs, anns = [], []
+    for city, frames in cities.items():
+        for fr in frames:
+            imgs.append(f"Cityscapes/images/train/{city}/{city}_{fr}_leftImg8bit.png")
+            for kind in ("color", "instanceIds", "labelIds"):
+                anns.append(f"Cityscapes/gtFine/train/{city}/{city}_{fr}_gtFine_{kind}.png")
+    perm = torch.randperm(len(imgs), generator=g).tolist()
+    imgs = [imgs[i] for i in perm]
+    perm = torch.randperm(len(anns), generator=g).tolist()
+    anns = [anns[i] for i in perm]
+    cs = types.SimpleNamespace(images_filename=imgs, annotations_filename=anns)
+    df = CityScapes.__merge_ids__(cs)
+    meta["cityscapes"] = {"images": imgs, "annotations": anns,
+                          "merged": [[r["path"], list(r["labels"])] for _, r in df.iterrows()]}
+    gi = [f"GTA5/images/{i:05d}.png" for i in (3, 1, 10, 2, 25)]
+    gl = [f"GTA5/labels/{i:05d}.png" for i in (25, 2, 3, 10, 1)]
+    gt = types.SimpleNamespace(images_filenames=gi, labels_filenames=gl)
+    df = GTA5.__make_dataset__(gt)
+    meta["gta5_dataset"] = {"images": gi, "labels": gl,
+                            "pairs": [[r["image"], list(r["label"])] for _, r in df.iterrows()]}
+    save("inputs", arrays, meta)
 
 
 if __name__ == "__main__":

@@ -1,7 +1,9 @@
 """Device input pipeline (rtsds_amd.transforms, csrc/data.hip) vs the CPU restatement of the
-reference's torchvision transforms (oracle/transforms.py).  Parity unpinned by reference
-fixtures (torchvision is absent and the reference has no tests); the checker is torch's own
-interpolate / conv2d on the CPU.
+reference's torchvision transforms (oracle/transforms.py).  The resize / normalize / blur
+arithmetic is torchvision's: parity unpinned by reference fixtures (torchvision is absent and
+the reference has no tests); the checker is torch's own interpolate / conv2d on the CPU.  The
+GTA5 colour decode and the IntRangeTransformer clamp are the reference's own code and are
+pinned by fixtures captured from it (tests/golden/inputs.npz, tests/test_inputs_golden.py).
 
 Tolerances: images in fp32 -- |err| <= 2e-5 x max|ref| (the same separable weights; fma vs
 separate multiply-add in the taps); bf16 images -- the fp32 result rounded once (2^-8 rel);
@@ -89,6 +91,28 @@ def test_gta5_decode():
     rgb[:5, :5] = torch.tensor([1, 2, 3], dtype=torch.uint8)  # unknown colour -> 0
     want = OT.decode_gta5(rgb.permute(2, 0, 1).long())
     got = T.decode_gta5_labels(rgb.to(DEV)).cpu()
+    assert torch.equal(got, want)
+
+
+def test_gta5_decode_kernel_matches_reference_fixture(golden):
+    """rtsds_gta5_decode vs GTA5.__decode_label__ captured from the reference
+    (tests/golden/inputs.npz: every colour of the map incl. ignore classes and shared colours,
+    near-miss and random colours): identical ids."""
+    arrays, _ = golden("inputs")
+    rgb = torch.from_numpy(arrays["gta5_rgb"])
+    want = torch.from_numpy(arrays["gta5_ids"]).long()
+    got = T.decode_gta5_labels(rgb.to(DEV)).cpu()
+    assert torch.equal(got, want)
+
+
+def test_label_clamp_matches_reference_fixture(golden):
+    """The label pipeline's IntRangeTransformer(0, 19) clamp (inside rtsds_resize_aa, at an
+    identity resize so only the clamp acts) vs the reference's IntRangeTransformer captured on
+    int64 labels in [-40, 300): identical."""
+    arrays, _ = golden("inputs")
+    x = torch.from_numpy(arrays["int_range_in_long"]).long()
+    want = torch.from_numpy(arrays["int_range_out_long"]).long()
+    got = T.LabelPipeline(tuple(x.shape[-2:]), clamp=(0, 19))([x.to(DEV)])[0].cpu()
     assert torch.equal(got, want)
 
 
