@@ -1752,10 +1752,19 @@ int imgconv_tiles(const rtsds_conv_desc* d);
 void imgconv_fwd(const rtsds_conv_desc* d, const void* x4, const void* w, const float* bias, const float* scale, void* y,
                  int act, float* stats, hipStream_t st);
 void pw_dgrad(const rtsds_conv_desc* d, const void* dy, const void* w, void* dx, int accum, hipStream_t st);
+// Register-resident-weight direct conv for 3x3 64 -> 64 stride-1 convs (tapconv.hip).
+bool tapconv_ok(const rtsds_conv_desc* d);
+int tapconv_rows(const rtsds_conv_desc* d, int dgrad);
+void tapconv_fwd(const rtsds_conv_desc* d, const void* x, const void* w, const float* bias, const float* scale, const void* res,
+                 void* y, int act, float* stats, hipStream_t st);
+void tapconv_dgrad(const rtsds_conv_desc* d, const void* dy, const void* wt, void* dx, int accumulate, const void* mask,
+                   int mask_act, float* bnb_part, const void* bnb_x, const float* gamma, const float* beta, const float* mean,
+                   const float* invstd, int bnb_act, hipStream_t st);
 
 // Number of M tiles (= BatchNorm partial-statistics rows) the forward launch of d uses.
 extern "C" int rtsds_conv2d_fwd_stats_tiles(const rtsds_conv_desc* d) {
   if (pooled_1x1(d)) return 1;
+  if (tapconv_ok(d)) return tapconv_rows(d, 0);
   if (hconv_ok(d)) return hconv_tiles(d);
   if (imgconv_ok(d)) return imgconv_tiles(d);
   int bm, bn;
@@ -1878,6 +1887,11 @@ extern "C" int rtsds_conv2d_fwd(const rtsds_conv_desc* d0, const void* x, const 
   }
   const bool x_padded = (act & RTSDS_INPUT_PADDED) != 0;
   if (x_padded && input_pitch(d0) == d0->c) return RTSDS_ERR_UNSUPPORTED;
+  if (tapconv_ok(d0) && !(act & RTSDS_ACCUMULATE)) {
+    if (bn_stats && (act & 0xff)) return RTSDS_ERR_UNSUPPORTED;
+    tapconv_fwd(d0, x, w, bias, nullptr, nullptr, y, act & 0xff, bn_stats, st);
+    return hipGetLastError() == hipSuccess ? RTSDS_OK : RTSDS_ERR_LAUNCH;
+  }
   if (hconv_ok(d0) && !(act & RTSDS_ACCUMULATE)) {
     if (bn_stats && (act & 0xff)) return RTSDS_ERR_UNSUPPORTED;
     hconv_fwd(d0, x, w, bias, nullptr, y, act & 0xff, bn_stats, st);
@@ -1928,6 +1942,10 @@ extern "C" int rtsds_conv2d_fwd_bn(const rtsds_conv_desc* d0, const void* x, con
   const bool x_padded = (act & RTSDS_INPUT_PADDED) != 0;
   if (x_padded && input_pitch(d0) == d0->c) return RTSDS_ERR_UNSUPPORTED;
   hipStream_t st = (hipStream_t)stream;
+  if (tapconv_ok(d0)) {
+    tapconv_fwd(d0, x, w, shift, scale, res, y, act & 0xff, nullptr, st);
+    return hipGetLastError() == hipSuccess ? RTSDS_OK : RTSDS_ERR_LAUNCH;
+  }
   if (hconv_ok(d0) && !res) {
     hconv_fwd(d0, x, w, shift, scale, y, act & 0xff, nullptr, st);
     return hipGetLastError() == hipSuccess ? RTSDS_OK : RTSDS_ERR_LAUNCH;
@@ -2034,7 +2052,7 @@ extern "C" size_t rtsds_conv2d_dgrad_workspace(const rtsds_conv_desc* d) {
   const size_t es = esize(d->dtype);
   size_t b = al256((size_t)kp * d->kh * d->kw * d->c * es);
   if (kp != d->k) b += al256((size_t)d->n * d->ho * d->wo * kp * es);
-  if (dgrad_hconv(d, kp)) return b;  // the halo conv needs no split-K slabs
+  if (dgrad_hconv(d, kp) || tapconv_ok(d)) return b;  // the direct convs need no split-K slabs
   return b + dgrad_split(d, kp).slab_bytes;
 }
 
@@ -2118,7 +2136,7 @@ static int dgrad_pack_plan(const rtsds_conv_desc* d, PackSeg* seg, int& kp) {
     q.wt = (void*)(intptr_t)boff;  // element offset until the caller adds the base
     return q;
   };
-  if (dgrad_hconv(d, kp)) {
+  if (dgrad_hconv(d, kp) || tapconv_ok(d)) {  // flipped taps: the direct convs run over dY
     seg[0] = one(d->kh, d->kw, d->kh - 1, d->kw - 1, -1, 0);
     return 1;
   }
@@ -2208,6 +2226,7 @@ static DgradSplit dgrad_split(const rtsds_conv_desc* d, int kp);
 extern "C" int rtsds_conv2d_dgrad_bnstats_tiles(const rtsds_conv_desc* d) {
   if (check_desc(d) || d->dtype != RTSDS_BF16 || d->sh != 1 || d->sw != 1 || d->c % 8 != 0) return 0;
   if (pooled_1x1(d) || pw_ok(d)) return 0;
+  if (tapconv_ok(d)) return tapconv_rows(d, 1);
   const int kp = pad_c(d->k, d->dtype);
   if (dgrad_hconv(d, kp) || dgrad_split(d, kp).splits > 1) return 0;
   int bm, bn;
@@ -2269,6 +2288,16 @@ static int dgrad_impl(const rtsds_conv_desc* d0, const void* dy, const void* w, 
   }
   const int k_real = d.k;
   d.k = kp;
+  if (tapconv_ok(d0)) {
+    // 3x3 64 -> 64 stride 1: the register-resident-weight direct conv over dY with the flipped,
+    // transposed weights; mask / accumulate / BatchNorm backward statistics in its epilogue
+    if (!packed) repack_launch(d.dtype, w, wt, k_real, kp, d.kh, d.kw, d.c, d.kh, d.kw, d.kh - 1, d.kw - 1, -1, st);
+    tapconv_dgrad(d0, dy, wt, dx, accumulate, mask, mask_act, bnb ? bnb->part : nullptr, bnb ? bnb->x : nullptr,
+                  bnb ? bnb->gamma : nullptr, bnb ? bnb->beta : nullptr, bnb ? bnb->mean : nullptr,
+                  bnb ? bnb->invstd : nullptr, bnb ? bnb->act : 0, st);
+    masked = mask != nullptr;
+    return hipGetLastError() == hipSuccess ? RTSDS_OK : RTSDS_ERR_LAUNCH;
+  }
   if (dgrad_hconv(d0, kp)) {
     // narrow-output 3x3 conv: halo direct conv over dY with the flipped, transposed weights
     if (!packed) repack_launch(d.dtype, w, wt, k_real, kp, d.kh, d.kw, d.c, d.kh, d.kw, d.kh - 1, d.kw - 1, -1, st);

@@ -6,7 +6,7 @@ cd "$(dirname "$0")/../rtsds_amd/csrc"
 name=$1; flags=$2
 out=build/var_$name
 mkdir -p $out
-for f in conv hconv imgconv pw bn ew upce data graph; do
+for f in conv hconv imgconv tapconv pw bn ew upce data graph; do
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-function -Wno-unused-variable $flags -c $f.hip -o $out/$f.o &
 done
 wait
