@@ -421,6 +421,9 @@ int rtsds_graph_split(void* graph, int max_lanes, void** handle, int* n_segments
 /* Number of chains (<= max_lanes) rtsds_graph_split would use for `graph` -- 1 for a linear
  * (single-stream) capture; a negative RTSDS_ERR_* code on failure.  Nothing is instantiated. */
 int rtsds_graph_lanes(void* graph, int max_lanes);
+/* Number of nodes of a captured hipGraph (negative status on error); GraphedStep drops empty
+ * segments (a capture between two back-to-back collectives). */
+int rtsds_graph_nodes(void* graph);
 int rtsds_graph_split_launch(void* handle, void* stream);
 int rtsds_graph_split_destroy(void* handle);
 

@@ -12,7 +12,8 @@ import torch  # noqa: F401  (must precede the dlopen below)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # RTSDS_LIB: alternative in-tree build of the same ABI (kernel-variant A/B measurements)
-LIB_PATH = os.environ.get("RTSDS_LIB") or os.path.join(_HERE, "librtsds_hip.so")
+DEFAULT_LIB_PATH = os.path.join(_HERE, "librtsds_hip.so")
+LIB_PATH = os.environ.get("RTSDS_LIB") or DEFAULT_LIB_PATH
 
 F32, BF16 = 0, 1
 ACT_NONE, ACT_RELU, ACT_LEAKY, ACT_SIGMOID = 0, 1, 2, 3
@@ -77,6 +78,7 @@ SIGNATURES = {
     "rtsds_graph_split": (c_int, [P, c_int, P, P, P]),
     "rtsds_graph_split_launch": (c_int, [P, P]),
     "rtsds_graph_lanes": (c_int, [P, c_int]),
+    "rtsds_graph_nodes": (c_int, [P]),
     "rtsds_graph_split_destroy": (c_int, [P]),
     "rtsds_copy_channels": (c_int, [P, c_int, c_int, P, c_int, c_int, c_long, c_int, c_int, c_int, P]),
     "rtsds_act_fwd": (c_int, [P, P, c_long, c_int, c_int, P]),
@@ -140,7 +142,12 @@ def load(path=LIB_PATH):
             raise RuntimeError(f"rtsds_amd: HIP library not built ({path}); run __graft_entry__.build()")
         lib = ctypes.CDLL(path)
         for name, (res, args) in SIGNATURES.items():
-            fn = getattr(lib, name)
+            try:
+                fn = getattr(lib, name)
+            except AttributeError:
+                if os.path.abspath(path) == DEFAULT_LIB_PATH:
+                    raise
+                continue  # an older variant library (tools/build_rev_variant.sh) for A/B timing
             fn.restype, fn.argtypes = res, args
         _lib = lib
     return _lib

@@ -130,6 +130,14 @@ int analyze(hipGraph_t graph, int max_lanes, Analysis& A) {
 
 }  // namespace
 
+// Node count of a captured graph (0: an empty capture, e.g. between two back-to-back collectives).
+extern "C" int rtsds_graph_nodes(void* graph) {
+  if (!graph) return -RTSDS_ERR_SHAPE;
+  size_t n = 0;
+  if (hipGraphGetNodes((hipGraph_t)graph, nullptr, &n) != hipSuccess) return -RTSDS_ERR_LAUNCH;
+  return (int)n;
+}
+
 extern "C" int rtsds_graph_lanes(void* graph, int max_lanes) {
   if (!graph || max_lanes < 1) return -RTSDS_ERR_SHAPE;
   Analysis A;

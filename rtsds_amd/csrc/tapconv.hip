@@ -386,8 +386,11 @@ __global__ void __launch_bounds__(512, 1) tapconv_kernel(const TapArgs P) {
 
 // ---- host -------------------------------------------------------------------------------
 static bool tap_geom(const rtsds_conv_desc* d) {
+  // widths that leave a nearly empty last column tile (DeepLab's 257 / 321: 64-pixel tiles with
+  // one valid column) stay on the implicit GEMM, which measured faster there
   return d->dtype == RTSDS_BF16 && d->c == kC && d->k == kC && d->kh == 3 && d->kw == 3 && d->sh == 1 && d->sw == 1 &&
-         d->ph == 1 && d->pw == 1 && d->dh == 1 && d->dw == 1 && (long)d->n * d->h * d->w * kC * 2 < (1L << 31);
+         d->ph == 1 && d->pw == 1 && d->dh == 1 && d->dw == 1 && (d->w % kTW == 0 || d->w % kTW > 3 * kTW / 4) &&
+         (long)d->n * d->h * d->w * kC * 2 < (1L << 31);
 }
 bool tapconv_ok(const rtsds_conv_desc* d) {
 #ifdef RTSDS_NO_TAPCONV  // A/B builds (tools/build_variant.sh): the implicit GEMM instead

@@ -56,9 +56,9 @@ class BCEWithLogitsLoss(nn.Module):
             # part, the third must agree (all ranks miss together on the same call)
             cnt = torch.tensor([float(n), 1.0, float(len(self._global))], dtype=torch.float64, device=input.device)
             dist.all_reduce(cnt)  # eager, outside any graph capture: warm-up iterations fill the cache
-            w = dp_world()
+            w = dist.get_world_size()  # the ranks the collective actually ran over
             if int(cnt[1].item()) != w or float(cnt[2].item()) != w * len(self._global):
                 raise RuntimeError("rtsds_amd.BCEWithLogitsLoss: ranks disagree on the global element count "
                                    "cache (local batch sizes must follow the same pattern on every rank)")
-            total = self._global[(n, w)] = float(cnt[0].item())
+            total = self._global[(n, dp_world())] = float(cnt[0].item())
         return loss * (n / total)

@@ -114,7 +114,15 @@ class ResNetMulti(nn.Module):
         _, _, H, W = x.size()
         t = to_input(x)
         t = conv_bn_relu_maxpool(self.conv1, self.bn1, self.maxpool, t)
-        t = self.layer4(grad_cut(self.layer3(self.layer2(self.layer1(t)))))  # runtime.grad_cut
+        # runtime.grad_cut: under data parallelism the backward runs in phases split at layer2's
+        # output, the middle of layer3 (23 blocks) and layer3's output, so G's 175 MB gradient
+        # arena is all-reduced in ~4 buckets while the backward proceeds
+        t = grad_cut(self.layer2(self.layer1(t)))
+        for i, blk in enumerate(self.layer3):
+            t = blk(t)
+            if i == len(self.layer3) // 2:
+                t = grad_cut(t)
+        t = self.layer4(grad_cut(t))
         t = self.layer6(t)
         return [(t, F.upsample_geometry(t, size=(H, W)))]
 

@@ -62,6 +62,18 @@ def allreduce_flat(buffers):
 
 
 _OVERLAP = {"on": True}
+# gradient-arrival generation: every gradient write into an arena records the current value;
+# begin_grad_phase() advances it, so a partial all-reduce can select the parameters that received
+# their gradient in the current backward phase (DA iteration: the adversarial backward through G
+# after the source backward already touched every parameter)
+_GEN = [0]
+
+
+def begin_grad_phase():
+    """Start a new gradient-arrival generation; returns its number (start_grad_allreduce's
+    ``since``)."""
+    _GEN[0] += 1
+    return _GEN[0]
 
 
 def set_overlap_allreduce(on):
@@ -123,6 +135,7 @@ class _Arena:
         self.shadow = torch.empty(total, dtype=torch.bfloat16, device=dev)
         self.steps = [0] * len(params)
         self.touched = [False] * len(params)
+        self.gen = [0] * len(params)  # generation of the last gradient write (_GEN)
         # per parameter: its gradient's all-reduce has been started (optimizer.start_grad_allreduce
         # with partial=True); a later gradient write would be missing from the reduced sum
         self.reduced = None
@@ -148,6 +161,7 @@ class _Arena:
         def mark(_p):
             self._check_open(i)
             self.touched[i] = True
+            self.gen[i] = _GEN[0]
         return mark
 
     def _check_open(self, i):
@@ -177,6 +191,7 @@ class _Arena:
             return None
         self._check_open(i)
         self.touched[i] = True
+        self.gen[i] = _GEN[0]
         return self.params[i].grad
 
     def grad_ptr_ok(self, i):
@@ -311,12 +326,14 @@ class _FlatOptimizer(torch.optim.Optimizer):
         return [(lo, hi) for lo, hi, _ in out]
 
     @torch.no_grad()
-    def start_grad_allreduce(self, partial=False):
+    def start_grad_allreduce(self, partial=False, since=None):
         """Data parallelism: the gradients are final now -- start their all-reduce so it overlaps
         the work enqueued before step(), which then only waits for it.  ``partial``: only the
         parameters that have received their gradients so far (a backward pass split at a cut,
         train.seg_step: the later phase writes only the others), as contiguous arena ranges;
-        the rest follow at step() (or a later call).  No-op at world 1."""
+        the rest follow at step() (or a later call).  ``since`` (with ``partial``): only the
+        parameters whose last gradient write belongs to generation >= since (begin_grad_phase):
+        a phased backward after an earlier one that touched every parameter.  No-op at world 1."""
         if not _OVERLAP["on"] or dp_world() <= 1 or not (dist.is_available() and dist.is_initialized()):
             return
         arenas = self._ensure()
@@ -327,7 +344,8 @@ class _FlatOptimizer(torch.optim.Optimizer):
                 a.reduced = red
         bufs = []
         for a, red in zip(arenas, self._reduced):
-            idx = [i for i in range(len(a.params)) if not red[i] and (a.touched[i] or not partial)]
+            idx = [i for i in range(len(a.params)) if not red[i] and
+                   (not partial or (a.touched[i] and (since is None or a.gen[i] >= since)))]
             for i in idx:
                 red[i] = True
             bufs += [a.gflat[lo:hi] for lo, hi in self._ranges(a, idx)]

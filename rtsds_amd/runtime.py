@@ -266,6 +266,16 @@ class BranchOut(torch.autograd.Function):
 SUBMIT = {"mode": "auto", "max_lanes": 4, "trial_calls": 3}
 
 
+def graph_nodes(graph):
+    """Nodes of a captured graph (0 = empty capture)."""
+    import ctypes
+    from ._lib import load
+    n = load().rtsds_graph_nodes(ctypes.c_void_p(graph.raw_cuda_graph()))
+    if n < 0:
+        raise RuntimeError(f"rtsds_amd: rtsds_graph_nodes failed (status {-n})")
+    return n
+
+
 def graph_lanes(graph):
     """Stream chains of a captured graph (1 = linear)."""
     import ctypes
@@ -438,7 +448,7 @@ class GraphedStep:
             o.stage_hyper()  # allocates the device hyper buffer outside the capture
         torch.cuda.synchronize()
         self._pool = torch.cuda.graph_pool_handle()  # shared by the variants (never run concurrently)
-        self.variants = []  # [(name, segments [(graph, collective)], runners, outputs)]
+        self.variants = []  # [(name, segments [(graph or None, [collectives])], runners, outputs)]
         first = "serial" if mode == "serial" else ("split" if mode == "split" else "branches")
         self._add_variant(first, fn, serial=first == "serial", split=first == "split")
         if mode == "auto" and max(r.lanes for r, _ in self.variants[0][2]) > 1:
@@ -447,7 +457,8 @@ class GraphedStep:
             # ~GPU time of the branch graph at the serial graph's host cost where it has few
             # segments (DeepLab DA: 54.8 ms GPU / 0.9 ms host vs 54.3 / 52 host-bound)
             name, segs, _, outs = self.variants[0]
-            self.variants.append(("split", segs, [(GraphRunner(g, split=True), coll) for g, coll in segs], outs))
+            self.variants.append(("split", segs, [(GraphRunner(g, split=True) if g is not None else None, colls)
+                                                  for g, colls in segs], outs))
         self._use(0)
         self._trial = [[] for _ in self.variants] if len(self.variants) > 1 else None
         self._calls = 0
@@ -457,7 +468,7 @@ class GraphedStep:
 
     def _add_variant(self, name, fn, serial, split):
         cur = torch.cuda.current_stream()
-        self.segments = []  # [(graph, collective run after it or None)]
+        self.segments = []  # [(graph or None, [collectives run after it])]
         cap_stream = torch.cuda.Stream(device=cur.device)
         cap_stream.wait_stream(cur)
         # the capture runs the optimizers' Python bookkeeping (step counters) without executing
@@ -475,13 +486,14 @@ class GraphedStep:
                 finally:
                     _capture["step"] = None
                     self._graph.capture_end()
-                self.segments.append((self._graph, None))
+                if graph_nodes(self._graph) > 0 or not self.segments:
+                    self.segments.append((self._graph, []))
         finally:
             for o, st in zip(self.optimizers, saved):
                 o._capturing = False
                 o.restore_steps(st)
         cur.wait_stream(cap_stream)
-        runners = [(GraphRunner(g, split=split), coll) for g, coll in self.segments]
+        runners = [(GraphRunner(g, split=split) if g is not None else None, colls) for g, colls in self.segments]
         self.variants.append((name, self.segments, runners, outputs))
 
     def _use(self, i):
@@ -490,8 +502,16 @@ class GraphedStep:
         self.graph = self.segments[0][0]
 
     def _break(self, coll):
+        """End the current segment at a collective.  An empty capture (two collectives back to
+        back, or one at the very start) is dropped: its collective joins the previous segment's
+        list, so a replay launches no empty graph."""
         self._graph.capture_end()
-        self.segments.append((self._graph, coll))
+        if graph_nodes(self._graph) > 0:
+            self.segments.append((self._graph, [coll]))
+        elif self.segments:
+            self.segments[-1][1].append(coll)
+        else:
+            self.segments.append((None, [coll]))
         self._graph = torch.cuda.CUDAGraph(keep_graph=True)
         self._graph.capture_begin(pool=self._pool, capture_error_mode=CAPTURE_MODE)
 
@@ -507,9 +527,10 @@ class GraphedStep:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
         t0 = time.perf_counter()
-        for r, coll in self.runners:
-            r.replay()
-            if coll is not None:
+        for r, colls in self.runners:
+            if r is not None:
+                r.replay()
+            for coll in colls:
                 coll()
         dt = time.perf_counter() - t0
         self.host_launch_s += dt

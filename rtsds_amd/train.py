@@ -12,6 +12,7 @@ import torch
 
 from . import functional as F
 from . import losses, utils
+from .optim import begin_grad_phase
 from .runtime import branch_stream, branches_enabled, branches_serial, collect_cuts, dp_world
 from .callbacks import Callback
 from .validation import val_GTA5
@@ -57,15 +58,19 @@ def _fused_heads(model, criterion, inputs):
     return ts, geo
 
 
-def _backward(loss, optimizer, cuts):
-    """loss.backward(); with cuts (runtime.grad_cut under data parallelism): phase 1 down to the
-    cut leaves, the all-reduce of the gradients complete so far started, then phase 2 through
-    the cut tensors -- same gradients (the cut leaves accumulate exactly what the cut tensors
-    would have received)."""
+def _backward(loss, optimizer, cuts, since=None):
+    """loss.backward(); with cuts (runtime.grad_cut under data parallelism, recorded in forward
+    order): phase 1 down to the last cut's leaf, then, cut by cut from the last, the all-reduce
+    of the gradients complete so far is started and the backward continues through that cut
+    tensor down to the previous cut's leaf -- one gradient bucket per phase, each reducing
+    while the next phase computes.  Same gradients (a cut leaf accumulates exactly what its
+    tensor would have received).  ``since``: the gradient-arrival generation of this backward
+    (optim.begin_grad_phase) when an earlier backward already touched the parameters."""
     loss.backward()
-    if cuts:
-        optimizer.start_grad_allreduce(partial=True)
-        torch.autograd.backward([x for x, _ in cuts], [xd.grad for _, xd in cuts])
+    for x, xd in reversed(cuts or []):
+        optimizer.start_grad_allreduce(partial=True, since=since)
+        if xd.grad is not None:
+            torch.autograd.backward([x], [xd.grad])
 
 
 def seg_step(model, criterion, optimizer, inputs, targets):
@@ -209,12 +214,16 @@ def da_step(generator, discriminator, generator_optimizer, discriminator_optimiz
     with torch.no_grad():
         source_features = _full(main.detach(), geo)
 
-    target_feature = _main_output(generator, target_image)
+    split = dp_world() > 1 and hasattr(generator_optimizer, "start_grad_allreduce")
+    with collect_cuts(split) as cuts:
+        target_feature = _main_output(generator, target_image)
     pred_t = discriminator(F.softmax(target_feature, dim=1))
     ones = torch.ones(pred_t.size(), device=pred_t.device)
     loss_adv = lambda_ * discriminator_loss(pred_t, ones) / iterations
-    loss_adv.backward()
-    # G's gradients are final: under data parallelism their all-reduce overlaps the D phase
+    # the adversarial backward in bucketed phases at the generator's cuts (each bucket's
+    # all-reduce overlaps the next phase); the rest of G's gradients are final after it and
+    # their all-reduce overlaps the D phase
+    _backward(loss_adv, generator_optimizer, cuts, since=begin_grad_phase() if split else None)
     _start_allreduce(generator_optimizer)
 
     for p in discriminator.parameters():
@@ -257,7 +266,8 @@ def _da_step_fused(generator, discriminator, generator_optimizer, discriminator_
     else:
         loss_seg.backward()
         ctx = contextlib.nullcontext()
-    with ctx, (branches_serial() if overlap else contextlib.nullcontext()):
+    split = dp_world() > 1 and hasattr(generator_optimizer, "start_grad_allreduce")
+    with ctx, (branches_serial() if overlap else contextlib.nullcontext()), collect_cuts(split) as cuts:
         (t_low, t_geo), = generator.forward_lowres(target_image, main_only=True)
         target_probs = F.upsample_softmax(t_low, t_geo)
         pred_t = discriminator(target_probs)
@@ -278,7 +288,7 @@ def _da_step_fused(generator, discriminator, generator_optimizer, discriminator_
         side2 = branch_stream(main.device, "da_disc")
         side2.wait_stream(amb)
         source_probs.record_stream(side2)
-    loss_adv.backward()
+    _backward(loss_adv, generator_optimizer, cuts, since=begin_grad_phase() if split else None)
     _start_allreduce(generator_optimizer)
 
     for p in discriminator.parameters():

@@ -463,15 +463,18 @@ def one_rank_rccl():
     dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("model", ["bisenet", "deeplab"])
 @pytest.mark.parametrize("da", [False, True])
-def test_graphed_step_with_collectives(da, monkeypatch, one_rank_rccl):
+def test_graphed_step_with_collectives(da, model, monkeypatch, one_rank_rccl):
     """Data-parallel iterations under runtime.GraphedStep: every collective (the losses'
     global valid-pixel counts, the gradient all-reduce -- started early and awaited in step()
     in the DA iteration) is a break between captured graph segments and is re-issued eagerly
     between their replays.  A one-rank RCCL group with the
     data-parallel code paths forced on (dp_world patched to 2; all_reduce over one rank is the
     identity) must leave parameters, optimizer state and BN buffers bit-identical to the same
-    iterations run eagerly."""
+    iterations run eagerly.  DeepLabV2 has three backward cuts (layer2, mid-layer3, layer3:
+    four gradient buckets); in the DA iteration the adversarial backward is bucketed by
+    gradient-arrival generation (optim.begin_grad_phase)."""
     from rtsds_amd import functional as rf
     from rtsds_amd import losses as rl
     from rtsds_amd import runtime
@@ -485,16 +488,16 @@ def test_graphed_step_with_collectives(da, monkeypatch, one_rank_rccl):
         xt = torch.randn(2, 3, 64, 128, generator=g).to(DEV)
         y = torch.randint(0, 20, (2, 64, 128), generator=g).to(DEV)
         ce, bce = losses.CrossEntropyLoss(ignore_index=19), losses.BCEWithLogitsLoss()
-        states, nseg = [], None
+        states, nseg, ncoll = [], None, 0
         with rtsds_amd.precision(torch.bfloat16):
             # serial all-reduce (inside step()), the DA iteration's early overlapped all-reduce
             # (optim.start_grad_allreduce) eager, and the same replayed as graph segments
             for overlap, graphed in ((False, False), (True, False), (True, True)):
                 optim.set_overlap_allreduce(overlap)
                 torch.manual_seed(3)
-                net = BiSeNet(19, "resnet18").to(DEV).train()
+                net = (BiSeNet(19, "resnet18") if model == "bisenet" else get_deeplab_v2(19, pretrain=False)).to(DEV).train()
                 disc = TinyDomainDiscriminator(19).to(DEV).train()
-                opt = optim.Adam(net.parameters(), lr=1e-3)
+                opt = optim.Adam([p for p in net.parameters() if p.requires_grad], lr=1e-3)
                 dopt = optim.Adam(disc.parameters(), lr=1e-3, weight_decay=1e-4)
 
                 def core():
@@ -507,11 +510,15 @@ def test_graphed_step_with_collectives(da, monkeypatch, one_rank_rccl):
                     if graphed and i == 1:
                         run = GraphedStep(core, [opt, dopt] if da else [opt], warmup=0)
                         nseg = len(run.segments)
+                        # no empty segment is replayed: back-to-back collectives share one
+                        assert all(g is not None and runtime.graph_nodes(g) > 0 for g, _ in run.segments), \
+                            [None if g is None else runtime.graph_nodes(g) for g, _ in run.segments]
+                        ncoll = sum(len(c) for _, c in run.segments)
                     run()
                 torch.cuda.synchronize()
                 states.append({k: v.detach().float().cpu().clone() for k, v in
                                list(net.state_dict().items()) + list(disc.state_dict().items())})
-        assert nseg is not None and nseg >= 3, nseg  # count all-reduce(s) + gradient all-reduce
+        assert nseg is not None and nseg >= 3 and ncoll >= nseg - 1, (nseg, ncoll)  # count + gradient all-reduces
         for st in states[1:]:
             for k in states[0]:
                 assert torch.equal(states[0][k], st[k]), k

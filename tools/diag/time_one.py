@@ -20,7 +20,15 @@ P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
 st = torch.cuda.current_stream().cuda_stream
 wsf = workspace(lib.rtsds_conv2d_fwd_workspace(ctypes.byref(d)), x.device)
 wsd = workspace(lib.rtsds_conv2d_dgrad_workspace(ctypes.byref(d)), x.device)
+sp = torch.empty(k * max(1, lib.rtsds_conv2d_fwd_stats_tiles(ctypes.byref(d))) * 4, device=dev)
+sc, sh = torch.ones(k, device=dev), torch.zeros(k, device=dev)
+hp, wp = (d.ho + 2 - 3) // 2 + 1, (d.wo + 2 - 3) // 2 + 1
+yp = torch.empty(n, k, hp, wp, device=dev, dtype=torch.bfloat16).contiguous(memory_format=CL)
 fn = {"fwd": lambda: lib.rtsds_conv2d_fwd(ctypes.byref(d), P(x), P(wt), None, P(y), 0, None, P(wsf), wsf.numel(), st),
+      "fwdstats": lambda: lib.rtsds_conv2d_fwd(ctypes.byref(d), P(x), P(wt), None, P(y), 0, P(sp), P(wsf), wsf.numel(), st),
+      "eval": lambda: lib.rtsds_conv2d_fwd_bn(ctypes.byref(d), P(x), P(wt), P(sc), P(sh), None, P(y), 1, P(wsf), wsf.numel(), st),
+      "pool": lambda: lib.rtsds_conv2d_fwd_bn_maxpool(ctypes.byref(d), P(x), P(wt), P(sc), P(sh), P(yp), 1, hp, wp, 1,
+                                                      P(wsf), wsf.numel(), st),
       "dgrad": lambda: lib.rtsds_conv2d_dgrad(ctypes.byref(d), P(dy), P(wt), P(dx), 0, P(wsd), wsd.numel(), st)}[pas]
 for _ in range(5):
     fn()
