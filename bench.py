@@ -316,7 +316,8 @@ def main():
         del spacer
     conv_ms = sum(r[0].elapsed_time(r[1]) for r in recs) or float("nan")
     conv_flop = sum(r[2] for r in recs)
-    if args.conv_report and rank == 0:
+
+    def conv_report(recs):
         rows = []
         for e0, e1, fl, tag, d in recs:
             ms_ = e0.elapsed_time(e1)
@@ -328,7 +329,9 @@ def main():
         for tag in ("fwd", "dgrad", "wgrad"):
             sel = [r for r in rows if r[1] == tag]
             print(f"total {tag:5s} {sum(r[0] for r in sel):8.3f} ms over {len(sel)} convs", file=sys.stderr)
-        print(f"total conv  {conv_ms:8.3f} ms, {conv_flop / 1e9:.1f} GF", file=sys.stderr)
+        print(f"total conv  {sum(r[0] for r in rows):8.3f} ms, {sum(r[3] for r in rows):.1f} GF", file=sys.stderr)
+    if args.conv_report and rank == 0:
+        conv_report(recs)
     achieved = conv_flop / (conv_ms * 1e-3) / 1e12
 
     # ---- inference FPS (eval forward, no grad)
@@ -370,6 +373,9 @@ def main():
                     net(xb)
                     torch.cuda.synchronize()
                     irecs, F.CONV_PROFILE = F.CONV_PROFILE, None
+                    if args.conv_report and rank == 0:
+                        print("-- eval forward (bs 8):", file=sys.stderr)
+                        conv_report(irecs)
                     del spacer
                     ims = sum(r[0].elapsed_time(r[1]) for r in irecs)
                     ifl = sum(r[2] for r in irecs)

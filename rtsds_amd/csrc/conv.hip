@@ -14,6 +14,7 @@
 // buffer, one barrier per K-step.  bf16 uses v_mfma_f32_16x16x32_bf16, f32 (parity mode)
 // v_mfma_f32_16x16x4_f32 (exact f32 FMA chain).
 #include "common.h"
+#include <type_traits>
 #include <algorithm>
 #include <cstdlib>
 
@@ -898,11 +899,18 @@ __global__ void __launch_bounds__(256, (BM == 160 && GL) ? 2 : 1) conv_gemm_kern
         }
     }
   } else {
+   // The bf16 / fp32 output epilogue, instantiated per activation: the networks' launches
+   // (none, ReLU) get it with the activation fixed at compile time, anything else reads it from
+   // P.act.  A per-value runtime activation cost a chain of uniform compare-and-branches for
+   // every one of a lane's 64 values (~2,000 scalar branches in a 128 x 128 tile's code).
+   auto epilogue = [&](auto act_c) {
+    constexpr int ACT = decltype(act_c)::value;
     T* out = (T*)P.out;
     auto act_f = [&](float v) {
-      if (P.act == RTSDS_ACT_RELU) return fmaxf(v, 0.f);
-      if (P.act == RTSDS_ACT_LEAKY) return v > 0.f ? v : 0.2f * v;
-      if (P.act == RTSDS_ACT_SIGMOID) return 1.f / (1.f + expf(-v));
+      const int a = ACT >= 0 ? ACT : P.act;
+      if (a == RTSDS_ACT_RELU) return fmaxf(v, 0.f);
+      if (a == RTSDS_ACT_LEAKY) return v > 0.f ? v : 0.2f * v;
+      if (a == RTSDS_ACT_SIGMOID) return 1.f / (1.f + expf(-v));
       return v;
     };
     auto out_row = [&](int gm) -> long {  // DGRAD phase rows scatter back to the full grid
@@ -1102,6 +1110,10 @@ __global__ void __launch_bounds__(256, (BM == 160 && GL) ? 2 : 1) conv_gemm_kern
           }
       }
     }
+   };
+    if (P.act == RTSDS_ACT_NONE) epilogue(std::integral_constant<int, RTSDS_ACT_NONE>());
+    else if (P.act == RTSDS_ACT_RELU) epilogue(std::integral_constant<int, RTSDS_ACT_RELU>());
+    else epilogue(std::integral_constant<int, -1>());
   }
   if (MODE == MODE_FWD && P.stats != nullptr) {
     // BatchNorm batch statistics fused into the producing conv: exact two-pass mean / M2 of

@@ -45,6 +45,20 @@ RT_DEV void store8(rsrc_t r, bf16x4 v, int off) {
 #endif
 }
 
+// Activation of the epilogues.  ACT >= 0: the activation fixed at compile time (RTSDS_ACT_NONE /
+// RTSDS_ACT_RELU, the ones the image convs run with), ACT < 0: chosen per launch.  With the
+// runtime choice every value paid the uniform compare-and-branch chain of the switch (~200
+// scalar branches per tile in the pooled stem); the fixed forms are one VALU op or none.
+template <int ACT>
+RT_DEV float img_act(float t, int act) {
+  const int a = ACT >= 0 ? ACT : act;
+  if (a == RTSDS_ACT_RELU) return fmaxf(t, 0.f);
+  if (a == RTSDS_ACT_LEAKY) return t > 0.f ? t : 0.2f * t;
+  if (a == RTSDS_ACT_SIGMOID) return 1.f / (1.f + expf(-t));
+  return t;
+}
+static int img_act_variant(int act) { return act == RTSDS_ACT_NONE ? 0 : act == RTSDS_ACT_RELU ? 1 : -1; }
+
 namespace {
 constexpr int kTH = 4, kTW = 64;   // output tile rows x columns (all 64 channels)
 constexpr int kCo = 64;            // output channels (4 waves x 16)
@@ -62,7 +76,7 @@ struct ImgArgs {
 };
 
 // WP x WC waves: WP pixel halves (8 groups each) x WC channel slices of 64 / WC
-template <int KH, int KW, int WP>
+template <int KH, int KW, int WP, int ACT>
 __global__ void __launch_bounds__(256, (KH == 7 || WP != 1) ? 2 : 3) imgconv_fwd_kernel(const ImgArgs P) {
   constexpr int WC = 4 / WP, GP = 16 / WP, NCB = kCo / WC / 16;  // pixel groups, 16-channel blocks per wave
   constexpr int KWP = (KW + 1) / 2;          // superpixels per row tap
@@ -163,12 +177,7 @@ __global__ void __launch_bounds__(256, (KH == 7 || WP != 1) ? 2 : 3) imgconv_fwd
     const int qq = q < NQ ? q : 0;
     koff[ks] = ((qq / KWP) * NC + (qq % KWP) + fr) * 16;
   }
-  auto act_f = [&](float t) {
-    if (P.act == RTSDS_ACT_RELU) return fmaxf(t, 0.f);
-    if (P.act == RTSDS_ACT_LEAKY) return t > 0.f ? t : 0.2f * t;
-    if (P.act == RTSDS_ACT_SIGMOID) return 1.f / (1.f + expf(-t));
-    return t;
-  };
+  auto act_f = [&](float t) { return img_act<ACT>(t, P.act); };
 
   float rn = 0.f, rmean[NCB][4], rm2[NCB][4];  // running BatchNorm statistics of this wave's channels
 #pragma unroll
@@ -319,7 +328,7 @@ struct ImgPoolArgs {
   int hp, wp, pp;      // pooled output size, pool padding
   int tiles, per;
 };
-template <int KH, int KW, int PH>
+template <int KH, int KW, int PH, int ACT>
 __global__ void __launch_bounds__(256, 2) imgconv_pool_kernel(const ImgPoolArgs P) {
   constexpr int KWP = (KW + 1) / 2, NQ = KH * KWP, KS = (NQ + 3) / 4;
   constexpr int CR = 2 * PH + 1, NG = 4 * CR;  // conv rows, pixel groups per tile
@@ -403,12 +412,7 @@ __global__ void __launch_bounds__(256, 2) imgconv_pool_kernel(const ImgPoolArgs 
     const int qq = q < NQ ? q : 0;
     koff[ks] = ((qq / KWP) * NC + (qq % KWP) + fr) * 16;
   }
-  auto act_f = [&](float t) {
-    if (P.act == RTSDS_ACT_RELU) return fmaxf(t, 0.f);
-    if (P.act == RTSDS_ACT_LEAKY) return t > 0.f ? t : 0.2f * t;
-    if (P.act == RTSDS_ACT_SIGMOID) return 1.f / (1.f + expf(-t));
-    return t;
-  };
+  auto act_f = [&](float t) { return img_act<ACT>(t, P.act); };
   // window maximum with maxpool_fwd_k3's rule (a NaN wins)
   auto mx = [](float best, float f) { return (f > best || (f != f && best == best)) ? f : best; };
 
@@ -438,26 +442,52 @@ __global__ void __launch_bounds__(256, 2) imgconv_pool_kernel(const ImgPoolArgs 
       for (int ks = 0; ks < KS; ++ks) acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[ks], fa[ks], acc[g], 0, 0, 0);
       __builtin_amdgcn_sched_barrier(0);
     }
+    // the conv outputs as stored by the conv kernel (folded BN, activation, bf16 rounding), in
+    // place; a NaN anywhere in the wave's tile sends the wave down the exact NaN-ordered path
+    float probe = 0.f;
+#pragma unroll
+    for (int g = 0; g < NG; ++g)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        acc[g][e] = (float)(bf16)act_f(fmaf(acc[g][e], sv[e], bv[e]));
+        probe = fmaf(acc[g][e], 0.f, probe);  // NaN iff some value is NaN or infinite
+      }
+    const bool exact = __builtin_amdgcn_ballot_w64(probe != probe) != 0;  // wave-uniform
 #pragma unroll
     for (int pr = 0; pr < PH; ++pr) {
-      // vertical maxima of the bf16-rounded conv outputs (invalid conv positions skipped)
+      // vertical maxima (invalid conv positions skipped: -inf)
       float vm[4][4];
 #pragma unroll
       for (int cg = 0; cg < 4; ++cg) {
         const int cc = cc0 + cg * 16 + fr;
+        const bool cok = (unsigned)cc < (unsigned)P.wo;
 #pragma unroll
         for (int e = 0; e < 4; ++e) vm[cg][e] = -INFINITY;
-        bool any = false;
+        if (exact) {
+          bool any = false;
 #pragma unroll
-        for (int tr = 0; tr < 3; ++tr) {
-          const int cr = cr0 + 2 * pr + tr;
-          if ((unsigned)cr < (unsigned)P.ho && (unsigned)cc < (unsigned)P.wo) {
+          for (int tr = 0; tr < 3; ++tr) {
+            const int cr = cr0 + 2 * pr + tr;
+            if ((unsigned)cr < (unsigned)P.ho && cok) {
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              const float v = (float)(bf16)act_f(fmaf(acc[(2 * pr + tr) * 4 + cg][e], sv[e], bv[e]));
-              vm[cg][e] = any ? mx(vm[cg][e], v) : v;
+              for (int e = 0; e < 4; ++e) {
+                const float v = acc[(2 * pr + tr) * 4 + cg][e];
+                vm[cg][e] = any ? mx(vm[cg][e], v) : v;
+              }
+              any = true;
             }
-            any = true;
+          }
+        } else {  // no NaN: compare-and-select from -inf gives the same maximum (and the same zero sign)
+#pragma unroll
+          for (int tr = 0; tr < 3; ++tr) {
+            const int cr = cr0 + 2 * pr + tr;
+            if ((unsigned)cr < (unsigned)P.ho) {
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                const float v = cok ? acc[(2 * pr + tr) * 4 + cg][e] : -INFINITY;
+                vm[cg][e] = v > vm[cg][e] ? v : vm[cg][e];
+              }
+            }
           }
         }
       }
@@ -474,8 +504,13 @@ __global__ void __launch_bounds__(256, 2) imgconv_pool_kernel(const ImgPoolArgs 
           const float a2 = fr + 2 < 16 ? a2s : a2n;  // (the selection is the reader's)
           // window order: left column, then middle, then right (skip -inf = no valid position)
           float best = vm[cg][e];
-          best = a1 == -INFINITY ? best : (best == -INFINITY ? a1 : mx(best, a1));
-          best = a2 == -INFINITY ? best : (best == -INFINITY ? a2 : mx(best, a2));
+          if (exact) {
+            best = a1 == -INFINITY ? best : (best == -INFINITY ? a1 : mx(best, a1));
+            best = a2 == -INFINITY ? best : (best == -INFINITY ? a2 : mx(best, a2));
+          } else {
+            best = a1 > best ? a1 : best;
+            best = a2 > best ? a2 : best;
+          }
           o[e] = best;
         }
         const int pc = pc0 + cg * 8 + (fr >> 1), pry = po + pr;
@@ -502,9 +537,14 @@ bool imgconv_ok(const rtsds_conv_desc* d) {
 // 2 channel halves (71.5 / 57 us train / eval vs 74 / 60.5 in 4 channel quarters); the 3x3
 // spatial-path conv in channel quarters with the statistics epilogue (54 vs 58 us) and pixel
 // halves without it (41.5 vs 45.8 us).
-static const void* img_kernel(int kh, bool stats) {
-  if (kh == 7) return (const void*)imgconv_fwd_kernel<7, 7, 2>;
-  return stats ? (const void*)imgconv_fwd_kernel<3, 3, 1> : (const void*)imgconv_fwd_kernel<3, 3, 2>;
+template <int ACT>
+static const void* img_kernel_act(int kh, bool stats) {
+  if (kh == 7) return (const void*)imgconv_fwd_kernel<7, 7, 2, ACT>;
+  return stats ? (const void*)imgconv_fwd_kernel<3, 3, 1, ACT> : (const void*)imgconv_fwd_kernel<3, 3, 2, ACT>;
+}
+static const void* img_kernel(int kh, bool stats, int act) {
+  const int v = img_act_variant(act);
+  return v == 0 ? img_kernel_act<0>(kh, stats) : v == 1 ? img_kernel_act<1>(kh, stats) : img_kernel_act<-1>(kh, stats);
 }
 static int img_wp(int kh, bool stats) { return kh == 7 ? 2 : (stats ? 1 : 2); }
 static int img_tiles(const rtsds_conv_desc* d) { return d->n * rt_cdiv(d->ho, kTH) * rt_cdiv(d->wo, kTW); }
@@ -514,7 +554,8 @@ static int img_tiles(const rtsds_conv_desc* d) { return d->n * rt_cdiv(d->ho, kT
 static void img_grid(const rtsds_conv_desc* d, bool stats, int& grid, int& per) {
   static int occ[3] = {0, 0, 0}, cus = 0;
   const int v = d->kh == 7 ? 2 : (stats ? 1 : 0);
-  if (!occ[v] && (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ[v], img_kernel(d->kh, stats), 256, 0) != hipSuccess ||
+  // (the activation variants share the launch bounds and register budget: ReLU's stands for all)
+  if (!occ[v] && (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ[v], img_kernel(d->kh, stats, RTSDS_ACT_RELU), 256, 0) != hipSuccess ||
                   occ[v] < 1))
     occ[v] = 1;
   if (!cus && (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0) != hipSuccess || cus < 1)) cus = 256;
@@ -536,9 +577,8 @@ void imgconv_fwd(const rtsds_conv_desc* d, const void* x4, const void* w, const 
   a.tiles = img_tiles(d);
   int grid;
   img_grid(d, stats != nullptr, grid, a.per);
-  if (d->kh == 7) hipLaunchKernelGGL((imgconv_fwd_kernel<7, 7, 2>), dim3(grid), dim3(256), 0, st, a);
-  else if (stats) hipLaunchKernelGGL((imgconv_fwd_kernel<3, 3, 1>), dim3(grid), dim3(256), 0, st, a);
-  else hipLaunchKernelGGL((imgconv_fwd_kernel<3, 3, 2>), dim3(grid), dim3(256), 0, st, a);
+  void* args[] = {&a};
+  (void)hipLaunchKernel(img_kernel(d->kh, stats != nullptr, act), dim3(grid), dim3(256), args, 0, st);
 }
 
 // Pooled stem at inference (imgconv_pool_kernel): conv + folded BN + act + MaxPool2d(3, 2, pp).
@@ -557,13 +597,18 @@ void imgconv_pool_fwd(const rtsds_conv_desc* d, const void* x4, const void* w, c
 #define IMG_POOL_PH 2
 #endif
   a.tiles = d->n * rt_cdiv(hp, IMG_POOL_PH) * rt_cdiv(wp, kPW);
+  const int v = img_act_variant(act);
+  const void* k = v == 0 ? (const void*)imgconv_pool_kernel<7, 7, IMG_POOL_PH, 0>
+                : v == 1 ? (const void*)imgconv_pool_kernel<7, 7, IMG_POOL_PH, 1>
+                         : (const void*)imgconv_pool_kernel<7, 7, IMG_POOL_PH, -1>;
   static int occ = 0, cus = 0;
-  if (!occ && (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)imgconv_pool_kernel<7, 7, IMG_POOL_PH>, 256, 0) != hipSuccess ||
+  if (!occ && (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)imgconv_pool_kernel<7, 7, IMG_POOL_PH, 1>, 256, 0) != hipSuccess ||
                occ < 1))
     occ = 1;
   if (!cus && (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0) != hipSuccess || cus < 1)) cus = 256;
   const int slots = cus * occ;
   a.per = (a.tiles + slots - 1) / slots;
   const int grid = (a.tiles + a.per - 1) / a.per;
-  hipLaunchKernelGGL((imgconv_pool_kernel<7, 7, IMG_POOL_PH>), dim3(grid), dim3(256), 0, st, a);
+  void* args[] = {&a};
+  (void)hipLaunchKernel(k, dim3(grid), dim3(256), args, 0, st);
 }

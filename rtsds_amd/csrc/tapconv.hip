@@ -77,8 +77,18 @@ RT_DEV bf16x4 tap_load8(rsrc_t r, int off) {
 // Wave w: output row (w >> 1) of the 4 x 64 tile (4 groups of 16 pixels) x channels 32 (w & 1)
 // .. + 32; one 8-wave workgroup per CU (two waves per SIMD), so the weights are read from L2
 // once per CU (staged through LDS) and the 6 x 66 halo feeds 256 output pixels.
-template <int DGRAD>
+template <int DGRAD, int EPI>
 __global__ void __launch_bounds__(512, 1) tapconv_kernel(const TapArgs P) {
+  // epilogue flags: compile-time for the modes the networks launch (tap_epi), read from P for
+  // EPI < 0 -- per-element uniform branches on P's fields cost ~10 us per launch otherwise
+  constexpr bool kGen = EPI < 0;
+  const bool f_stats = kGen ? P.stats != nullptr : EPI == 1;
+  const bool f_res = !DGRAD && (kGen ? P.res != nullptr : EPI == 3);
+  const int f_act = DGRAD ? RTSDS_ACT_NONE : (kGen ? P.act : (EPI >= 2 ? RTSDS_ACT_RELU : RTSDS_ACT_NONE));
+  const bool f_accum = DGRAD && (kGen ? P.accum != 0 : EPI == 3);
+  const bool f_aux = DGRAD && (kGen ? P.aux != nullptr : (EPI == 1 || EPI == 2));
+  const int f_mask_act = kGen ? P.mask_act : RTSDS_ACT_RELU;
+  const int f_bnb_act = kGen ? P.bnb_act : RTSDS_ACT_RELU;
   __shared__ __attribute__((aligned(16))) unsigned char lds[2 * kHBytes + kWHalf];
   // running statistics of the wave's channels across its tiles (kept here, not in registers):
   // FWD (mean, M2) per channel, DGRAD bnb (sum g, sum g (x - mean))
@@ -127,7 +137,7 @@ __global__ void __launch_bounds__(512, 1) tapconv_kernel(const TapArgs P) {
     }
   };
   issue(t0, 0);
-  if (P.stats) srun[wave][lane & 31][lane >> 5] = 0.f;
+  if (f_stats) srun[wave][lane & 31][lane >> 5] = 0.f;
 
   // weight fragments (the MFMA's A operand): row = output channel c0 + 16 cb + fr, K slot =
   // channels 32 kk + 8 fc .. + 8 of tap (r, s).  Each 32-channel half of the weights is copied
@@ -174,9 +184,9 @@ __global__ void __launch_bounds__(512, 1) tapconv_kernel(const TapArgs P) {
     }
   };
   auto act_f = [&](float t) {
-    if (P.act == RTSDS_ACT_RELU) return fmaxf(t, 0.f);
-    if (P.act == RTSDS_ACT_LEAKY) return t > 0.f ? t : 0.2f * t;
-    if (P.act == RTSDS_ACT_SIGMOID) return 1.f / (1.f + expf(-t));
+    if (f_act == RTSDS_ACT_RELU) return fmaxf(t, 0.f);
+    if (f_act == RTSDS_ACT_LEAKY) return t > 0.f ? t : 0.2f * t;
+    if (f_act == RTSDS_ACT_SIGMOID) return 1.f / (1.f + expf(-t));
     return t;
   };
   float rn = 0.f;  // FWD statistics: pixels merged so far (uniform over the wave)
@@ -254,10 +264,10 @@ __global__ void __launch_bounds__(512, 1) tapconv_kernel(const TapArgs P) {
 #pragma unroll
       for (int g = 0; g < 4; ++g) off[g] = 16 * g + fr < vcols ? (pix0 + (16 * g + fr) * kC + 16 * cb) * 2 : (int)0x80000000;
       // operand of the epilogue (residual / accumulate target / mask / BatchNorm input)
-      const bool need_r = DGRAD ? (P.accum || P.aux != nullptr) : (P.res != nullptr);
+      const bool need_r = DGRAD ? (f_accum || f_aux) : f_res;
       bf16x4 ro[4];
       if (need_r) {
-        const rsrc_t rsrc = (DGRAD && P.accum) ? ry : rr;
+        const rsrc_t rsrc = f_accum ? ry : rr;
 #pragma unroll
         for (int g = 0; g < 4; ++g) ro[g] = tap_load8(rsrc, off[g]);
       }
@@ -271,21 +281,21 @@ __global__ void __launch_bounds__(512, 1) tapconv_kernel(const TapArgs P) {
         for (int e = 0; e < 4; ++e) {
           if (!DGRAD) {
             float v = fmaf(acc[g][cb][e], sv[e], bv[e]);
-            if (P.res) v = (float)(bf16)v + (float)ro[g][e];
+            if (f_res) v = (float)(bf16)v + (float)ro[g][e];
             ov[g][e] = (bf16)act_f(v);
             acc[g][cb][e] = v;  // (statistics: the pre-rounding value, as the GEMM epilogue)
           } else {
             const bf16 q = (bf16)acc[g][cb][e];
             float v = (float)q;
-            if (P.accum) v += (float)ro[g][e];
-            else if (P.aux && !P.stats) {  // mask: the backward of the input's activation
+            if (f_accum) v += (float)ro[g][e];
+            else if (f_aux && !f_stats) {  // mask: the backward of the input's activation
               const float xv = (float)ro[g][e];
-              v = xv > 0.f ? v : (P.mask_act == RTSDS_ACT_LEAKY ? 0.2f * v : 0.f);
+              v = xv > 0.f ? v : (f_mask_act == RTSDS_ACT_LEAKY ? 0.2f * v : 0.f);
             }
-            ov[g][e] = (P.accum || (P.aux && !P.stats)) ? (bf16)v : q;
+            ov[g][e] = (f_accum || (f_aux && !f_stats)) ? (bf16)v : q;
           }
         }
-      if (!DGRAD && P.stats) {
+      if (!DGRAD && f_stats) {
         // per-channel (count, mean, M2) over this wave's valid pixels of the tile (two-pass),
         // merged (Chan) into the wave's running statistics in LDS
         float mean[4];
@@ -320,7 +330,7 @@ __global__ void __launch_bounds__(512, 1) tapconv_kernel(const TapArgs P) {
           }
         }
       }
-      if (DGRAD && P.stats) {
+      if (DGRAD && f_stats) {
         // BatchNorm backward statistics from the stored dx: g = dx * act'(x * scale + shift)
         float ga[4], be[4], mu[4], is[4], sg[4] = {0.f, 0.f, 0.f, 0.f}, sgx[4] = {0.f, 0.f, 0.f, 0.f};
         ld4(P.bn_gamma, cb, 1.f, ga);
@@ -335,7 +345,7 @@ __global__ void __launch_bounds__(512, 1) tapconv_kernel(const TapArgs P) {
             const float sc = ga[e] * is[e], sh = fmaf(-mu[e], sc, be[e]);
             const float xv = (float)ro[g][e];
             float gv = (float)ov[g][e];
-            gv *= fmaf(xv, sc, sh) > 0.f ? 1.f : (P.bnb_act == RTSDS_ACT_LEAKY ? 0.2f : 0.f);
+            gv *= fmaf(xv, sc, sh) > 0.f ? 1.f : (f_bnb_act == RTSDS_ACT_LEAKY ? 0.2f : 0.f);
             sg[e] += gv;
             sgx[e] = fmaf(gv, xv - mu[e], sgx[e]);
           }
@@ -376,7 +386,7 @@ __global__ void __launch_bounds__(512, 1) tapconv_kernel(const TapArgs P) {
       tap_store16(ry, v, ok ? (((img * P.h + oh0 + row) * P.w + ow0 + col) * kC + 8 * j) * 2 : (int)0x80000000);
     }
   }
-  if (P.stats && lane < 32) {  // partial-statistics row 2 bid + prow of the wave's 32 channels
+  if (f_stats && lane < 32) {  // partial-statistics row 2 bid + prow of the wave's 32 channels
     const int rows = kTH * gridDim.x, row = kTH * bid + prow, ch = c0 + lane;
     const float* st = srun[wave][lane];
     if (!DGRAD) *(f32x4*)(P.stats + ((long)ch * rows + row) * 4) = f32x4{rn, st[0], st[1], 0.f};
@@ -409,13 +419,24 @@ static void tap_geom_args(const rtsds_conv_desc* d, TapArgs& a) {
 template <int DGRAD>
 static void tap_grid(const rtsds_conv_desc* d, int& grid, int& per) {
   static int occ = 0, cus = 0;
-  if (!occ && (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)tapconv_kernel<DGRAD>, 64 * kWaves, 0) != hipSuccess ||
+  if (!occ && (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)tapconv_kernel<DGRAD, -1>, 64 * kWaves, 0) != hipSuccess ||
                occ < 1))
     occ = 1;
   if (!cus && (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0) != hipSuccess || cus < 1)) cus = 256;
   const int tiles = tap_tiles(d), slots = cus * occ;
   per = (tiles + slots - 1) / slots;
   grid = (tiles + per - 1) / per;
+}
+template <int DGRAD>
+static void tap_launch(int epi, int grid, const TapArgs& a, hipStream_t st) {
+  const dim3 g(grid), b(64 * kWaves);
+  switch (epi) {
+    case 0: hipLaunchKernelGGL((tapconv_kernel<DGRAD, 0>), g, b, 0, st, a); break;
+    case 1: hipLaunchKernelGGL((tapconv_kernel<DGRAD, 1>), g, b, 0, st, a); break;
+    case 2: hipLaunchKernelGGL((tapconv_kernel<DGRAD, 2>), g, b, 0, st, a); break;
+    case 3: hipLaunchKernelGGL((tapconv_kernel<DGRAD, 3>), g, b, 0, st, a); break;
+    default: hipLaunchKernelGGL((tapconv_kernel<DGRAD, -1>), g, b, 0, st, a); break;
+  }
 }
 // partial-statistics rows of a launch: one per workgroup and output row of the tile
 int tapconv_rows(const rtsds_conv_desc* d, int dgrad) {
@@ -432,7 +453,11 @@ void tapconv_fwd(const rtsds_conv_desc* d, const void* x, const void* w, const f
   tap_geom_args(d, a);
   int grid;
   tap_grid<0>(d, grid, a.per);
-  hipLaunchKernelGGL(tapconv_kernel<0>, dim3(grid), dim3(64 * kWaves), 0, st, a);
+  // epilogue modes: 1 BatchNorm statistics, 2 ReLU, 3 residual + ReLU, 0 plain, -1 anything else
+  const int epi = stats ? (!res && act == RTSDS_ACT_NONE ? 1 : -1)
+                : act == RTSDS_ACT_RELU ? (res ? 3 : 2)
+                : (act == RTSDS_ACT_NONE && !res ? 0 : -1);
+  tap_launch<0>(epi, grid, a, st);
 }
 // dx (+)= conv(dy, wt_flipped) (wt: [c][3][3][k], rtsds_conv2d_dgrad_pack_many's halo layout);
 // mask: act' of the input's activation; bnb: BatchNorm backward statistics [c][rows][2]
@@ -449,5 +474,10 @@ void tapconv_dgrad(const rtsds_conv_desc* d, const void* dy, const void* wt, voi
   tap_geom_args(d, a);
   int grid;
   tap_grid<1>(d, grid, a.per);
-  hipLaunchKernelGGL(tapconv_kernel<1>, dim3(grid), dim3(64 * kWaves), 0, st, a);
+  // epilogue modes: 1 ReLU BatchNorm-backward statistics, 2 ReLU mask, 3 accumulate, 0 plain
+  int epi = -1;
+  if (bnb_part) epi = (!accumulate && bnb_act == RTSDS_ACT_RELU) ? 1 : -1;
+  else if (mask) epi = (!accumulate && mask_act == RTSDS_ACT_RELU) ? 2 : -1;
+  else epi = accumulate ? 3 : 0;
+  tap_launch<1>(epi, grid, a, st);
 }

@@ -21,6 +21,7 @@ for wl in $wls; do
   timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $r/fetch -o run -- python3 $args >> $o/log 2>&1
   timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $r/write -o run -- python3 $args >> $o/log 2>&1
   timeout -s KILL 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAVES GRBM_GUI_ACTIVE --output-format csv -d $r/mfma -o run -- python3 $args >> $o/log 2>&1
+  python3 tools/diag/copy_sites.py $(ls $r/kt/run_kernel_trace.csv) > $o/copy_sites.txt || true
   python3 tools/kstats.py $(ls $r/kt/run_kernel_stats.csv) $STEPS > $o/kernel_stats.txt
   python3 tools/kstats.py $(ls $r/kt/run_kernel_stats.csv) $STEPS --all > $o/kernel_stats_all.txt
   python3 tools/pmc_traffic.py $r $STEPS $o/traffic.json > $o/traffic.txt
