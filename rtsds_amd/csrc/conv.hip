@@ -1417,6 +1417,9 @@ static void pick_tile(long M, int N, bool b16, int& bm, int& bn, bool fwd = fals
       bm = (fwd || m160) && r160 * 160 < r128 * 128 ? 160 : 128;
     }
     else if (blocks(128, 64) >= 384) { bm = 128; bn = 64; }
+#ifdef PICK_SMALLM_128x64
+    else if (K >= 2048 && blocks(128, 64) >= 192) { bm = 128; bn = 64; }
+#endif
     else { bm = 64; bn = 64; }
   } else {
     if (N <= 32) { bm = 128; bn = 32; } else { bm = 64; bn = 64; }
@@ -1750,7 +1753,7 @@ static void sp_pad4(const rtsds_conv_desc* d, const void* x, void* x4, hipStream
 // Halo-resident direct conv for narrow 3x3 outputs (hconv.hip).
 bool hconv_ok(const rtsds_conv_desc* d);
 int hconv_tiles(const rtsds_conv_desc* d);
-void hconv_fwd(const rtsds_conv_desc* d, const void* x, const void* w, const float* bias, const float* scale, void* y,
+void hconv_fwd(const rtsds_conv_desc* d, const void* x, const void* w, const float* bias, const float* scale, const void* res, void* y,
                int act, float* stats, hipStream_t st);
 bool hconv_dgrad_ok(const rtsds_conv_desc* d);
 void hconv_dgrad(const rtsds_conv_desc* d, const void* dyp, int kp, const void* wt, void* dx, int accumulate, hipStream_t st);
@@ -1906,7 +1909,7 @@ extern "C" int rtsds_conv2d_fwd(const rtsds_conv_desc* d0, const void* x, const 
   }
   if (hconv_ok(d0) && !(act & RTSDS_ACCUMULATE)) {
     if (bn_stats && (act & 0xff)) return RTSDS_ERR_UNSUPPORTED;
-    hconv_fwd(d0, x, w, bias, nullptr, y, act & 0xff, bn_stats, st);
+    hconv_fwd(d0, x, w, bias, nullptr, nullptr, y, act & 0xff, bn_stats, st);
     return hipGetLastError() == hipSuccess ? RTSDS_OK : RTSDS_ERR_LAUNCH;
   }
   if (imgconv_ok(d0) && !(act & RTSDS_ACCUMULATE)) {
@@ -1958,8 +1961,8 @@ extern "C" int rtsds_conv2d_fwd_bn(const rtsds_conv_desc* d0, const void* x, con
     tapconv_fwd(d0, x, w, shift, scale, res, y, act & 0xff, nullptr, st);
     return hipGetLastError() == hipSuccess ? RTSDS_OK : RTSDS_ERR_LAUNCH;
   }
-  if (hconv_ok(d0) && !res) {
-    hconv_fwd(d0, x, w, shift, scale, y, act & 0xff, nullptr, st);
+  if (hconv_ok(d0)) {
+    hconv_fwd(d0, x, w, shift, scale, res, y, act & 0xff, nullptr, st);
     return hipGetLastError() == hipSuccess ? RTSDS_OK : RTSDS_ERR_LAUNCH;
   }
   if (imgconv_ok(d0) && !res) {

@@ -20,12 +20,17 @@
 #include "common.h"
 
 namespace {
-constexpr int kTR = 4, kTC = 64, kCK = 32;
-constexpr int kHR = kTR + 2, kHC = kTC + 2, kHaloPix = kHR * kHC;  // 6 x 66 = 396
-constexpr int kHaloInstr = 28;  // ceil(396 * 4 / 64) = 25 wave-instructions, padded to 7 per wave
+// A tile is 256 output pixels: 4 rows x 64 columns, or 8 x 32 for 32-wide maps (ResNet layer4
+// at 1024 x 512: 16 x 32); wave w computes pixels 64 w .. 64 w + 63 of the row-major tile.
+constexpr int kCK = 32;
+template <int TC> struct HTile {
+  static constexpr int TR = 256 / TC, HR = TR + 2, HC = TC + 2, HaloPix = HR * HC;  // 396 / 340
+  // 16-B DMA pieces (4 per halo pixel) in wave-instructions, padded to a multiple of 4 waves
+  static constexpr int HaloInstr = ((HaloPix * 4 + 63) / 64 + 3) / 4 * 4;           // 28 / 24
+  static constexpr int HaloBytes = HaloInstr * 1024;
+};
 constexpr int kWInstr = 20;     // 9 taps x 32 rows x 4 chunks / 64 = 18, padded to 5 per wave
-constexpr int kHaloBytes = kHaloInstr * 1024, kWBytes = kWInstr * 1024;
-constexpr int kBuf = kHaloBytes + kWBytes;  // 48 KB per stage
+constexpr int kWBytes = kWInstr * 1024;
 }  // namespace
 
 struct HconvArgs {
@@ -33,13 +38,19 @@ struct HconvArgs {
   const bf16* wt;      // [k][3][3][c]
   const float* bias;   // [k] or null (eval fold: shift)
   const float* scale;  // [k] or null (eval fold)
+  const bf16* res;     // NHWC [n][h][w][k] residual (added to the bf16-rounded conv output) or null
   bf16* y;             // NHWC [n][h][w][k]
   float* stats;        // [k][tiles][4] or null
   int n, h, w, c, k, act, accum;  // k = output channels, tiled by 32 over blockIdx.y
 };
 
+// ACT >= 0: the activation fixed at compile time (none / ReLU), < 0: P.act (see imgconv.hip)
+template <int ACT, int TC>
 __global__ void __launch_bounds__(256, 1) hconv_fwd_kernel(const HconvArgs P) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];  // 2 x kBuf
+  using G = HTile<TC>;
+  constexpr int kTR = G::TR, kTC = TC, kHC = G::HC, kHaloPix = G::HaloPix, kHaloInstr = G::HaloInstr;
+  constexpr int kHaloBytes = G::HaloBytes, kStage = kHaloBytes + kWBytes;
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];  // 2 stages
   __shared__ float red[4][32];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int tw_n = P.w / kTC, th_n = P.h / kTR;
@@ -85,7 +96,7 @@ __global__ void __launch_bounds__(256, 1) hconv_fwd_kernel(const HconvArgs P) {
     woff[u] = v;
   }
   auto issue = [&](int q, int buf) {
-    unsigned char* hb = lds + buf * kBuf;
+    unsigned char* hb = lds + buf * kStage;
     unsigned char* wb = hb + kHaloBytes;
     const int qoff = q * kCK * 2;
 #pragma unroll
@@ -118,7 +129,7 @@ __global__ void __launch_bounds__(256, 1) hconv_fwd_kernel(const HconvArgs P) {
     }
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    const unsigned char* hb = lds + (q & 1) * kBuf;
+    const unsigned char* hb = lds + (q & 1) * kStage;
     const unsigned char* wb = hb + kHaloBytes;
 #pragma unroll
     for (int tap = 0; tap < 9; ++tap) {
@@ -126,7 +137,8 @@ __global__ void __launch_bounds__(256, 1) hconv_fwd_kernel(const HconvArgs P) {
       bf16x8 fa[4], fb[2];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const int hp = (wave + r) * kHC + 16 * i + fr + s;
+        const int p0 = 64 * wave + 16 * i;  // first pixel of group i (16 | TC: one tile row)
+        const int hp = (p0 / kTC + r) * kHC + p0 % kTC + fr + s;
         fa[i] = *(const bf16x8*)(hb + hp * 64 + ((fc ^ ((hp >> 2) & 3)) << 4));
       }
 #pragma unroll
@@ -192,9 +204,10 @@ __global__ void __launch_bounds__(256, 1) hconv_fwd_kernel(const HconvArgs P) {
     }
   }
   auto act_f = [&](float t) {
-    if (P.act == RTSDS_ACT_RELU) return fmaxf(t, 0.f);
-    if (P.act == RTSDS_ACT_LEAKY) return t > 0.f ? t : 0.2f * t;
-    if (P.act == RTSDS_ACT_SIGMOID) return 1.f / (1.f + expf(-t));
+    const int a = ACT >= 0 ? ACT : P.act;
+    if (a == RTSDS_ACT_RELU) return fmaxf(t, 0.f);
+    if (a == RTSDS_ACT_LEAKY) return t > 0.f ? t : 0.2f * t;
+    if (a == RTSDS_ACT_SIGMOID) return 1.f / (1.f + expf(-t));
     return t;
   };
   if (P.k % 8 == 0) {
@@ -207,18 +220,18 @@ __global__ void __launch_bounds__(256, 1) hconv_fwd_kernel(const HconvArgs P) {
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          const int px = wave * kTC + 16 * i + er + e;
-          cs[px * 32 + 16 * j + fr] = (bf16)(P.accum ? v[i][j][e] : act_f(v[i][j][e]));
+          const int px = 64 * wave + 16 * i + er + e;
+          cs[px * 32 + 16 * j + fr] = (bf16)((P.accum || P.res) ? v[i][j][e] : act_f(v[i][j][e]));
         }
     __syncthreads();
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int cidx = tid + 256 * u, px = cidx >> 2, n = n0 + (cidx & 3) * 8;
       if (n >= P.k) continue;
-      const long o = (((long)img * P.h + oh0 + (px >> 6)) * P.w + ow0 + (px & 63)) * P.k + n;
+      const long o = (((long)img * P.h + oh0 + px / kTC) * P.w + ow0 + px % kTC) * P.k + n;
       bf16x8 t = *(const bf16x8*)(cs + px * 32 + (cidx & 3) * 8);
-      if (P.accum) {
-        const bf16x8 old = *(const bf16x8*)(P.y + o);
+      if (P.accum || P.res) {  // (exclusive: the data gradient accumulates, the forward adds a residual)
+        const bf16x8 old = *(const bf16x8*)(P.accum ? (const bf16*)P.y + o : P.res + o);
 #pragma unroll
         for (int q = 0; q < 8; ++q) t[q] = (bf16)act_f((float)t[q] + (float)old[q]);
       }
@@ -226,7 +239,6 @@ __global__ void __launch_bounds__(256, 1) hconv_fwd_kernel(const HconvArgs P) {
     }
     return;
   }
-  const long row = ((long)img * P.h + oh0 + wave) * P.w + ow0;
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const int n = n0 + 16 * j + fr;
@@ -235,25 +247,37 @@ __global__ void __launch_bounds__(256, 1) hconv_fwd_kernel(const HconvArgs P) {
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
+        const int px = 64 * wave + 16 * i + er + e;
+        const long o = ((long)img * P.h + oh0 + px / kTC) * P.w + ow0 + px % kTC;
         float t = v[i][j][e];
-        if (P.accum) t += (float)P.y[(row + 16 * i + er + e) * P.k + n];
-        P.y[(row + 16 * i + er + e) * P.k + n] = (bf16)act_f(t);
+        if (P.accum) t += (float)P.y[o * P.k + n];
+        if (P.res) t = (float)(bf16)t + (float)P.res[o * P.k + n];
+        P.y[o * P.k + n] = (bf16)act_f(t);
       }
   }
 }
 
 // ---- host -------------------------------------------------------------------------------
+// tile width: 64 columns, or 32 for 32-wide maps
+static int hconv_tc(const rtsds_conv_desc* d) {
+  if (d->w % 64 == 0 && d->h % 4 == 0) return 64;
+  if (d->w % 32 == 0 && d->h % 8 == 0) return 32;
+  return 0;
+}
 static bool hconv_geom(const rtsds_conv_desc* d) {
   return d->dtype == RTSDS_BF16 && d->kh == 3 && d->kw == 3 && d->sh == 1 && d->sw == 1 && d->ph == 1 && d->pw == 1 &&
-         d->dh == 1 && d->dw == 1 && d->h % kTR == 0 && d->w % kTC == 0;
+         d->dh == 1 && d->dw == 1 && hconv_tc(d) > 0;
 }
-// forward: narrow outputs (Cout <= 32), or Cout a multiple of 32 up to 256 when the reduction
+#ifndef HCONV_KMAX
+#define HCONV_KMAX 512
+#endif
+// forward: narrow outputs (Cout <= 32), or Cout a multiple of 32 up to 512 when the reduction
 // is deep enough (Cin >= 256: >= 8 double-buffered channel chunks) -- N-tiled over blockIdx.y,
 // each N tile re-staging the halo.  Measured (bs 8, 1024x512): ResNet layer3 3x3 256 -> 256
 // at 32 x 64: 34 / 40 us fwd / dgrad vs 38 / 44 us on the implicit GEMM; layer1 / layer2
 // (64 / 128 channels, 2-4 chunks) lose to the GEMM (59 vs 41 us, 42 vs 32 us fwd).
 static bool hconv_kc_ok(int k, int c) {
-  return k <= 32 || (k % 32 == 0 && k <= 256 && c >= 256);
+  return k <= 32 || (k % 32 == 0 && k <= HCONV_KMAX && c >= 256);
 }
 bool hconv_ok(const rtsds_conv_desc* d) {
   if (!hconv_geom(d) || d->c % kCK != 0 || !hconv_kc_ok(d->k, d->c)) return false;
@@ -265,25 +289,41 @@ bool hconv_dgrad_ok(const rtsds_conv_desc* d) {
   if (!hconv_geom(d) || !hconv_kc_ok(d->k, d->k)) return false;  // reduction over Cout here
   return (long)d->n * d->h * d->w * d->c * 2 < (1L << 31);
 }
-int hconv_tiles(const rtsds_conv_desc* d) { return d->n * (d->h / kTR) * (d->w / kTC); }
-static void hconv_launch(const HconvArgs& a, int tiles, int ntiles, hipStream_t st) {
-  static const bool lds_ok = hipFuncSetAttribute((const void*)hconv_fwd_kernel,
-                                                 hipFuncAttributeMaxDynamicSharedMemorySize, 2 * kBuf) == hipSuccess;
-  (void)lds_ok;
-  const int lds = a.c / kCK > 1 ? 2 * kBuf : kBuf;  // one channel chunk: a single stage
-  hipLaunchKernelGGL(hconv_fwd_kernel, dim3(tiles, ntiles), dim3(256), lds, st, a);
+int hconv_tiles(const rtsds_conv_desc* d) {
+  const int tc = hconv_tc(d);
+  return d->n * (d->h / (256 / tc)) * (d->w / tc);
 }
-void hconv_fwd(const rtsds_conv_desc* d, const void* x, const void* w, const float* bias, const float* scale, void* y,
-               int act, float* stats, hipStream_t st) {
+template <int TC>
+static void hconv_launch_tc(const HconvArgs& a, int tiles, int ntiles, hipStream_t st) {
+  constexpr int stage = HTile<TC>::HaloBytes + kWBytes;
+  static const bool lds_ok =
+      hipFuncSetAttribute((const void*)hconv_fwd_kernel<0, TC>, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * stage) == hipSuccess &&
+      hipFuncSetAttribute((const void*)hconv_fwd_kernel<1, TC>, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * stage) == hipSuccess &&
+      hipFuncSetAttribute((const void*)hconv_fwd_kernel<-1, TC>, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * stage) == hipSuccess;
+  (void)lds_ok;
+  const int lds = a.c / kCK > 1 ? 2 * stage : stage;  // one channel chunk: a single stage
+  const dim3 g(tiles, ntiles), b(256);
+  if (a.act == RTSDS_ACT_NONE) hipLaunchKernelGGL((hconv_fwd_kernel<0, TC>), g, b, lds, st, a);
+  else if (a.act == RTSDS_ACT_RELU) hipLaunchKernelGGL((hconv_fwd_kernel<1, TC>), g, b, lds, st, a);
+  else hipLaunchKernelGGL((hconv_fwd_kernel<-1, TC>), g, b, lds, st, a);
+}
+static void hconv_launch(const HconvArgs& a, int tc, int tiles, int ntiles, hipStream_t st) {
+  if (tc == 64) hconv_launch_tc<64>(a, tiles, ntiles, st);
+  else hconv_launch_tc<32>(a, tiles, ntiles, st);
+}
+void hconv_fwd(const rtsds_conv_desc* d, const void* x, const void* w, const float* bias, const float* scale, const void* res,
+               void* y, int act, float* stats, hipStream_t st) {
   HconvArgs a;
-  a.x = (const bf16*)x; a.wt = (const bf16*)w; a.bias = bias; a.scale = scale; a.y = (bf16*)y; a.stats = stats;
+  a.x = (const bf16*)x; a.wt = (const bf16*)w; a.bias = bias; a.scale = scale; a.res = (const bf16*)res; a.y = (bf16*)y;
+  a.stats = stats;
   a.n = d->n; a.h = d->h; a.w = d->w; a.c = d->c; a.k = d->k; a.act = act; a.accum = 0;
-  hconv_launch(a, hconv_tiles(d), (d->k + 31) / 32, st);
+  hconv_launch(a, hconv_tc(d), hconv_tiles(d), (d->k + 31) / 32, st);
 }
 // dx (+)= conv(dy_p, wt_flipped): dy_p [n][h][w][kp] (kp % 32 == 0), wt [c][3][3][kp]
 void hconv_dgrad(const rtsds_conv_desc* d, const void* dyp, int kp, const void* wt, void* dx, int accumulate, hipStream_t st) {
   HconvArgs a;
-  a.x = (const bf16*)dyp; a.wt = (const bf16*)wt; a.bias = nullptr; a.scale = nullptr; a.y = (bf16*)dx; a.stats = nullptr;
+  a.x = (const bf16*)dyp; a.wt = (const bf16*)wt; a.bias = nullptr; a.scale = nullptr; a.res = nullptr; a.y = (bf16*)dx;
+  a.stats = nullptr;
   a.n = d->n; a.h = d->h; a.w = d->w; a.c = kp; a.k = d->c; a.act = 0; a.accum = accumulate ? 1 : 0;
-  hconv_launch(a, hconv_tiles(d), (d->c + 31) / 32, st);
+  hconv_launch(a, hconv_tc(d), hconv_tiles(d), (d->c + 31) / 32, st);
 }

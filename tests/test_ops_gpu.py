@@ -709,6 +709,8 @@ FOLD_CASES = [
     (8, 256, 1, 1, 256, 1, 1, 0, True, 3, False),    # ARM 1x1(bias) + bn + sigmoid
     (2, 1024, 8, 16, 19, 3, 1, 1, False, 1, False),  # FFM ConvBlock (N=19: scalar epilogue)
     (8, 128, 64, 64, 128, 3, 1, 1, False, 1, True),  # 128x128 LDS-DMA tile + residual
+    (2, 256, 8, 64, 256, 3, 1, 1, False, 1, True),   # halo conv (bf16), 4 x 64 tiles + residual
+    (2, 512, 8, 32, 512, 3, 1, 1, False, 1, True),   # halo conv (bf16), 8 x 32 tiles (layer4) + residual
 ]
 
 
