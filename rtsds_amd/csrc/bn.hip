@@ -7,6 +7,7 @@
 // main.py:69-72) do not cancel catastrophically.  Three launches per direction:
 // partial statistics (grid over row chunks) -> per-channel finalize -> vectorised apply.
 #include "common.h"
+#include <type_traits>
 #include <algorithm>
 
 static const int kBnMaxRB = 2048;  // row blocks of the partial-statistics pass
@@ -219,10 +220,14 @@ RT_DEV void load_coef(const float* __restrict__ p, int ch0, int c, float* v) {
 // Pass 3 (forward): y = act(x * scale + shift [+ res]).  Same [row group][channel vector]
 // layout as the statistics pass: each thread owns one channel vector for its whole row
 // sweep, so the coefficients sit in registers and there is no per-element index division.
-template <typename T, int VEC>
+// ACT (here and in the backward passes): the activation fixed at compile time for the ones the
+// networks use (RTSDS_ACT_NONE / RTSDS_ACT_RELU), < 0 = the runtime argument; with a runtime
+// activation every element paid act_f's uniform compare-and-branch chain.
+template <typename T, int VEC, int ACT>
 __global__ void __launch_bounds__(256) bn_apply_kernel(const T* __restrict__ x, const T* __restrict__ res, T* __restrict__ y,
                                                         const float* __restrict__ scale, const float* __restrict__ shift,
-                                                        long rows, int c, int act) {
+                                                        long rows, int c, int act_rt) {
+  const int act = ACT >= 0 ? ACT : act_rt;
   const int cbase = blockIdx.y * 256 * VEC;
   const int cl = min(c - cbase, 256 * VEC);
   const BnLayout<VEC> L(cl);
@@ -353,12 +358,13 @@ RT_DEV void bn_bwd_coef(int ch0, int c, const float* gamma, const float* beta, c
 // HAS_Y: the activation mask comes from y (residual BNs); otherwise from x (no y registers).
 // gout (HAS_Y): g = dy * act'(y) is also stored (the residual branch's gradient, and the apply
 // pass's input instead of dy and y).
-template <typename T, int VEC, bool HAS_Y, class GS>
+template <typename T, int VEC, bool HAS_Y, class GS, int ACT>
 __global__ void __launch_bounds__(256) bn_bwd_stats_kernel(const GS gs, const T* __restrict__ x,
                                                             const T* __restrict__ y, const float* __restrict__ gamma,
                                                             const float* __restrict__ beta, const float* __restrict__ mean,
                                                             const float* __restrict__ sinv, float* __restrict__ part,
-                                                            long rows, int c, int act, T* __restrict__ gout) {
+                                                            long rows, int c, int act_rt, T* __restrict__ gout) {
+  const int act = ACT >= 0 ? ACT : act_rt;
   __shared__ float red[2][256][VEC];
   const int cbase = blockIdx.y * 256 * VEC;
   const int cl = min(c - cbase, 256 * VEC);
@@ -545,10 +551,11 @@ __global__ void __launch_bounds__(256) bn_bwd_finalize_rb_kernel(const float* __
 }
 
 // Backward pass 3: dx = A*g + B*(x - mean) + C;  dres = g.  Layout as bn_apply_kernel.
-template <typename T, int VEC, class GS>
+template <typename T, int VEC, class GS, int ACT>
 __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const GS gs, const T* __restrict__ x,
                                                             const T* __restrict__ y, T* __restrict__ dx, T* __restrict__ dres,
-                                                            const float* __restrict__ coef, long rows, int c, int act) {
+                                                            const float* __restrict__ coef, long rows, int c, int act_rt) {
+  const int act = ACT >= 0 ? ACT : act_rt;
   const int cbase = blockIdx.y * 256 * VEC;
   const int cl = min(c - cbase, 256 * VEC);
   const BnLayout<VEC> L(cl);
@@ -603,6 +610,13 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const GS gs, const T*
 }
 
 // ------------------------------------------------------------------ host
+// f(std::integral_constant<int, A>) with A the compile-time activation variant of the kernels above
+template <typename F>
+static void with_act(int act, F f) {
+  if (act == RTSDS_ACT_NONE) f(std::integral_constant<int, RTSDS_ACT_NONE>());
+  else if (act == RTSDS_ACT_RELU) f(std::integral_constant<int, RTSDS_ACT_RELU>());
+  else f(std::integral_constant<int, -1>());
+}
 static long bn_need(long rows, int c, int vec) {
   int tpr = (c + vec - 1) / vec;
   if (tpr > 256) tpr = 256;
@@ -663,8 +677,10 @@ static void bn_fwd_launch(const void* x, const void* res, void* y, long rows, in
   } else {
     hipLaunchKernelGGL(bn_eval_coef_kernel, dim3(rt_cdiv(c, 256)), dim3(256), 0, st, c, gamma, beta, rm, rv, scale, shift, sm, si, eps);
   }
-  hipLaunchKernelGGL((bn_apply_kernel<T, VEC>), dim3(bn_apply_rb(rows, c, VEC), rt_cdiv(c, 256 * VEC)), dim3(256), 0, st,
-                     (const T*)x, (const T*)res, (T*)y, scale, shift, rows, c, act);
+  with_act(act, [&](auto a) {
+    hipLaunchKernelGGL((bn_apply_kernel<T, VEC, decltype(a)::value>), dim3(bn_apply_rb(rows, c, VEC), rt_cdiv(c, 256 * VEC)),
+                       dim3(256), 0, st, (const T*)x, (const T*)res, (T*)y, scale, shift, rows, c, act);
+  });
 }
 
 extern "C" int rtsds_bn_fwd(const void* x, const void* res, void* y, long rows, int c, const float* gamma, const float* beta,
@@ -720,11 +736,16 @@ static void bn_bwd_launch(const GS& gs, const void* x, const void* y, void* dx, 
     part = pre;
     rb = pre_nrb;
   } else if (y && act)
-    hipLaunchKernelGGL((bn_bwd_stats_kernel<T, VEC, true, GS>), dim3(rb, rt_cdiv(c, 256 * VEC)), dim3(256), 0, st, gs, (const T*)x,
-                       (const T*)y, gamma, beta, smean, sinv, w.part, rows, c, act, g_out ? (T*)dres : (T*)nullptr);
+    with_act(act, [&](auto a) {
+      hipLaunchKernelGGL((bn_bwd_stats_kernel<T, VEC, true, GS, decltype(a)::value>), dim3(rb, rt_cdiv(c, 256 * VEC)), dim3(256), 0,
+                         st, gs, (const T*)x, (const T*)y, gamma, beta, smean, sinv, w.part, rows, c, act,
+                         g_out ? (T*)dres : (T*)nullptr);
+    });
   else
-    hipLaunchKernelGGL((bn_bwd_stats_kernel<T, VEC, false, GS>), dim3(rb, rt_cdiv(c, 256 * VEC)), dim3(256), 0, st, gs, (const T*)x,
-                       (const T*)y, gamma, beta, smean, sinv, w.part, rows, c, act, (T*)nullptr);
+    with_act(act, [&](auto a) {
+      hipLaunchKernelGGL((bn_bwd_stats_kernel<T, VEC, false, GS, decltype(a)::value>), dim3(rb, rt_cdiv(c, 256 * VEC)), dim3(256),
+                         0, st, gs, (const T*)x, (const T*)y, gamma, beta, smean, sinv, w.part, rows, c, act, (T*)nullptr);
+    });
   if (pre)  // channel-major [c][tile][2] partials of the data-gradient epilogue
     hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(c), dim3(256), 0, st, part, rb, c, rows, gamma, beta, smean, sinv,
                        dgamma, dbeta, w.coef, training, accumulate);
@@ -733,11 +754,13 @@ static void bn_bwd_launch(const GS& gs, const void* x, const void* y, void* dx, 
                        sinv, dgamma, dbeta, w.coef, training, accumulate);
   if (g_out) {
     const GradDirect<T> gg{(const T*)dres, c};
-    hipLaunchKernelGGL((bn_bwd_apply_kernel<T, VEC, GradDirect<T>>), dim3(bn_apply_rb(rows, c, VEC), rt_cdiv(c, 256 * VEC)), dim3(256),
-                       0, st, gg, (const T*)x, (const T*)nullptr, (T*)dx, (T*)nullptr, w.coef, rows, c, 0);
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<T, VEC, GradDirect<T>, RTSDS_ACT_NONE>), dim3(bn_apply_rb(rows, c, VEC), rt_cdiv(c, 256 * VEC)),
+                       dim3(256), 0, st, gg, (const T*)x, (const T*)nullptr, (T*)dx, (T*)nullptr, w.coef, rows, c, 0);
   } else if (dx || dres) {
-    hipLaunchKernelGGL((bn_bwd_apply_kernel<T, VEC, GS>), dim3(bn_apply_rb(rows, c, VEC), rt_cdiv(c, 256 * VEC)), dim3(256), 0, st,
-                       gs, (const T*)x, (const T*)y, (T*)dx, (T*)dres, w.coef, rows, c, act);
+    with_act(act, [&](auto a) {
+      hipLaunchKernelGGL((bn_bwd_apply_kernel<T, VEC, GS, decltype(a)::value>), dim3(bn_apply_rb(rows, c, VEC), rt_cdiv(c, 256 * VEC)),
+                         dim3(256), 0, st, gs, (const T*)x, (const T*)y, (T*)dx, (T*)dres, w.coef, rows, c, act);
+    });
   }
 }
 template <typename T, int VEC>
