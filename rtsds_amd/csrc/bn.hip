@@ -632,9 +632,12 @@ static int bn_rb(long rows, int c, int vec) {
   return (int)rb;
 }
 // Row blocks of the elementwise passes: ~2 rows per thread.
+#ifndef BN_APPLY_MAXRB
+#define BN_APPLY_MAXRB (1L << 24)
+#endif
 static int bn_apply_rb(long rows, int c, int vec) {
   const long need = bn_need(rows, c, vec);
-  return (int)std::max<long>(1, std::min<long>((need + 1) / 2, 1L << 24));
+  return (int)std::max<long>(1, std::min<long>((need + 1) / 2, BN_APPLY_MAXRB));
 }
 
 static size_t bn_part_floats(long rows, int c) { return (size_t)bn_rb(rows, c, 1) * c * 4; }

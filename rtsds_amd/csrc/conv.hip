@@ -230,8 +230,17 @@ __global__ void __launch_bounds__(256, (BM == 160 && GL) ? 2 : 1) conv_gemm_kern
     const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
     const int t = RC ? wg % gxy : wg;
     kz = RC ? wg / gxy : (P.nph > 1 ? 0 : (int)blockIdx.z);
-    mt = t % gx;
-    nt = t / gx;
+    // FWD / DGRAD: the N tiles of one M tile run back to back on one XCD, so each XCD's L2 keeps
+    // its run of A rows across all N tiles (the weights are small and stay resident as well).
+    // M-fastest order streamed A through L2 once per N tile: DeepLab's 1x1 convs with N = 1024
+    // / 2048 re-read their inputs 16-32x (conv reads 53 GB per DeepLab step); 142 -> 147 img/s.
+    if (!RC) {
+      nt = t % (int)gridDim.y;
+      mt = t / (int)gridDim.y;
+    } else {
+      mt = t % gx;
+      nt = t / gx;
+    }
   }
   const int m0 = mt * BM, n0 = nt * BN;
   if (MODE == MODE_DGRAD && P.nph > 1 && mt * BM >= P.M) return;  // phase with fewer M tiles
