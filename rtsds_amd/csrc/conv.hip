@@ -1631,15 +1631,29 @@ __global__ void __launch_bounds__(256) pooled_dgrad_vec_kernel(const bf16* __res
   float v[64];
 #pragma unroll
   for (int i = 0; i < 64; ++i) v[i] = 0.f;
-  for (int k = lane; k < k_n; k += 64) {
-    const bf16x8 wv = *(const bf16x8*)(w + (long)k * c + ci0);
-    float g[8];
+  // KI k-rows per lane with every load issued before the FMAs (clamped, unconditional): one
+  // memory round trip per 64 KI rows -- the 512-row loop serialised eight of them (18.6 us)
+  constexpr int KI = 4;
+  for (int k0 = lane; k0 < k_n; k0 += 64 * KI) {
+    bf16x8 wv[KI];
+    float g[KI][8];
 #pragma unroll
-    for (int m = 0; m < 8; ++m) g[m] = m < m_n ? (float)dy[(long)m * k_n + k] : 0.f;
+    for (int u = 0; u < KI; ++u) {
+      const int k = min(k0 + 64 * u, k_n - 1);
+      wv[u] = *(const bf16x8*)(w + (long)k * c + ci0);
 #pragma unroll
-    for (int m = 0; m < 8; ++m)
+      for (int m = 0; m < 8; ++m) g[u][m] = (float)dy[(long)min(m, m_n - 1) * k_n + k];
+    }
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[m * 8 + j] = fmaf(g[m], (float)wv[j], v[m * 8 + j]);
+    for (int u = 0; u < KI; ++u) {
+      if (k0 + 64 * u >= k_n) break;
+#pragma unroll
+      for (int m = 0; m < 8; ++m) {
+        const float gm = m < m_n ? g[u][m] : 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[m * 8 + j] = fmaf(gm, (float)wv[u][j], v[m * 8 + j]);
+      }
+    }
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {  // keep the half of v[0, 2o) this lane's bit o selects
@@ -2444,7 +2458,10 @@ static WgradPlan wgrad_plan(const rtsds_conv_desc* d) {
   // 125).  Wide grids that fill only 432 of a round's 512 slots (DeepLab layer4 3x3, 144
   // tiles x 3) take ~2 full rounds of splits instead when every split keeps >= 64 K-tiles
   // (373 -> 325 us); short reductions (BiSeNet layer4, 64 K-tiles) would pay it in slab traffic.
-  long want = std::max<long>(1, (w.bm == 64 && M <= 32 ? 1536 : 512) / tiles);
+#ifndef WGRAD_WANT
+#define WGRAD_WANT 512
+#endif
+  long want = std::max<long>(1, (w.bm == 64 && M <= 32 ? 1536 : WGRAD_WANT) / tiles);
   if (!(w.bm == 64 && M <= 32) && tiles >= 64 && tiles * want < 480) {
     const long w2 = 1024 / tiles;
     if (tiles * w2 >= 922 && nk / w2 >= 64) want = w2;

@@ -152,11 +152,12 @@ def test_fwd_split_k_accumulate():
     _close(y, y0.double() + fresh.double(), torch.bfloat16, "y accum", tol=1e-2)
 
 
-@pytest.mark.parametrize("c", [512, 19])
+@pytest.mark.parametrize("c", [512, 256, 19])
 def test_pw_backward_accumulate(c):
-    """Narrow 1x1 backward with the accumulate flag (pw.hip dgrad, GEMM wgrad): dx += dgrad,
-    dw/db += wgrad (the flat-arena gradient sink and ConvSum paths), checked against the
-    non-accumulating call plus the prior contents."""
+    """Narrow 1x1 backward with the accumulate flag (pw.hip dgrad, split-K GEMM wgrad): dx +=
+    dgrad, dw/db += wgrad (the flat-arena gradient sink and ConvSum paths), checked against the
+    non-accumulating call plus the prior contents; the weight gradient against fp64, and for the
+    19-channel input also from the 32-channel padded image (RTSDS_INPUT_PADDED)."""
     import ctypes
     from rtsds_amd._lib import lib
     from rtsds_amd.functional import _conv_desc, _P
@@ -189,6 +190,13 @@ def test_pw_backward_accumulate(c):
     ref_w = torch.einsum("nkhw,nchw->kc", dy.double(), x.double())
     _close(dw_f, ref_w, torch.float32, "dw", tol=1e-4)
     _close(db_f, dy.double().sum((0, 2, 3)), torch.float32, "db", tol=1e-4)
+    if c % 8:
+        xp = torch.nn.functional.pad(x.permute(0, 2, 3, 1), (0, 32 - c)).contiguous()  # NHWC, pitch 32
+        dw_p, db_p = torch.empty_like(dw0), torch.empty_like(db0)
+        assert lib.rtsds_conv2d_wgrad(ctypes.byref(d), _P(xp), _P(dy), _P(dw_p), _P(db_p), 0x400, _P(ws), ws.numel(),
+                                      stream()) == 0
+        torch.cuda.synchronize()
+        assert torch.equal(dw_p, dw_f) and torch.equal(db_p, db_f)
 
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])

@@ -24,8 +24,18 @@ db = torch.empty(c, device=dev)
 ws = workspace(lib.rtsds_bn_workspace(rows, c), x.device)
 P = lambda t: t.data_ptr()  # noqa: E731
 st = torch.cuda.current_stream().cuda_stream
+if os.environ.get("BN_FWD"):  # forward: statistics + finalize + apply (training, ReLU)
+    rm, rv, y = torch.zeros(c, device=dev), torch.ones(c, device=dev), torch.empty_like(x)
+    fwd = lambda: lib.rtsds_bn_fwd(P(x), None, P(y), rows, c, P(g), P(b), P(rm), P(rv), None, P(sm), P(si),  # noqa: E731
+                                   0.1, 1e-5, 1, 1, None, 0, 1, P(ws), ws.numel(), st)
 fn = lambda: lib.rtsds_bn_bwd(P(dy), P(x), None, P(dx), None, P(dg), P(db), rows, c, P(g), P(b), P(sm), P(si),  # noqa: E731
                               1, 1, 0, 1, P(ws), ws.numel(), st)
+if os.environ.get("BN_Y"):  # residual BatchNorm + ReLU: mask from y, dres = dy * relu'(y) as well
+    yy, dres = torch.randn(rows, c, device=dev).to(torch.bfloat16), torch.empty_like(x)
+    fn = lambda: lib.rtsds_bn_bwd(P(dy), P(x), P(yy), P(dx), P(dres), P(dg), P(db), rows, c, P(g), P(b), P(sm),  # noqa: E731
+                                  P(si), 1, 1, 0, 1, P(ws), ws.numel(), st)
+if os.environ.get("BN_FWD"):
+    fn = fwd  # noqa: F811
 for _ in range(3):
     fn()
 torch.cuda.synchronize()

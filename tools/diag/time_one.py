@@ -20,6 +20,8 @@ P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
 st = torch.cuda.current_stream().cuda_stream
 wsf = workspace(lib.rtsds_conv2d_fwd_workspace(ctypes.byref(d)), x.device)
 wsd = workspace(lib.rtsds_conv2d_dgrad_workspace(ctypes.byref(d)), x.device)
+wsw = workspace(lib.rtsds_conv2d_wgrad_workspace(ctypes.byref(d)), x.device)
+dw, db = torch.empty(k, c * kh * kh, device=dev), torch.empty(k, device=dev)
 sp = torch.empty(k * max(1, lib.rtsds_conv2d_fwd_stats_tiles(ctypes.byref(d))) * 4, device=dev)
 sc, sh = torch.ones(k, device=dev), torch.zeros(k, device=dev)
 hp, wp = (d.ho + 2 - 3) // 2 + 1, (d.wo + 2 - 3) // 2 + 1
@@ -35,7 +37,8 @@ fn = {"fwd": lambda: lib.rtsds_conv2d_fwd(ctypes.byref(d), P(x), P(wt), None, P(
       "eval": lambda: lib.rtsds_conv2d_fwd_bn(ctypes.byref(d), P(x), P(wt), P(sc), P(sh), None, P(y), 1 | pad, P(wsf), wsf.numel(), st),
       "pool": lambda: lib.rtsds_conv2d_fwd_bn_maxpool(ctypes.byref(d), P(x), P(wt), P(sc), P(sh), P(yp), 1 | pad, hp, wp, 1,
                                                       P(wsf), wsf.numel(), st),
-      "dgrad": lambda: lib.rtsds_conv2d_dgrad(ctypes.byref(d), P(dy), P(wt), P(dx), 0, P(wsd), wsd.numel(), st)}[pas]
+      "dgrad": lambda: lib.rtsds_conv2d_dgrad(ctypes.byref(d), P(dy), P(wt), P(dx), 0, P(wsd), wsd.numel(), st),
+      "wgrad": lambda: lib.rtsds_conv2d_wgrad(ctypes.byref(d), P(x), P(dy), P(dw), P(db), pad, P(wsw), wsw.numel(), st)}[pas]
 for _ in range(5):
     fn()
 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

@@ -43,6 +43,14 @@ def main():
         steps = float(sys.argv[2])
     fetch, write = load(d + "/fetch", "FETCH_SIZE"), load(d + "/write", "WRITE_SIZE")
     names = sorted(set(fetch) | set(write))
+    if "--variants" in sys.argv:  # per instantiation (full kernel name) instead of per base name
+        sys.argv.remove("--variants")
+        rows = sorted(((2 * 1024 * fetch.get(n, 0.0) / steps, 1024 * write.get(n, 0.0) / steps, n) for n in names),
+                      key=lambda x: -(x[0] + x[1]))
+        print(f"{'kernel (instantiation)':90s} {'read MB/step':>13s} {'write MB/step':>14s}")
+        for r, w, n in rows[:40]:
+            print(f"{n[:90]:90s} {r / 1e6:13.1f} {w / 1e6:14.1f}")
+        return
     per = collections.defaultdict(lambda: [0.0, 0.0])
     for n, s in zip(names, short(names)):
         per[s][0] += 2 * 1024 * fetch.get(n, 0.0) / steps

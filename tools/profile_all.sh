@@ -22,9 +22,11 @@ for wl in $wls; do
   timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $r/write -o run -- python3 $args >> $o/log 2>&1
   timeout -s KILL 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAVES GRBM_GUI_ACTIVE --output-format csv -d $r/mfma -o run -- python3 $args >> $o/log 2>&1
   python3 tools/diag/copy_sites.py $(ls $r/kt/run_kernel_trace.csv) > $o/copy_sites.txt || true
+  python3 tools/diag/copy_sites.py $(ls $r/kt/run_kernel_trace.csv) adam_dev_kernel vectorized_elementwise > $o/torch_elementwise_sites.txt || true
   python3 tools/kstats.py $(ls $r/kt/run_kernel_stats.csv) $STEPS > $o/kernel_stats.txt
   python3 tools/kstats.py $(ls $r/kt/run_kernel_stats.csv) $STEPS --all > $o/kernel_stats_all.txt
   python3 tools/pmc_traffic.py $r $STEPS $o/traffic.json > $o/traffic.txt
+  python3 tools/pmc_traffic.py $r $STEPS --variants > $o/traffic_by_variant.txt || true
   python3 tools/pmc_mfma_summary.py $(ls $r/mfma/run_counter_collection.csv) $STEPS > $o/mfma.txt
   echo "$wl done"
 done
