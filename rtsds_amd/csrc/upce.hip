@@ -74,7 +74,10 @@ RT_DEV float upce_block_sum(float v, float* red) {
 // i.e. once per scale-factor rows instead of once per row, and no workgroup barrier runs
 // inside the row loop.
 template <typename T, int CP>
-__global__ void __launch_bounds__(256, 3) upce_fwd_kernel(UpceArgs a) {
+#ifndef UPCE_OCC
+#define UPCE_OCC 3
+#endif
+__global__ void __launch_bounds__(256, UPCE_OCC) upce_fwd_kernel(UpceArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const UpceGeo& q = a.g;
   const int TH = q.th, TW = q.tw, C = q.c, TW1 = TW + 1, tid = threadIdx.x, nthr = blockDim.x;
