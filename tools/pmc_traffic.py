@@ -61,7 +61,14 @@ def main():
         print(f"{k:40s} {r / 1e6:13.1f} {w / 1e6:14.1f}")
     print(f"{'total':40s} {tot[0] / 1e6:13.1f} {tot[1] / 1e6:14.1f}")
     if len(sys.argv) > 3:
-        conv = per.get("conv_gemm_kernel", [0.0, 0.0])
+        # every conv-family launch (implicit GEMM, direct convs and their helpers), as the
+        # live roofline's event-timed conv calls include them
+        fams = ("conv_gemm_kernel", "hconv_fwd_kernel", "tapconv_kernel", "imgconv_fwd_kernel", "imgconv_pool_kernel",
+                "pw_dgrad_kernel", "pooled_fwd_vec_kernel", "pooled_dgrad_vec_kernel", "pooled_wgrad_kernel",
+                "split_reduce_many_kernel", "split_reduce_kernel", "dgrad_pack_kernel", "repack_wt_kernel",
+                "pad_channels_kernel", "dgrad_split_reduce_kernel", "fwd_split_reduce_kernel", "sp_repack_w_kernel",
+                "sp_unpack_dw_kernel")
+        conv = [sum(per[k][0] for k in fams if k in per), sum(per[k][1] for k in fams if k in per)]
         json.dump({"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of bench.py (tools/pmc_bench.sh); "
                              "fetch x2 gfx950 correction", "steps_profiled": steps,
                    "conv_gemm_kernel_bytes_per_step": conv[0] + conv[1],
