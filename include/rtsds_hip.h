@@ -239,7 +239,9 @@ int rtsds_maxpool_bwd(const void* dy, const uint8_t* idx, void* dx, int n, int h
 size_t rtsds_gap_workspace(int n, long hw, int c);
 int rtsds_gap_fwd(const void* x, void* y, int n, long hw, int c, int dtype, void* ws, size_t ws_bytes,
                   void* stream);
-int rtsds_gap_bwd(const void* dy, void* dx, int n, long hw, int c, int dtype, void* stream);
+/* dx (+)= broadcast(dy) / hw; accumulate: add into dx (the gradient another reader of x already
+ * wrote there -- functional.GradJoin; same roundings as a separate elementwise add).          */
+int rtsds_gap_bwd(const void* dy, void* dx, int n, long hw, int c, int accumulate, int dtype, void* stream);
 
 /* ---------------------------------------------------------------- channel attention
  * mode 0: y = x*a[n][c] (build_bisenet.py:52,149); mode 1: y = x*a + x (build_bisenet.py:79-80).

@@ -87,7 +87,7 @@ SIGNATURES = {
     "rtsds_maxpool_bwd": (c_int, [P, P, P] + [c_int] * 10 + [P]),
     "rtsds_gap_workspace": (c_size_t, [c_int, c_long, c_int]),
     "rtsds_gap_fwd": (c_int, [P, P, c_int, c_long, c_int, c_int, P, c_size_t, P]),
-    "rtsds_gap_bwd": (c_int, [P, P, c_int, c_long, c_int, c_int, P]),
+    "rtsds_gap_bwd": (c_int, [P, P, c_int, c_long, c_int, c_int, c_int, P]),
     "rtsds_chscale_fwd": (c_int, [P, P, P, c_int, c_long, c_int, c_int, c_int, P]),
     "rtsds_chscale_bwd": (c_int, [P, P, P, P, P, c_int, c_long, c_int, c_int, c_int, P, c_size_t, P]),
     "rtsds_bilinear_fwd": (c_int, [P, P] + [c_int] * 6 + [c_float, c_float, c_int, c_int, c_int, P]),

@@ -591,14 +591,17 @@ static void chan_reduce(const T* a, const T* b, T* out, int n, long hw, int c, f
     hipLaunchKernelGGL((chan_part_kernel<T, 1, DOT>), dim3(S, n, rt_cdiv(c, 256)), dim3(256), 0, st, a, b, part, hw, c);
   hipLaunchKernelGGL(chan_final_kernel<T>, dim3(rt_cdiv(c, 256), n), dim3(256), 0, st, (const float*)part, out, S, c, scale);
 }
+// accum: dx += the (rounded) gradient -- the other reader's contribution already in dx
+// (functional.GradJoin), the same two roundings as autograd's separate elementwise add
 template <typename T>
-__global__ void gap_bwd_kernel(const T* __restrict__ dy, T* __restrict__ dx, int n, long hw, int c) {
+__global__ void gap_bwd_kernel(const T* __restrict__ dy, T* __restrict__ dx, int n, long hw, int c, int accum) {
   const long total = (long)n * hw * c;
   const float inv = 1.f / (float)hw;
   GRID_STRIDE(i, total) {
     const int ch = (int)(i % c);
     const long img = i / c / hw;
-    dx[i] = from_f<T>(to_f(dy[img * c + ch]) * inv);
+    const T g = from_f<T>(to_f(dy[img * c + ch]) * inv);
+    dx[i] = accum ? from_f<T>(to_f(dx[i]) + to_f(g)) : g;
   }
 }
 extern "C" int rtsds_gap_fwd(const void* x, void* y, int n, long hw, int c, int dtype, void* ws, size_t ws_bytes, void* stream) {
@@ -607,9 +610,9 @@ extern "C" int rtsds_gap_fwd(const void* x, void* y, int n, long hw, int c, int 
   DISPATCH_T(dtype, (chan_reduce<T, false>((const T*)x, nullptr, (T*)y, n, hw, c, 1.f / (float)hw, (float*)ws, (hipStream_t)stream)));
   RET_LAUNCH();
 }
-extern "C" int rtsds_gap_bwd(const void* dy, void* dx, int n, long hw, int c, int dtype, void* stream) {
+extern "C" int rtsds_gap_bwd(const void* dy, void* dx, int n, long hw, int c, int accumulate, int dtype, void* stream) {
   if (n <= 0 || hw <= 0 || c <= 0) return RTSDS_ERR_SHAPE;
-  DISPATCH_T(dtype, hipLaunchKernelGGL(gap_bwd_kernel<T>, dim3(ew_blocks((long)n * hw * c)), dim3(256), 0, (hipStream_t)stream, (const T*)dy, (T*)dx, n, hw, c));
+  DISPATCH_T(dtype, hipLaunchKernelGGL(gap_bwd_kernel<T>, dim3(ew_blocks((long)n * hw * c)), dim3(256), 0, (hipStream_t)stream, (const T*)dy, (T*)dx, n, hw, c, accumulate ? 1 : 0));
   RET_LAUNCH();
 }
 

@@ -988,10 +988,12 @@ def bn_relu_maxpool(x, gamma, beta, running_mean, running_var, training, momentu
 
 
 class GapFn(torch.autograd.Function):
-    """Mean over H, W keeping dims -> [N, C, 1, 1]."""
+    """Mean over H, W keeping dims -> [N, C, 1, 1].  ``join``: GradJoin shared with the other
+    reader of x (the attention modules' channel scale): the backward adds its broadcast into
+    that reader's gradient buffer instead of autograd summing two full-size gradients."""
 
     @staticmethod
-    def forward(ctx, x):
+    def forward(ctx, x, join=None):
         require_hip(x)
         x = nhwc(x)
         n, c, h, w = x.shape
@@ -999,26 +1001,31 @@ class GapFn(torch.autograd.Function):
         ws = workspace(lib.rtsds_gap_workspace(n, h * w, c), x.device)
         lib.rtsds_gap_fwd(_P(x), _P(y), n, h * w, c, dcode(x), _P(ws), ws.numel(), stream())
         ctx.shape = (n, c, h, w)
+        ctx.join = join
         return y
 
     @staticmethod
     def backward(ctx, dy):
         n, c, h, w = ctx.shape
         dy = dy.contiguous()
-        dx = empty_nhwc(n, c, h, w, dy.dtype, dy.device)
-        lib.rtsds_gap_bwd(_P(dy), _P(dx), n, h * w, c, dcode(dy), stream())
-        return dx
+        join = ctx.join
+        acc = join is not None and join.buf is not None
+        dx = join.buf if acc else empty_nhwc(n, c, h, w, dy.dtype, dy.device)
+        lib.rtsds_gap_bwd(_P(dy), _P(dx), n, h * w, c, 1 if acc else 0, dcode(dy), stream())
+        return (join.put(dx) if join is not None else dx), None
 
 
-def global_avg_pool(x):
-    return GapFn.apply(x)
+def global_avg_pool(x, join=None):
+    """``join``: GradJoin shared with x's other reader (see GapFn)."""
+    return GapFn.apply(x, join)
 
 
 class ChScaleFn(torch.autograd.Function):
-    """x * a[N,C,1,1] (mode 0) or x * a + x (mode 1)."""
+    """x * a[N,C,1,1] (mode 0) or x * a + x (mode 1).  ``join``: GradJoin shared with x's
+    other reader (GapFn)."""
 
     @staticmethod
-    def forward(ctx, x, a, mode):
+    def forward(ctx, x, a, mode, join=None):
         require_hip(x, a)
         x = nhwc(x)
         a = a.contiguous()
@@ -1028,6 +1035,7 @@ class ChScaleFn(torch.autograd.Function):
         y = torch.empty_like(x, memory_format=CL)
         lib.rtsds_chscale_fwd(_P(x), _P(a), _P(y), n, h * w, c, mode, dcode(x), stream())
         ctx.mode = mode
+        ctx.join = join
         ctx.save_for_backward(x, a)
         return y
 
@@ -1041,11 +1049,14 @@ class ChScaleFn(torch.autograd.Function):
         ws = workspace(lib.rtsds_gap_workspace(n, h * w, c) if da is not None else 0, x.device)
         lib.rtsds_chscale_bwd(_P(dy), _P(x), _P(a), _P(dx), _P(da), n, h * w, c, ctx.mode,
                               dcode(x), _P(ws), ws.numel(), stream())
-        return dx, da, None
+        if dx is not None and ctx.join is not None:
+            dx = _join_add(ctx.join, dx)
+        return dx, da, None, None
 
 
-def channel_scale(x, a, residual=False):
-    return ChScaleFn.apply(x, a, 1 if residual else 0)
+def channel_scale(x, a, residual=False, join=None):
+    """``join``: GradJoin shared with x's other reader (see GapFn)."""
+    return ChScaleFn.apply(x, a, 1 if residual else 0, join)
 
 
 # ----------------------------------------------------------------------------- bilinear

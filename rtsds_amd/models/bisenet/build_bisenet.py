@@ -57,18 +57,24 @@ class AttentionRefinementModule(torch.nn.Module):
         self.in_channels = in_channels
         self.avgpool = AdaptiveAvgPool2d(output_size=(1, 1))
 
-    def attention(self, input, pooled=None):
+    def attention(self, input, pooled=None, join=None):
         """sigmoid(BN(conv(GAP(input)))) [N, C, 1, 1]; ``pooled``: GAP(input) when the caller
         already has it (BiSeNet's ARM2 reads the context path's tail, the same kernel on the
-        same tensor)."""
+        same tensor); ``join``: GradJoin of input's two readers (the pool and the scale)."""
         if pooled is None:
-            pooled = self.avgpool(input)
+            pooled = F.global_avg_pool(input, join)
         assert self.in_channels == pooled.size(1), \
             "in_channels and out_channels should all be {}".format(pooled.size(1))
         return conv_bn(self.conv, self.bn, pooled, "sigmoid")
 
-    def forward(self, input, pooled=None):
-        return F.channel_scale(input, self.attention(input, pooled))
+    def forward(self, input, pooled=None, join=None):
+        """``join``: with ``pooled``, the caller's GradJoin of input's readers (the pool that made
+        ``pooled`` and this scale)."""
+        # input's two readers (the pool and the scale) share one gradient buffer: the pool's
+        # backward adds into the scale's (no autograd sum of two full-size gradients)
+        if pooled is None:
+            join = F.GradJoin(2) if torch.is_grad_enabled() and input.requires_grad else None
+        return F.channel_scale(input, self.attention(input, pooled, join if pooled is None else None), join=join)
 
 
 class FeatureFusionModule(torch.nn.Module):
@@ -97,8 +103,9 @@ class FeatureFusionModule(torch.nn.Module):
         assert self.in_channels == x.size(1), \
             "in_channels of ConvBlock should be {}".format(x.size(1))
         feature = self.convblock(x)
-        att = self.conv2(self.conv1(self.avgpool(feature), act="relu"), act="sigmoid")
-        return F.channel_scale(feature, att, residual=True)
+        join = F.GradJoin(2) if torch.is_grad_enabled() and feature.requires_grad else None  # see ARM.forward
+        att = self.conv2(self.conv1(F.global_avg_pool(feature, join), act="relu"), act="sigmoid")
+        return F.channel_scale(feature, att, residual=True, join=join)
 
 
 _HEADS = {"resnet18": (256, 512), "resnet101": (1024, 2048)}
@@ -153,6 +160,9 @@ class BiSeNet(torch.nn.Module):
         heads (build_bisenet.py:151-166).  main_only: skip the supervision heads (1x1 convs
         with no state; for callers that discard them, e.g. the DA target branch)."""
         x = to_input(input)
+        # the 1/32 features have two readers, the context path's GAP (the tail) and ARM2's scale:
+        # one gradient buffer (functional.GradJoin).  Only when ARM2 runs with autograd below.
+        j4 = F.GradJoin(2) if self.training and torch.is_grad_enabled() else None
         if self.branch_parallel and self.training and x.is_cuda and F.CONV_PROFILE is None and branches_enabled():
             # (not while bench.py event-times each conv: concurrent branches would inflate them)
             # spatial path on the branch stream, concurrently with the context path (forward and,
@@ -166,13 +176,13 @@ class BiSeNet(torch.nn.Module):
                 x.record_stream(side)  # read (and saved for backward) on the branch stream
                 with torch.cuda.stream(side):
                     box.append(BranchOut.apply(self.saptial_path(x), main, side))
-            f3, f4, tail = self.context_path(x, mid=fork)
+            f3, f4, tail = self.context_path(x, mid=fork, tail_join=j4)
             sx = box[0]
             main.wait_stream(side)
             sx.record_stream(main)
         else:
             sx = self.saptial_path(x)
-            f3, f4, tail = self.context_path(x)
+            f3, f4, tail = self.context_path(x, tail_join=j4)
         hw = sx.shape[-2:]
         heads = []
         cat = None
@@ -188,7 +198,7 @@ class BiSeNet(torch.nn.Module):
         if cat is None:
             cx1 = self.attention_refinement_module1(f3)
             # ARM2's global average pool is the tail itself (same kernel, same f4)
-            cx2 = F.channel_scale(self.attention_refinement_module2(f4, pooled=tail), tail)
+            cx2 = F.channel_scale(self.attention_refinement_module2(f4, pooled=tail, join=j4), tail)
         if infer:
             if cat is None:  # a geometry outside the fused resize
                 cat = F.concat_resized(sx, (cx1, cx2), hw)

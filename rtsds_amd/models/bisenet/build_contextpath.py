@@ -120,17 +120,18 @@ class _ContextPath(nn.Module):
         self.layer1, self.layer2 = trunk.layer1, trunk.layer2
         self.layer3, self.layer4 = trunk.layer3, trunk.layer4
 
-    def forward(self, x, mid=None):
+    def forward(self, x, mid=None, tail_join=None):
         """x: NHWC compute-dtype batch -> (1/16 features, 1/32 features, GAP(1/32)).  ``mid``:
         called after layer2 (BiSeNet forks its spatial path there, beside the narrow late
-        layers)."""
+        layers).  ``tail_join``: GradJoin of the 1/32 features' readers (the GAP here and the
+        caller's attention scale)."""
         t = conv_bn_relu_maxpool(self.conv1, self.bn1, self.maxpool1, x)
         t = self.layer2(self.layer1(t))
         if mid is not None:
             mid()
         f3 = grad_cut(self.layer3(t))  # data-parallel two-phase backward (runtime.grad_cut)
         f4 = self.layer4(f3)
-        return f3, f4, F.global_avg_pool(f4)
+        return f3, f4, F.global_avg_pool(f4, tail_join)
 
 
 class resnet18(_ContextPath):
