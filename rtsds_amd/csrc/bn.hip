@@ -141,6 +141,15 @@ __global__ void __launch_bounds__(256) bn_finalize_kernel(const float* __restric
   __shared__ float wr[4][3];
   const int ch = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   if (nbt && ch == 0 && threadIdx.x == 0) *nbt += 1;  // num_batches_tracked.add_(1)
+  // the per-channel operands of the tail, loaded up front (in flight with the partials: the
+  // tail then pays no extra memory round trip; thread 0 alone reads and writes them)
+  float g0 = 1.f, b0 = 0.f, rm0 = 0.f, rv0 = 0.f;
+  if (threadIdx.x == 0) {
+    if (gamma) g0 = gamma[ch];
+    if (beta) b0 = beta[ch];
+    if (rmean) rm0 = rmean[ch];
+    if (rvar) rv0 = rvar[ch];
+  }
   float n = 0.f, m = 0.f, M = 0.f;
   // up to 8 partials per thread loaded before any merge (one L2 round trip instead of eight);
   // merge order b = tid, tid + 256, ... as before
@@ -167,13 +176,12 @@ __global__ void __launch_bounds__(256) bn_finalize_kernel(const float* __restric
   const float inv = 1.0f / sqrtf(var + eps);
   smean[ch] = m;
   sinv[ch] = inv;
-  if (rmean) rmean[ch] = (1.f - momentum) * rmean[ch] + momentum * m;
+  if (rmean) rmean[ch] = (1.f - momentum) * rm0 + momentum * m;
   if (rvar) {
     const float unb = rows > 1 ? M / (float)(rows - 1) : var;
-    rvar[ch] = (1.f - momentum) * rvar[ch] + momentum * unb;
+    rvar[ch] = (1.f - momentum) * rv0 + momentum * unb;
   }
-  const float g = gamma ? gamma[ch] : 1.f, b = beta ? beta[ch] : 0.f;
-  bn_coef(g, b, m, inv, scale[ch], shift[ch]);
+  bn_coef(g0, b0, m, inv, scale[ch], shift[ch]);
 }
 
 __global__ void bn_eval_coef_kernel(int c, const float* gamma, const float* beta, const float* rmean, const float* rvar,
@@ -470,6 +478,16 @@ __global__ void __launch_bounds__(256) bn_bwd_finalize_kernel(const float* __res
                                        float* coef, int training, int accumulate) {
   __shared__ float wr[4][2];
   const int ch = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  // the tail's per-channel operands up front (see bn_finalize_kernel)
+  float inv = 0.f, g = 1.f, bt = 0.f, mu = 0.f, dg0 = 0.f, db0 = 0.f;
+  if (threadIdx.x == 0) {
+    inv = sinv[ch];
+    mu = smean[ch];
+    if (gamma) g = gamma[ch];
+    if (beta) bt = beta[ch];
+    if (accumulate && dgamma) dg0 = dgamma[ch];
+    if (accumulate && dbeta) db0 = dbeta[ch];
+  }
   float sg = 0.f, sgx = 0.f;
   for (int b0 = threadIdx.x; b0 < nrb; b0 += 256 * 8) {  // 8 partials in flight per thread
     float pg[8], px[8];
@@ -492,16 +510,15 @@ __global__ void __launch_bounds__(256) bn_bwd_finalize_kernel(const float* __res
   if (threadIdx.x != 0) return;
   sg = (wr[0][0] + wr[1][0]) + (wr[2][0] + wr[3][0]);
   sgx = (wr[0][1] + wr[1][1]) + (wr[2][1] + wr[3][1]);
-  const float inv = sinv[ch], g = gamma ? gamma[ch] : 1.f;
-  if (dgamma) dgamma[ch] = accumulate ? dgamma[ch] + sgx * inv : sgx * inv;
-  if (dbeta) dbeta[ch] = accumulate ? dbeta[ch] + sg : sg;
+  if (dgamma) dgamma[ch] = accumulate ? dg0 + sgx * inv : sgx * inv;
+  if (dbeta) dbeta[ch] = accumulate ? db0 + sg : sg;
   const float a = g * inv;
   const float invn = 1.f / (float)rows;
   coef[ch] = a;
   coef[c + ch] = training ? -a * inv * inv * sgx * invn : 0.f;
   coef[2 * c + ch] = training ? -a * sg * invn : 0.f;
-  coef[3 * c + ch] = smean[ch];
-  bn_coef(g, beta ? beta[ch] : 0.f, smean[ch], inv, coef[4 * c + ch], coef[5 * c + ch]);
+  coef[3 * c + ch] = mu;
+  bn_coef(g, bt, mu, inv, coef[4 * c + ch], coef[5 * c + ch]);
 }
 
 // Backward pass 2 for the row-block-major partials of bn_bwd_stats_kernel: 16 channels per
@@ -515,6 +532,16 @@ __global__ void __launch_bounds__(256) bn_bwd_finalize_rb_kernel(const float* __
   __shared__ float wr[16][16][2];
   const int cl = threadIdx.x & 15, q = threadIdx.x >> 4, ch = blockIdx.x * 16 + cl;
   const int chc = min(ch, c - 1);
+  // the tail's per-channel operands up front (see bn_finalize_kernel)
+  float inv = 0.f, g = 1.f, bt = 0.f, mu = 0.f, dg0 = 0.f, db0 = 0.f;
+  if (q == 0) {
+    inv = sinv[chc];
+    mu = smean[chc];
+    if (gamma) g = gamma[chc];
+    if (beta) bt = beta[chc];
+    if (accumulate && dgamma) dg0 = dgamma[chc];
+    if (accumulate && dbeta) db0 = dbeta[chc];
+  }
   float sg = 0.f, sgx = 0.f;
   for (int b0 = q; b0 < nrb; b0 += 16 * 8) {
     float2 pv[8];
@@ -538,16 +565,15 @@ __global__ void __launch_bounds__(256) bn_bwd_finalize_rb_kernel(const float* __
   for (int i = 0; i < 4; ++i) { t0[i] = t0[2 * i] + t0[2 * i + 1]; t1[i] = t1[2 * i] + t1[2 * i + 1]; }
   sg = (t0[0] + t0[1]) + (t0[2] + t0[3]);
   sgx = (t1[0] + t1[1]) + (t1[2] + t1[3]);
-  const float inv = sinv[ch], g = gamma ? gamma[ch] : 1.f;
-  if (dgamma) dgamma[ch] = accumulate ? dgamma[ch] + sgx * inv : sgx * inv;
-  if (dbeta) dbeta[ch] = accumulate ? dbeta[ch] + sg : sg;
+  if (dgamma) dgamma[ch] = accumulate ? dg0 + sgx * inv : sgx * inv;
+  if (dbeta) dbeta[ch] = accumulate ? db0 + sg : sg;
   const float a = g * inv;
   const float invn = 1.f / (float)rows;
   coef[ch] = a;
   coef[c + ch] = training ? -a * inv * inv * sgx * invn : 0.f;
   coef[2 * c + ch] = training ? -a * sg * invn : 0.f;
-  coef[3 * c + ch] = smean[ch];
-  bn_coef(g, beta ? beta[ch] : 0.f, smean[ch], inv, coef[4 * c + ch], coef[5 * c + ch]);
+  coef[3 * c + ch] = mu;
+  bn_coef(g, bt, mu, inv, coef[4 * c + ch], coef[5 * c + ch]);
 }
 
 // Backward pass 3: dx = A*g + B*(x - mean) + C;  dres = g.  Layout as bn_apply_kernel.
