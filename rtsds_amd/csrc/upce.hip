@@ -360,14 +360,33 @@ __global__ void __launch_bounds__(256) upce_final_kernel(const float* __restrict
                                                          int nheads, float* __restrict__ loss, float* __restrict__ loss_sum,
                                                          float* __restrict__ stat) {
   __shared__ float red[4];
-  float c = 0.f;
-  for (int b = threadIdx.x; b < nblocks; b += 256) c += cpart[b];
-  c = upce_block_sum(c, red);
+  // every array's partials of a thread loaded in one batch (8 rows in flight per array), then
+  // summed in the original per-thread order b = tid, tid + 256, ...
+  float acc[1 + kUpceMaxHeads];
+#pragma unroll
+  for (int a = 0; a <= kUpceMaxHeads; ++a) acc[a] = 0.f;
+  for (int b0 = threadIdx.x; b0 < nblocks; b0 += 256 * 8) {
+    float v[1 + kUpceMaxHeads][8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int b = min(b0 + 256 * u, nblocks - 1);
+      v[0][u] = cpart[b];
+#pragma unroll
+      for (int h = 0; h < kUpceMaxHeads; ++h) v[1 + h][u] = h < nheads ? lpart[(long)h * nblocks + b] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (b0 + 256 * u < nblocks) {
+#pragma unroll
+        for (int a = 0; a <= kUpceMaxHeads; ++a) acc[a] += v[a][u];
+      }
+  }
+  const float c = upce_block_sum(acc[0], red);
   if (threadIdx.x == 0) stat[0] = c;
-  for (int h = 0; h < nheads; ++h) {
-    float s = 0.f;
-    for (int b = threadIdx.x; b < nblocks; b += 256) s += lpart[(long)h * nblocks + b];
-    s = upce_block_sum(s, red);
+#pragma unroll
+  for (int h = 0; h < kUpceMaxHeads; ++h) {
+    if (h >= nheads) break;
+    const float s = upce_block_sum(acc[1 + h], red);
     if (threadIdx.x == 0) stat[1 + h] = s;
   }
   if (threadIdx.x == 0) upce_losses(stat, nheads, loss, loss_sum);
