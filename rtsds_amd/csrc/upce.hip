@@ -222,7 +222,20 @@ __global__ void __launch_bounds__(256, UPCE_OCC) upce_fwd_kernel(UpceArgs a) {
         const float* wr = wcol + pj[u] * q.wmax;
         const float* xr = xrow + pc[u] - xb * CP;
         float s = 0.f;
-        for (int x2 = plo[u]; x2 <= phi[u]; ++x2) s = fmaf(wr[x2], xr[x2 * CP], s);
+        // 8 columns' LDS loads in flight per chunk (clamped, in range), then the FMAs in the
+        // original ascending order: the same sum, one LDS latency per chunk instead of per column
+        for (int x0 = plo[u]; x0 <= phi[u]; x0 += 8) {
+          float wv[8], xv8[8];
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            const int x2 = min(x0 + k, phi[u]);
+            wv[k] = wr[x2];
+            xv8[k] = xr[x2 * CP];
+          }
+#pragma unroll
+          for (int k = 0; k < 8; ++k)
+            if (x0 + k <= phi[u]) s = fmaf(wv[k], xv8[k], s);
+        }
         float* o = gdst + il * npair + p;
         *o = add ? *o + s : s;
       }
