@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-enum { RTSDS_F32 = 0, RTSDS_BF16 = 1 };
+enum { RTSDS_F32 = 0, RTSDS_BF16 = 1, RTSDS_F16 = 2 /* the gradient wire only: rtsds_cast, optimizer grad_dtype */ };
 enum {
   RTSDS_OK = 0,
   RTSDS_ERR_SHAPE = 1,        /* inconsistent / out-of-range shape */
@@ -316,26 +316,28 @@ int rtsds_bce_bwd(const float* x, const float* target, const float* grad_loss, f
 
 /* ---------------------------------------------------------------- optimizer
  * torch.optim.Adam step (main.py:116-117) over flat fp32 arenas; grad is multiplied by
- * grad_scale first (data-parallel 1/world).  bf16_shadow (may be NULL) receives bf16(param). */
-int rtsds_adam_step(float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
+ * grad_scale first (data-parallel 1/world).  bf16_shadow (may be NULL) receives bf16(param).
+ * grad_dtype: RTSDS_F32, or RTSDS_F16 / RTSDS_BF16 for the all-reduced reduced-precision wire
+ * copy of the gradients, read directly (no cast back into the fp32 gradient arena).         */
+int rtsds_adam_step(float* param, const void* grad, float* exp_avg, float* exp_avg_sq,
                     void* bf16_shadow, long n, float lr, float beta1, float beta2, float eps,
-                    float weight_decay, int step, float grad_scale, void* stream);
+                    float weight_decay, int step, float grad_scale, int grad_dtype, void* stream);
 
 /* The same update with hyper = {lr, 1 - beta1^step, sqrt(1 - beta2^step)} (fp32, device
  * memory) read by the kernel: a captured hipGraph of the training step replays correct
  * updates while the host advances lr and step between replays.                            */
-int rtsds_adam_step_dev(float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
+int rtsds_adam_step_dev(float* param, const void* grad, float* exp_avg, float* exp_avg_sq,
                         void* bf16_shadow, long n, const float* hyper, float beta1, float beta2,
-                        float eps, float weight_decay, float grad_scale, void* stream);
+                        float eps, float weight_decay, float grad_scale, int grad_dtype, void* stream);
 
 /* torch.optim.SGD step (main.py:118-120) over a flat fp32 arena: d = grad*grad_scale
  * (+ weight_decay*param); with momentum, buf = d on the first step (first != 0), else
  * buf = momentum*buf + (1-dampening)*d; d = nesterov ? d + momentum*buf : buf;
  * param -= lr*d.  hyper (device fp32 {lr, first}, may be NULL) overrides lr / first for
  * hipGraph replays.  bf16_shadow (may be NULL) receives bf16(param).                       */
-int rtsds_sgd_step(float* param, const float* grad, float* momentum_buf, void* bf16_shadow,
+int rtsds_sgd_step(float* param, const void* grad, float* momentum_buf, void* bf16_shadow,
                    long n, const float* hyper, float lr, float momentum, float dampening,
-                   float weight_decay, int nesterov, int first, float grad_scale, void* stream);
+                   float weight_decay, int nesterov, int first, float grad_scale, int grad_dtype, void* stream);
 
 /* ---------------------------------------------------------------- metrics
  * argmax over channels, first maximum wins (train.py:102-106,272-275; validation.py:51).
@@ -426,8 +428,17 @@ int rtsds_graph_lanes(void* graph, int max_lanes);
 /* Number of nodes of a captured hipGraph (negative status on error); GraphedStep drops empty
  * segments (a capture between two back-to-back collectives). */
 int rtsds_graph_nodes(void* graph);
+/* Nodes captured so far by the capture `stream` records into (negative status when it is not
+ * capturing); GraphedStep ends a graph segment at a collective only when it has nodes.        */
+int rtsds_capture_nodes(void* stream);
 int rtsds_graph_split_launch(void* handle, void* stream);
 int rtsds_graph_split_destroy(void* handle);
+
+/* ABI revision of this header (RTSDS_ABI_VERSION): bumped whenever an entry point's signature
+ * changes.  The Python loader refuses a library whose revision differs (A/B variant libraries
+ * built from older sources would otherwise be called with the wrong argument lists). */
+#define RTSDS_ABI_VERSION 6
+int rtsds_abi_version(void);
 
 #ifdef __cplusplus
 }

@@ -13,6 +13,7 @@ import torch  # noqa: F401  (must precede the dlopen below)
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # RTSDS_LIB: alternative in-tree build of the same ABI (kernel-variant A/B measurements)
 DEFAULT_LIB_PATH = os.path.join(_HERE, "librtsds_hip.so")
+ABI_VERSION = 6  # include/rtsds_hip.h RTSDS_ABI_VERSION
 LIB_PATH = os.environ.get("RTSDS_LIB") or DEFAULT_LIB_PATH
 
 F32, BF16 = 0, 1
@@ -79,6 +80,8 @@ SIGNATURES = {
     "rtsds_graph_split_launch": (c_int, [P, P]),
     "rtsds_graph_lanes": (c_int, [P, c_int]),
     "rtsds_graph_nodes": (c_int, [P]),
+    "rtsds_abi_version": (c_int, []),
+    "rtsds_capture_nodes": (c_int, [P]),
     "rtsds_graph_split_destroy": (c_int, [P]),
     "rtsds_copy_channels": (c_int, [P, c_int, c_int, P, c_int, c_int, c_long, c_int, c_int, c_int, P]),
     "rtsds_act_fwd": (c_int, [P, P, c_long, c_int, c_int, P]),
@@ -104,7 +107,7 @@ SIGNATURES = {
                              P]),
     "rtsds_bce_fwd": (c_int, [P, P, P, c_int, P]),
     "rtsds_bce_bwd": (c_int, [P, P, P, P, c_int, P]),
-    "rtsds_adam_step_dev": (c_int, [P, P, P, P, P, c_long, P, c_float, c_float, c_float, c_float, c_float, P]),
+    "rtsds_adam_step_dev": (c_int, [P, P, P, P, P, c_long, P, c_float, c_float, c_float, c_float, c_float, c_int, P]),
     "rtsds_upsoftmax_fwd": (c_int, [P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_float, c_int, c_int, P]),
     "rtsds_upsoftmax_bwd_workspace": (c_size_t, [c_int, c_int, c_int, c_int, c_int, c_int]),
     "rtsds_upsoftmax_bwd": (c_int, [P, c_int, P, c_int, P, c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_float,
@@ -115,9 +118,9 @@ SIGNATURES = {
     "rtsds_gaussian_blur": (c_int, [P, c_int, P, c_int, c_int, c_int, c_int, c_int, c_float, c_float, P]),
     "rtsds_gta5_decode": (c_int, [P, P, c_int, c_int, P]),
     "rtsds_sgd_step": (c_int, [P, P, P, P, c_long, P, c_float, c_float, c_float, c_float, c_int, c_int,
-                               c_float, P]),
+                               c_float, c_int, P]),
     "rtsds_adam_step": (c_int, [P, P, P, P, P, c_long, c_float, c_float, c_float, c_float, c_float,
-                                c_int, c_float, P]),
+                                c_int, c_float, c_int, P]),
     "rtsds_argmax": (c_int, [P, c_long, c_long, c_long, P, P, P, c_int, c_long, c_int, c_int, P]),
     "rtsds_confusion": (c_int, [P, P, P, c_long, c_int, P]),
     "rtsds_adaptive_avgpool_fwd": (c_int, [P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, P]),
@@ -141,13 +144,17 @@ def load(path=LIB_PATH):
         if not os.path.exists(path):
             raise RuntimeError(f"rtsds_amd: HIP library not built ({path}); run __graft_entry__.build()")
         lib = ctypes.CDLL(path)
+        # the library must be built from this ABI revision (include/rtsds_hip.h RTSDS_ABI_VERSION):
+        # an A/B variant built from older sources (tools/build_rev_variant.sh) with a changed
+        # signature would otherwise be called with the wrong arguments
+        ver = getattr(lib, "rtsds_abi_version", None)
+        if ver is None:
+            raise RuntimeError(f"rtsds_amd: {path} predates the ABI version check; rebuild it")
+        ver.restype, ver.argtypes = ctypes.c_int, []
+        if ver() != ABI_VERSION:
+            raise RuntimeError(f"rtsds_amd: {path} has ABI revision {ver()}, this package needs {ABI_VERSION}")
         for name, (res, args) in SIGNATURES.items():
-            try:
-                fn = getattr(lib, name)
-            except AttributeError:
-                if os.path.abspath(path) == DEFAULT_LIB_PATH:
-                    raise
-                continue  # an older variant library (tools/build_rev_variant.sh) for A/B timing
+            fn = getattr(lib, name)
             fn.restype, fn.argtypes = res, args
         _lib = lib
     return _lib

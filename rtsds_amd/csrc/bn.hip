@@ -386,10 +386,7 @@ __global__ void __launch_bounds__(256) bn_bwd_stats_kernel(const GS gs, const T*
   if (active) {
     bn_bwd_coef<VEC>(ch0, c, gamma, beta, mean, sinv, mu, sc, sh);
     const long step = (long)gridDim.x * L.rpi;
-#ifndef BN_STATS_U
-#define BN_STATS_U 2
-#endif
-    constexpr int U = BN_STATS_U;  // rows in flight per thread (loads issued before any use)
+    constexpr int U = 2;  // rows in flight per thread (loads issued before any use)
     for (long r = (long)blockIdx.x * L.rpi + rg; r < rows; r += U * step) {
       float g[U][VEC], xv[U][VEC], yv[HAS_Y ? U : 1][VEC];
 #pragma unroll
@@ -658,12 +655,10 @@ static int bn_rb(long rows, int c, int vec) {
   return (int)rb;
 }
 // Row blocks of the elementwise passes: ~2 rows per thread.
-#ifndef BN_APPLY_MAXRB
-#define BN_APPLY_MAXRB (1L << 24)
-#endif
+static constexpr auto kBnApplyMaxRB = (1L << 24);
 static int bn_apply_rb(long rows, int c, int vec) {
   const long need = bn_need(rows, c, vec);
-  return (int)std::max<long>(1, std::min<long>((need + 1) / 2, BN_APPLY_MAXRB));
+  return (int)std::max<long>(1, std::min<long>((need + 1) / 2, kBnApplyMaxRB));
 }
 
 static size_t bn_part_floats(long rows, int c) { return (size_t)bn_rb(rows, c, 1) * c * 4; }
@@ -735,20 +730,16 @@ extern "C" int rtsds_bn_fwd(const void* x, const void* res, void* y, long rows, 
   return hipGetLastError() == hipSuccess ? RTSDS_OK : RTSDS_ERR_LAUNCH;
 }
 
-#ifndef BN_BWD_RB_MAX
-#define BN_BWD_RB_MAX 512
-#endif
-#ifndef BN_BWD_RB_DIV
-#define BN_BWD_RB_DIV 8
-#endif
+static constexpr auto kBnBwdRBMax = 512;
+static constexpr auto kBnBwdRBDiv = 8;
 // Row blocks of the backward statistics pass (row-block-major partials, merged 16 lanes per
 // channel by bn_bwd_finalize_rb_kernel).  At most 512 (tools/ab_bn2.sh, stats pass: 33,540 x
 // 1024 58.8 -> 29.2 us, 262,144 x 128 41.3 -> 27.7 us, 262,144 x 64 17.6 -> 15.6 us against 2048
 // channel-major row blocks; finalize unchanged at ~5 us).
 static int bn_bwd_rb(long rows, int c, int vec) {
   const long need = bn_need(rows, c, vec);
-  long rb = std::min<long>(need, BN_BWD_RB_MAX);
-  rb = std::max<long>(1, std::min<long>(rb, (need + BN_BWD_RB_DIV - 1) / BN_BWD_RB_DIV));
+  long rb = std::min<long>(need, kBnBwdRBMax);
+  rb = std::max<long>(1, std::min<long>(rb, (need + kBnBwdRBDiv - 1) / kBnBwdRBDiv));
   return (int)rb;
 }
 template <typename T, int VEC, class GS>

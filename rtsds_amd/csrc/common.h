@@ -6,6 +6,7 @@
 #include "../../include/rtsds_hip.h"
 
 typedef __bf16 bf16;
+typedef _Float16 f16;  // the fp16 gradient wire only (rtsds_cast, optimizer gradients)
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
 typedef __attribute__((ext_vector_type(4))) short s16x4;
@@ -21,9 +22,11 @@ template <> struct VecT<bf16> { typedef bf16x8 v16; static constexpr int N = 8; 
 
 RT_DEV float to_f(float x) { return x; }
 RT_DEV float to_f(bf16 x) { return (float)x; }
+RT_DEV float to_f(f16 x) { return (float)x; }
 template <typename T> RT_DEV T from_f(float x);
 template <> RT_DEV float from_f<float>(float x) { return x; }
 template <> RT_DEV bf16 from_f<bf16>(float x) { return (bf16)x; }
+template <> RT_DEV f16 from_f<f16>(float x) { return (f16)x; }
 
 // Exact unsigned division by a runtime-invariant divisor (Granlund-Montgomery), valid
 // for n < 2^31.  Built on the host by fastdiv_make(), carried in kernel arguments.

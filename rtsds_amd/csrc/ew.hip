@@ -118,6 +118,8 @@ extern "C" int rtsds_cast(const void* src, int src_dtype, void* dst, int dst_dty
   else if (src_dtype == RTSDS_BF16 && dst_dtype == RTSDS_F32) hipLaunchKernelGGL((cast_kernel<bf16, float>), dim3(b), dim3(256), 0, st, (const bf16*)src, (float*)dst, n);
   else if (src_dtype == RTSDS_F32 && dst_dtype == RTSDS_F32) hipLaunchKernelGGL((cast_kernel<float, float>), dim3(b), dim3(256), 0, st, (const float*)src, (float*)dst, n);
   else if (src_dtype == RTSDS_BF16 && dst_dtype == RTSDS_BF16) hipLaunchKernelGGL((cast_kernel<bf16, bf16>), dim3(b), dim3(256), 0, st, (const bf16*)src, (bf16*)dst, n);
+  else if (src_dtype == RTSDS_F32 && dst_dtype == RTSDS_F16) hipLaunchKernelGGL((cast_kernel<float, f16>), dim3(b), dim3(256), 0, st, (const float*)src, (f16*)dst, n);
+  else if (src_dtype == RTSDS_F16 && dst_dtype == RTSDS_F32) hipLaunchKernelGGL((cast_kernel<f16, float>), dim3(b), dim3(256), 0, st, (const f16*)src, (float*)dst, n);
   else return RTSDS_ERR_UNSUPPORTED;
   RET_LAUNCH();
 }
@@ -1076,13 +1078,8 @@ __global__ void __launch_bounds__(256) bilinear_fwd_rowgroup_kernel(const T* __r
   }
 }
 
-#ifndef BIL_ROWGROUP
-#define BIL_ROWGROUP 1
-#endif
-static const bool kBilRowGroup = BIL_ROWGROUP;
-#ifndef BIL_J
-#define BIL_J 2  // output vectors per thread and column chunk (2, 3, 4, 6 measured: 2 best)
-#endif
+static const bool kBilRowGroup = true;
+static constexpr auto kBilJ = 2;  // output vectors per thread and column chunk (2, 3, 4, 6 measured: 2 best)
 
 // Backward, separable gather (deterministic, no atomics): input index i along one axis
 // receives from outputs o with i0(o) == i (weight l0) or i1(o) == i (weight l1); those o lie
@@ -1247,7 +1244,7 @@ extern "C" int rtsds_bilinear_fwd(const void* x, void* y, int n, int hi, int wi,
       hipLaunchKernelGGL((bilinear_fwd_kernel<T, 0>), dim3(ew_blocks(pix * (c / V))), dim3(256), 0, st, (const T*)x, (T*)y, n, hi, wi, c, ho, wo, scale_h, scale_w, y_ld, y_off);
     else if (c >= V && y_ld == c && y_off == 0 && (wo * c) % V == 0 && 2L * wi * c * 4 <= 64 * 1024 && ho >= hi && kBilRowGroup) {
       // column chunks: <= 256 * kJ vectors each, and enough workgroups to fill the chip
-      constexpr int kJ = BIL_J;
+      constexpr int kJ = kBilJ;
       const int nv = wo * c / V;
       int nchunk = std::max((nv + 256 * kJ - 1) / (256 * kJ), (1024 + n * hi - 1) / (n * hi));
       nchunk = std::min(nchunk, std::max(1, nv / 64));
@@ -1955,12 +1952,13 @@ extern "C" int rtsds_bce_bwd(const float* x, const float* target, const float* g
 // torch.optim.Adam (main.py:116-117; L2 weight decay folded into the gradient, as torch does
 // for weight_decay != 0 without decoupling).  One launch over the flat parameter arena;
 // optionally refreshes the bf16 shadow weights in the same pass.
-__global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m, float* __restrict__ v,
+template <typename GT>
+__global__ void adam_kernel(float* __restrict__ p, const GT* __restrict__ g, float* __restrict__ m, float* __restrict__ v,
                             bf16* __restrict__ shadow, long n, float lr, float b1, float b2, float eps, float wd, float bc1,
                             float bc2_sqrt, float gscale) {
   const float step = lr / bc1;
   GRID_STRIDE(i, n) {
-    float gi = g[i] * gscale;
+    float gi = to_f(g[i]) * gscale;
     float pi = p[i];
     if (wd != 0.f) gi = fmaf(wd, pi, gi);
     float mi = m[i], vi = v[i];
@@ -1977,13 +1975,14 @@ __global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, 
 // Same update with (lr, bias_correction1, sqrt(bias_correction2)) read from device memory, so
 // a captured hipGraph replays correct steps as the host advances lr / step counts between
 // replays (runtime.GraphedStep).
-__global__ void adam_dev_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m, float* __restrict__ v,
+template <typename GT>
+__global__ void adam_dev_kernel(float* __restrict__ p, const GT* __restrict__ g, float* __restrict__ m, float* __restrict__ v,
                                 bf16* __restrict__ shadow, long n, const float* __restrict__ hyper, float b1, float b2, float eps,
                                 float wd, float gscale) {
   const float lr = hyper[0], bc1 = hyper[1], bc2_sqrt = hyper[2];
   const float step = lr / bc1;
   GRID_STRIDE(i, n) {
-    float gi = g[i] * gscale;
+    float gi = to_f(g[i]) * gscale;
     float pi = p[i];
     if (wd != 0.f) gi = fmaf(wd, pi, gi);
     float mi = m[i], vi = v[i];
@@ -1997,21 +1996,32 @@ __global__ void adam_dev_kernel(float* __restrict__ p, const float* __restrict__
     if (shadow) shadow[i] = (bf16)pi;
   }
 }
-extern "C" int rtsds_adam_step_dev(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, void* bf16_shadow,
+// the gradient in fp32 (the arena), or the all-reduced fp16 / bf16 wire copy read directly
+#define DISPATCH_GRAD(gd, ...)                                               \
+  do {                                                                       \
+    if ((gd) == RTSDS_F32) { typedef float GT; __VA_ARGS__; }                \
+    else if ((gd) == RTSDS_BF16) { typedef bf16 GT; __VA_ARGS__; }           \
+    else if ((gd) == RTSDS_F16) { typedef f16 GT; __VA_ARGS__; }             \
+    else return RTSDS_ERR_UNSUPPORTED;                                       \
+  } while (0)
+extern "C" int rtsds_adam_step_dev(float* param, const void* grad, float* exp_avg, float* exp_avg_sq, void* bf16_shadow,
                                    long n, const float* hyper, float beta1, float beta2, float eps, float weight_decay,
-                                   float grad_scale, void* stream) {
+                                   float grad_scale, int grad_dtype, void* stream) {
   if (n <= 0 || !hyper) return RTSDS_ERR_SHAPE;
-  hipLaunchKernelGGL(adam_dev_kernel, dim3(ew_blocks(n, 256, 4096)), dim3(256), 0, (hipStream_t)stream, param, grad, exp_avg,
-                     exp_avg_sq, (bf16*)bf16_shadow, n, hyper, beta1, beta2, eps, weight_decay, grad_scale);
+  DISPATCH_GRAD(grad_dtype, hipLaunchKernelGGL(adam_dev_kernel<GT>, dim3(ew_blocks(n, 256, 4096)), dim3(256), 0,
+                                               (hipStream_t)stream, param, (const GT*)grad, exp_avg, exp_avg_sq,
+                                               (bf16*)bf16_shadow, n, hyper, beta1, beta2, eps, weight_decay, grad_scale));
   RET_LAUNCH();
 }
 
-extern "C" int rtsds_adam_step(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, void* bf16_shadow, long n, float lr,
-                               float beta1, float beta2, float eps, float weight_decay, int step, float grad_scale, void* stream) {
+extern "C" int rtsds_adam_step(float* param, const void* grad, float* exp_avg, float* exp_avg_sq, void* bf16_shadow, long n, float lr,
+                               float beta1, float beta2, float eps, float weight_decay, int step, float grad_scale, int grad_dtype,
+                               void* stream) {
   if (n <= 0 || step <= 0) return RTSDS_ERR_SHAPE;
   const double bc1 = 1.0 - pow((double)beta1, step), bc2 = 1.0 - pow((double)beta2, step);
-  hipLaunchKernelGGL(adam_kernel, dim3(ew_blocks(n, 256, 4096)), dim3(256), 0, (hipStream_t)stream, param, grad, exp_avg, exp_avg_sq,
-                     (bf16*)bf16_shadow, n, lr, beta1, beta2, eps, weight_decay, (float)bc1, (float)sqrt(bc2), grad_scale);
+  DISPATCH_GRAD(grad_dtype, hipLaunchKernelGGL(adam_kernel<GT>, dim3(ew_blocks(n, 256, 4096)), dim3(256), 0, (hipStream_t)stream,
+                                               param, (const GT*)grad, exp_avg, exp_avg_sq, (bf16*)bf16_shadow, n, lr, beta1, beta2,
+                                               eps, weight_decay, (float)bc1, (float)sqrt(bc2), grad_scale));
   RET_LAUNCH();
 }
 
@@ -2110,7 +2120,8 @@ extern "C" int rtsds_confusion(const int64_t* label, const int64_t* pred, unsign
 // first step, else buf = momentum buf + (1 - dampening) d; d = nesterov ? d + momentum buf :
 // buf; p -= lr d.  hyper (device, may be NULL) = {lr, first-step flag}: the hipGraph-replay
 // variant (runtime.GraphedStep) reads them per replay.
-__global__ void sgd_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ buf,
+template <typename GT>
+__global__ void sgd_kernel(float* __restrict__ p, const GT* __restrict__ g, float* __restrict__ buf,
                            bf16* __restrict__ shadow, long n, const float* __restrict__ hyper, float lr, float momentum,
                            float dampening, float wd, int nesterov, int first, float gscale) {
   if (hyper) {
@@ -2119,7 +2130,7 @@ __global__ void sgd_kernel(float* __restrict__ p, const float* __restrict__ g, f
   }
   GRID_STRIDE(i, n) {
     float pi = p[i];
-    float d = g[i] * gscale;
+    float d = to_f(g[i]) * gscale;
     if (wd != 0.f) d = d + wd * pi;
     if (momentum != 0.f) {
       const float b = first ? d : buf[i] * momentum + (1.f - dampening) * d;
@@ -2132,12 +2143,12 @@ __global__ void sgd_kernel(float* __restrict__ p, const float* __restrict__ g, f
   }
 }
 
-extern "C" int rtsds_sgd_step(float* param, const float* grad, float* momentum_buf, void* bf16_shadow, long n,
+extern "C" int rtsds_sgd_step(float* param, const void* grad, float* momentum_buf, void* bf16_shadow, long n,
                               const float* hyper, float lr, float momentum, float dampening, float weight_decay,
-                              int nesterov, int first, float grad_scale, void* stream) {
+                              int nesterov, int first, float grad_scale, int grad_dtype, void* stream) {
   if (n <= 0 || (momentum != 0.f && !momentum_buf)) return RTSDS_ERR_SHAPE;
-  hipLaunchKernelGGL(sgd_kernel, dim3(ew_blocks(n, 256, 4096)), dim3(256), 0, (hipStream_t)stream, param, grad,
-                     momentum_buf, (bf16*)bf16_shadow, n, hyper, lr, momentum, dampening, weight_decay, nesterov, first,
-                     grad_scale);
+  DISPATCH_GRAD(grad_dtype, hipLaunchKernelGGL(sgd_kernel<GT>, dim3(ew_blocks(n, 256, 4096)), dim3(256), 0, (hipStream_t)stream,
+                                               param, (const GT*)grad, momentum_buf, (bf16*)bf16_shadow, n, hyper, lr, momentum,
+                                               dampening, weight_decay, nesterov, first, grad_scale));
   RET_LAUNCH();
 }

@@ -130,6 +130,23 @@ int analyze(hipGraph_t graph, int max_lanes, Analysis& A) {
 
 }  // namespace
 
+extern "C" int rtsds_abi_version(void) { return RTSDS_ABI_VERSION; }
+
+// Nodes captured so far into the graph a capturing stream records into (negative status if the
+// stream is not capturing): GraphedStep ends a segment at a collective only when it has nodes.
+extern "C" int rtsds_capture_nodes(void* stream) {
+  hipStreamCaptureStatus st;
+  unsigned long long id = 0;
+  hipGraph_t g = nullptr;
+  const hipGraphNode_t* deps = nullptr;
+  size_t nd = 0;
+  if (hipStreamGetCaptureInfo_v2((hipStream_t)stream, &st, &id, &g, &deps, &nd) != hipSuccess) return -RTSDS_ERR_LAUNCH;
+  if (st != hipStreamCaptureStatusActive || !g) return -RTSDS_ERR_UNSUPPORTED;
+  size_t n = 0;
+  if (hipGraphGetNodes(g, nullptr, &n) != hipSuccess) return -RTSDS_ERR_LAUNCH;
+  return (int)n;
+}
+
 // Node count of a captured graph (0: an empty capture, e.g. between two back-to-back collectives).
 extern "C" int rtsds_graph_nodes(void* graph) {
   if (!graph) return -RTSDS_ERR_SHAPE;

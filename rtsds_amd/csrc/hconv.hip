@@ -131,10 +131,11 @@ __global__ void __launch_bounds__(256, 1) hconv_fwd_kernel(const HconvArgs P) {
     asm volatile("" ::: "memory");
     const unsigned char* hb = lds + (q & 1) * kStage;
     const unsigned char* wb = hb + kHaloBytes;
-#pragma unroll
-    for (int tap = 0; tap < 9; ++tap) {
+    // the fragments of tap t + 2 are read before the MFMAs of tap t (the scheduling barriers keep
+    // the reads where they are placed): with one wave per SIMD nothing else hides the LDS
+    // latency, which the read-then-use order exposed once per tap
+    auto rd = [&](int tap, bf16x8* fa, bf16x8* fb) {
       const int r = tap / 3, s = tap - 3 * r;
-      bf16x8 fa[4], fb[2];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int p0 = 64 * wave + 16 * i;  // first pixel of group i (16 | TC: one tile row)
@@ -143,10 +144,23 @@ __global__ void __launch_bounds__(256, 1) hconv_fwd_kernel(const HconvArgs P) {
       }
 #pragma unroll
       for (int j = 0; j < 2; ++j) fb[j] = *(const bf16x8*)(wb + tap * 32 * 64 + bslot[j]);
+    };
+    // two taps of look-ahead (three register sets): one tap's 8 MFMAs (128 cycles) did not
+    // cover the read latency where a launch walks a single channel chunk (the FFM data gradient)
+    bf16x8 fa_s[3][4], fb_s[3][2];
+    rd(0, fa_s[0], fb_s[0]);
+    rd(1, fa_s[1], fb_s[1]);
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+      bf16x8* fa = fa_s[tap % 3];
+      bf16x8* fb = fb_s[tap % 3];
+      if (tap + 2 < 9) rd(tap + 2, fa_s[(tap + 2) % 3], fb_s[(tap + 2) % 3]);
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
     }
     // every wave is done with this buffer before it is refilled: its ds_reads retired first
     // (a raw s_barrier does not wait for them; see gl_barrier in conv.hip)
@@ -268,16 +282,14 @@ static bool hconv_geom(const rtsds_conv_desc* d) {
   return d->dtype == RTSDS_BF16 && d->kh == 3 && d->kw == 3 && d->sh == 1 && d->sw == 1 && d->ph == 1 && d->pw == 1 &&
          d->dh == 1 && d->dw == 1 && hconv_tc(d) > 0;
 }
-#ifndef HCONV_KMAX
-#define HCONV_KMAX 512
-#endif
+static constexpr auto kHconvKmax = 512;
 // forward: narrow outputs (Cout <= 32), or Cout a multiple of 32 up to 512 when the reduction
 // is deep enough (Cin >= 256: >= 8 double-buffered channel chunks) -- N-tiled over blockIdx.y,
 // each N tile re-staging the halo.  Measured (bs 8, 1024x512): ResNet layer3 3x3 256 -> 256
 // at 32 x 64: 34 / 40 us fwd / dgrad vs 38 / 44 us on the implicit GEMM; layer1 / layer2
 // (64 / 128 channels, 2-4 chunks) lose to the GEMM (59 vs 41 us, 42 vs 32 us fwd).
 static bool hconv_kc_ok(int k, int c) {
-  return k <= 32 || (k % 32 == 0 && k <= HCONV_KMAX && c >= 256);
+  return k <= 32 || (k % 32 == 0 && k <= kHconvKmax && c >= 256);
 }
 bool hconv_ok(const rtsds_conv_desc* d) {
   if (!hconv_geom(d) || d->c % kCK != 0 || !hconv_kc_ok(d->k, d->c)) return false;

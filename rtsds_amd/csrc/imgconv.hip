@@ -205,15 +205,23 @@ __global__ void __launch_bounds__(256, (KH == 7 || WP != 1) ? 2 : 3) imgconv_fwd
 #pragma unroll
       for (int cb = 0; cb < NCB; ++cb) acc[i][cb] = f32x4{0.f, 0.f, 0.f, 0.f};
     const unsigned char* ab = abuf + b * A_BYTES;
-    // (group-major: a group's KS fragments are read and consumed before the next group's --
-    // the scheduler otherwise hoists all GP x KS reads and spills)
-#pragma unroll
-    for (int i = 0; i < GP; ++i) {
+    // group-major with one group of look-ahead: group i + 1's KS fragments are read before
+    // group i's MFMAs (two register sets; the scheduling barriers keep the reads where they
+    // are placed -- left alone the scheduler hoisted all GP x KS reads and spilled, and reading
+    // each group right before its MFMAs exposed the LDS latency once per group)
+    auto rdg = [&](int i, bf16x8* fa) {
       const int g = GP * wp + i;
       const int goff = ((2 * (g >> 2)) * NC + (g & 3) * 16) * 16;
-      bf16x8 fa[KS];
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) fa[ks] = *(const bf16x8*)(ab + koff[ks] + goff);
+    };
+    bf16x8 fa0[KS], fa1[KS];
+    rdg(0, fa0);
+#pragma unroll
+    for (int i = 0; i < GP; ++i) {
+      bf16x8* fa = (i & 1) ? fa1 : fa0;
+      if (i + 1 < GP) rdg(i + 1, (i & 1) ? fa0 : fa1);
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
@@ -432,6 +440,8 @@ __global__ void __launch_bounds__(256, 2) imgconv_pool_kernel(const ImgPoolArgs 
 #pragma unroll
     for (int g = 0; g < NG; ++g) acc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
     const unsigned char* ab = abuf + b * A_BYTES;
+    // (no look-ahead here, unlike imgconv_fwd_kernel: its second fragment set costs this kernel
+    // a workgroup per CU -- 155 -> 194 VGPRs, eval stem 70 -> 78 us)
 #pragma unroll
     for (int g = 0; g < NG; ++g) {
       const int goff = ((2 * (g >> 2)) * NC + (g & 3) * 16) * 16;
@@ -593,16 +603,14 @@ void imgconv_pool_fwd(const rtsds_conv_desc* d, const void* x4, const void* w, c
   a.hp = hp; a.wp = wp; a.pp = pp;
 // 2 pooled rows per tile (tools/ab_pool.sh, bs 8 1024x512: 106 us vs 111 at 1 row, 155 at 3 with
 // one group per CU; the separate folded conv + pool take 59 + 63 us)
-#ifndef IMG_POOL_PH
-#define IMG_POOL_PH 2
-#endif
-  a.tiles = d->n * rt_cdiv(hp, IMG_POOL_PH) * rt_cdiv(wp, kPW);
+static constexpr auto kImgPoolPH = 2;
+  a.tiles = d->n * rt_cdiv(hp, kImgPoolPH) * rt_cdiv(wp, kPW);
   const int v = img_act_variant(act);
-  const void* k = v == 0 ? (const void*)imgconv_pool_kernel<7, 7, IMG_POOL_PH, 0>
-                : v == 1 ? (const void*)imgconv_pool_kernel<7, 7, IMG_POOL_PH, 1>
-                         : (const void*)imgconv_pool_kernel<7, 7, IMG_POOL_PH, -1>;
+  const void* k = v == 0 ? (const void*)imgconv_pool_kernel<7, 7, kImgPoolPH, 0>
+                : v == 1 ? (const void*)imgconv_pool_kernel<7, 7, kImgPoolPH, 1>
+                         : (const void*)imgconv_pool_kernel<7, 7, kImgPoolPH, -1>;
   static int occ = 0, cus = 0;
-  if (!occ && (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)imgconv_pool_kernel<7, 7, IMG_POOL_PH, 1>, 256, 0) != hipSuccess ||
+  if (!occ && (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)imgconv_pool_kernel<7, 7, kImgPoolPH, 1>, 256, 0) != hipSuccess ||
                occ < 1))
     occ = 1;
   if (!cus && (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0) != hipSuccess || cus < 1)) cus = 256;

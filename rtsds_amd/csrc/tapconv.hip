@@ -128,12 +128,8 @@ __global__ void __launch_bounds__(512, 1) tapconv_kernel(const TapArgs P) {
       const int hr = f / kHC, hc = f - hr * kHC;
       const int ih = oh0 - 1 + hr, iw = ow0 - 1 + hc;
       const bool ok = f < kHalo && (unsigned)ih < (unsigned)P.h && (unsigned)iw < (unsigned)P.w;
-#ifndef TAP_DIAG_NO_DMA
       buf_lds16(rx, lds + b * kHBytes + (wave + kWaves * u) * 1024,
                 ok ? ((img * P.h + ih) * P.w + iw) * (kC * 2) + (((lz & 7) ^ (f & 7)) << 4) : (int)0x80000000, 0);
-#else
-      (void)ok;
-#endif
     }
   };
   issue(t0, 0);
@@ -235,11 +231,7 @@ __global__ void __launch_bounds__(512, 1) tapconv_kernel(const TapArgs P) {
       for (int g = 0; g < 4; ++g)
 #pragma unroll
         for (int cb = 0; cb < kNCB; ++cb)
-#ifndef TAP_DIAG_NO_MFMA
           acc[g][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[cb][step >> 1][step & 1], cur[g], acc[g][cb], 0, 0, 0);
-#else
-          acc[g][cb][0] += (float)cur[g][0];
-#endif
       __builtin_amdgcn_sched_barrier(0);
     }
 
@@ -380,9 +372,6 @@ __global__ void __launch_bounds__(512, 1) tapconv_kernel(const TapArgs P) {
       const int row = px / kTW, col = px - row * kTW;
       const bool ok = oh0 + row < P.h && ow0 + col < P.w;
       const bf16x8 v = *(const bf16x8*)(stage + px * (kC * 2) + ((j ^ (px & 7)) << 4));
-#ifdef TAP_DIAG_NO_STORE
-      if ((float)v[0] == 12345.f)
-#endif
       tap_store16(ry, v, ok ? (((img * P.h + oh0 + row) * P.w + ow0 + col) * kC + 8 * j) * 2 : (int)0x80000000);
     }
   }
@@ -403,11 +392,7 @@ static bool tap_geom(const rtsds_conv_desc* d) {
          (long)d->n * d->h * d->w * kC * 2 < (1L << 31);
 }
 bool tapconv_ok(const rtsds_conv_desc* d) {
-#ifdef RTSDS_NO_TAPCONV  // A/B builds (tools/build_variant.sh): the implicit GEMM instead
-  return false;
-#else
   return tap_geom(d);
-#endif
 }
 static int tap_tiles(const rtsds_conv_desc* d) { return d->n * ((d->h + kTH - 1) / kTH) * ((d->w + kTW - 1) / kTW); }
 static void tap_geom_args(const rtsds_conv_desc* d, TapArgs& a) {

@@ -30,9 +30,7 @@
 
 static const int kUpceCMax = 32;
 typedef float f2 __attribute__((ext_vector_type(2)));
-#ifndef UPCE_ROWS
-#define UPCE_ROWS 32.f  // full-res rows per tile (one wave walks them)
-#endif
+static constexpr auto kUpceRows = 32.f;  // full-res rows per tile (one wave walks them)
 static const int kUpceMaxHeads = 4;
 
 struct UpceGeo {
@@ -73,11 +71,9 @@ RT_DEV float upce_block_sum(float v, float* red) {
 // low-res row goes through the x-fold once (wave-private LDS row x the tile's weight table),
 // i.e. once per scale-factor rows instead of once per row, and no workgroup barrier runs
 // inside the row loop.
+static constexpr int kUpceOcc = 3;  // workgroups per CU (168 VGPRs)
 template <typename T, int CP>
-#ifndef UPCE_OCC
-#define UPCE_OCC 3
-#endif
-__global__ void __launch_bounds__(256, UPCE_OCC) upce_fwd_kernel(UpceArgs a) {
+__global__ void __launch_bounds__(256, kUpceOcc) upce_fwd_kernel(UpceArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const UpceGeo& q = a.g;
   const int TH = q.th, TW = q.tw, C = q.c, TW1 = TW + 1, tid = threadIdx.x, nthr = blockDim.x;
@@ -458,7 +454,7 @@ static bool upce_plan(int n, int hl, int wl, int c, int H, int W, float sh, floa
   g.tw = std::max(1, std::min(32, (int)(64.f / std::ceil(fx))));
   // 32 full-res rows per tile: one wave per (tile, head) walks them, so shorter tiles mean more
   // waves in flight (the row loop is latency-bound at ~3 waves per SIMD)
-  g.th = std::max(1, std::min(32, (int)(UPCE_ROWS / std::ceil(fy))));
+  g.th = std::max(1, std::min(32, (int)(kUpceRows / std::ceil(fy))));
   g.ntr = (hl + g.th - 1) / g.th;
   g.ntc = (wl + g.tw - 1) / g.tw;
   g.wmax = (int)std::ceil((g.tw + 1) * fx) + 4;

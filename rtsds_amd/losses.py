@@ -30,8 +30,10 @@ class BCEWithLogitsLoss(nn.Module):
     first iteration on -- equal shards (DistributedSampler pads its shards to equal length,
     synthetic loaders are equal, main.py's loaders drop_last) or unequal but fixed shards
     (those get the exact weighted mean).  A rank that meets a new local size while another
-    rank hits its cache would desynchronise the collectives; the per-rank cache keys are
-    therefore checked for agreement on every miss."""
+    rank hits its cache would desynchronise the collectives, and that case is NOT detected: the
+    check on a miss (every rank taking part, equal cache lengths) only catches ranks that miss
+    together with different cache histories.  The missing rank's count all-reduce would pair
+    with the other rank's next collective."""
 
     def __init__(self, reduction="mean"):
         super().__init__()

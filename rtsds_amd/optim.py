@@ -34,30 +34,55 @@ _ALLREDUCE = {"dtype": torch.float32}
 
 def set_allreduce_dtype(dtype):
     """Wire dtype of the gradient all-reduce: float32 (exact, default) or float16 / bfloat16
-    (half the xGMI bytes; BASELINE configs[4] runs fp16).  The fp32 arena is cast down, summed
-    and cast back before the Adam step."""
+    (half the xGMI bytes; BASELINE configs[4] runs fp16).  The fp32 gradients are cast into the
+    arena's persistent wire buffer (one rtsds_cast launch per bucket), summed there, and the
+    optimizer kernel reads the summed wire copy directly (no cast back into the fp32 arena,
+    which keeps the rank's local gradients)."""
     if dtype not in (torch.float32, torch.float16, torch.bfloat16):
         raise ValueError("all-reduce dtype must be float32, float16 or bfloat16")
     _ALLREDUCE["dtype"] = dtype
 
 
-def allreduce_flat(buffers):
+_DCODE = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2}
+
+
+def wire_active():
+    """The gradients are all-reduced over a reduced-precision wire (the optimizer then reads
+    the arenas' summed wire copies)."""
+    return _ALLREDUCE["dtype"] != torch.float32 and dp_world() > 1 and dist.is_available() and dist.is_initialized()
+
+
+def _to_wire(buffers, wires):
+    """The tensors to sum: the fp32 gradient slices themselves, or (reduced-precision wire)
+    their casts into the matching slices of the arenas' wire buffers (one rtsds_cast launch
+    each); the optimizer then reads the sums there.  Without ``wires`` (a caller outside the
+    optimizer, e.g. the gloo CPU tests) the buffers are cast by torch and the sums copied back
+    into them after the reduction: returns [(tensor to sum, buffer to copy it back into)]."""
+    if _ALLREDUCE["dtype"] == torch.float32:
+        return [(b, None) for b in buffers]
+    if wires is None:
+        return [(b.to(_ALLREDUCE["dtype"]), b) for b in buffers]
+    out = []
+    for b, w in zip(buffers, wires):
+        lib.rtsds_cast(b.data_ptr(), 0, w.data_ptr(), _DCODE[w.dtype], b.numel(), stream())
+        out.append((w, None))
+    return out
+
+
+def allreduce_flat(buffers, wires=None):
     """Sum flat gradient buffers over the data-parallel group (RCCL over xGMI for HIP
     tensors, gloo for CPU tests) -- one collective per buffer, replacing DataParallel's
     per-module reduce (utils.py:104-105).  The rtsds losses are already normalised by the
     global batch (runtime.dp_world), so the SUM is the single-device gradient; returns the
-    gradient scale the Adam kernel applies (1.0)."""
+    gradient scale the Adam kernel applies (1.0).  ``wires``: the buffers' slices of the
+    arenas' wire buffers (reduced-precision wire): the sum lands there."""
     if not (dist.is_available() and dist.is_initialized()):
         return 1.0
     if dp_world() > 1:
-        wire = _ALLREDUCE["dtype"]
-        for b in buffers:
-            if wire == torch.float32:
-                collective(lambda b=b: dist.all_reduce(b))
-            else:
-                t = b.to(wire)
-                collective(lambda t=t: dist.all_reduce(t))  # a graph-segment break under capture
-                b.copy_(t)
+        for t, back in _to_wire(buffers, wires):
+            collective(lambda t=t: dist.all_reduce(t))  # a graph-segment break under capture
+            if back is not None:
+                back.copy_(t)
     return 1.0
 
 
@@ -82,20 +107,17 @@ def set_overlap_allreduce(on):
     _OVERLAP["on"] = bool(on)
 
 
-def allreduce_start(buffers):
+def allreduce_start(buffers, wires=None):
     """Start the SUM all-reduce of flat gradient buffers now, asynchronously (RCCL on its own
     stream, overlapping whatever the caller enqueues next), and return a finisher that makes
-    the current stream wait for them (and casts reduced-precision wire copies back); None
-    when there is nothing to reduce.  Under runtime.GraphedStep capture the start and the wait
-    are graph-segment breaks re-issued between replays, so a replayed iteration overlaps the
-    same way (DA iteration: G's all-reduce runs beside the discriminator phase)."""
+    the current stream wait for them; None when there is nothing to reduce.  ``wires``: as
+    allreduce_flat.  Under runtime.GraphedStep capture the start and the wait are graph-segment
+    breaks re-issued between replays, so a replayed iteration overlaps the same way (DA
+    iteration: G's all-reduce runs beside the discriminator phase)."""
     if not (dist.is_available() and dist.is_initialized()) or dp_world() <= 1:
         return None
-    wire = _ALLREDUCE["dtype"]
-    pending, pairs = [], []
-    for b in buffers:
-        t = b if wire == torch.float32 else b.to(wire)
-        pairs.append((b, t))
+    pending, pairs = [], _to_wire(buffers, wires)
+    for t, _ in pairs:
         collective(lambda t=t: pending.append(dist.all_reduce(t, async_op=True)))
 
     def wait_all():
@@ -105,9 +127,9 @@ def allreduce_start(buffers):
 
     def finish():
         collective(wait_all)
-        for b, t in pairs:
-            if t is not b:
-                b.copy_(t)
+        for t, back in pairs:
+            if back is not None:
+                back.copy_(t)
     return finish
 
 
@@ -133,6 +155,7 @@ class _Arena:
         self.m = torch.zeros(total, dtype=torch.float32, device=dev)
         self.v = torch.zeros(total, dtype=torch.float32, device=dev) if second else None
         self.shadow = torch.empty(total, dtype=torch.bfloat16, device=dev)
+        self.gwire = None  # reduced-precision all-reduce wire: the summed gradients (wire())
         self.steps = [0] * len(params)
         self.touched = [False] * len(params)
         self.gen = [0] * len(params)  # generation of the last gradient write (_GEN)
@@ -156,6 +179,18 @@ class _Arena:
             p._rt_arena = (self, i)
             if p.requires_grad:
                 p.register_post_accumulate_grad_hook(self._hook(i))
+
+    def wire(self):
+        """The persistent gradient wire buffer in the current wire dtype (allocated once)."""
+        dt = _ALLREDUCE["dtype"]
+        if self.gwire is None or self.gwire.dtype != dt:
+            self.gwire = torch.zeros(self.total, dtype=dt, device=self.gflat.device)
+        return self.gwire
+
+    def reduced_grad(self):
+        """The all-reduced gradients the optimizer applies (fp32): the arena itself, or the
+        summed reduced-precision wire copy."""
+        return self.gwire.float() if wire_active() and self.gwire is not None else self.gflat
 
     def _hook(self, i):
         def mark(_p):
@@ -342,15 +377,18 @@ class _FlatOptimizer(torch.optim.Optimizer):
             self._reduced = [[False] * len(a.params) for a in arenas]
             for a, red in zip(arenas, self._reduced):
                 a.reduced = red
-        bufs = []
+        bufs, wires = [], []
         for a, red in zip(arenas, self._reduced):
             idx = [i for i in range(len(a.params)) if not red[i] and
                    (not partial or (a.touched[i] and (since is None or a.gen[i] >= since)))]
             for i in idx:
                 red[i] = True
-            bufs += [a.gflat[lo:hi] for lo, hi in self._ranges(a, idx)]
+            rng = self._ranges(a, idx)
+            bufs += [a.gflat[lo:hi] for lo, hi in rng]
+            if wire_active():
+                wires += [a.wire()[lo:hi] for lo, hi in rng]
         if bufs:
-            fin = allreduce_start(bufs)
+            fin = allreduce_start(bufs, wires if wire_active() else None)
             if fin is not None:
                 self._finish.append(fin)
 
@@ -371,7 +409,7 @@ class _FlatOptimizer(torch.optim.Optimizer):
             gscale = 1.0
         else:
             self._fix_grads(arenas)
-            gscale = allreduce_flat([a.gflat for a in arenas])
+            gscale = allreduce_flat([a.gflat for a in arenas], [a.wire() for a in arenas] if wire_active() else None)
         # contiguous runs of touched parameters with equal step counts -> one launch each
         runs = []
         for gi, a in enumerate(arenas):
@@ -456,6 +494,14 @@ def _ptrs(a, lo, hi, *attrs):
     return tuple(getattr(a, at).data_ptr() + 4 * lo for at in attrs)
 
 
+def _grad(a, lo):
+    """(pointer, dtype code) of the gradients the update reads from arena offset lo: the fp32
+    arena, or the summed reduced-precision wire copy."""
+    if wire_active() and a.gwire is not None:
+        return a.gwire.data_ptr() + a.gwire.element_size() * lo, _DCODE[a.gwire.dtype]
+    return a.gflat.data_ptr() + 4 * lo, 0
+
+
 class Adam(_FlatOptimizer):
     """torch.optim.Adam (main.py:116-117) as one rtsds_adam_step launch per run."""
 
@@ -469,13 +515,14 @@ class Adam(_FlatOptimizer):
 
     def _launch(self, g, a, lo, hi, t, hyper, gscale):
         b1, b2 = g["betas"]
-        ptrs = _ptrs(a, lo, hi, "flat", "gflat", "m", "v") + (a.shadow.data_ptr() + 2 * lo, hi - lo)
+        gp, gd = _grad(a, lo)
+        ptrs = _ptrs(a, lo, hi, "flat") + (gp,) + _ptrs(a, lo, hi, "m", "v") + (a.shadow.data_ptr() + 2 * lo, hi - lo)
         if hyper is not None:
             lib.rtsds_adam_step_dev(*ptrs, hyper, float(b1), float(b2), float(g["eps"]),
-                                    float(g["weight_decay"]), gscale, stream())
+                                    float(g["weight_decay"]), gscale, gd, stream())
         else:
             lib.rtsds_adam_step(*ptrs, float(g["lr"]), float(b1), float(b2), float(g["eps"]),
-                                float(g["weight_decay"]), t, gscale, stream())
+                                float(g["weight_decay"]), t, gscale, gd, stream())
 
     def _hyper3(self, g, t):
         # betas rounded to fp32 first, exactly as rtsds_adam_step receives them (eager and
@@ -503,9 +550,10 @@ class SGD(_FlatOptimizer):
                                       weight_decay=weight_decay, nesterov=nesterov))
 
     def _launch(self, g, a, lo, hi, t, hyper, gscale):
-        lib.rtsds_sgd_step(*_ptrs(a, lo, hi, "flat", "gflat", "m"), a.shadow.data_ptr() + 2 * lo, hi - lo,
+        gp, gd = _grad(a, lo)
+        lib.rtsds_sgd_step(*_ptrs(a, lo, hi, "flat"), gp, *_ptrs(a, lo, hi, "m"), a.shadow.data_ptr() + 2 * lo, hi - lo,
                            hyper, float(g["lr"]), float(g["momentum"]), float(g["dampening"]),
-                           float(g["weight_decay"]), int(bool(g["nesterov"])), int(t == 1), gscale, stream())
+                           float(g["weight_decay"]), int(bool(g["nesterov"])), int(t == 1), gscale, gd, stream())
 
     def _hyper3(self, g, t):
         return [float(g["lr"]), 1.0 if t == 1 else 0.0, 0.0]

@@ -7,6 +7,7 @@
 import contextlib
 import os
 import time
+import warnings
 
 import torch
 
@@ -263,7 +264,14 @@ class BranchOut(torch.autograd.Function):
 # segment launch and cross-queue wait costs ~20 us of GPU idle time.  GraphedStep therefore
 # captures both the branch-stream and the serial variant, adds the split replay of the branch
 # capture, and keeps whichever runs fastest (submit="auto").
-SUBMIT = {"mode": "auto", "max_lanes": 4, "trial_calls": 3}
+SUBMIT = {"mode": "auto", "max_lanes": 4, "trial_calls": 3, "host_frac": 0.5}
+
+
+def capture_nodes(stream):
+    """Nodes captured so far by the capture ``stream`` records into (None if it is not capturing)."""
+    from ._lib import load
+    n = load().rtsds_capture_nodes(stream.cuda_stream)
+    return n if n >= 0 else None
 
 
 def graph_nodes(graph):
@@ -451,7 +459,7 @@ class GraphedStep:
         self.variants = []  # [(name, segments [(graph or None, [collectives])], runners, outputs)]
         first = "serial" if mode == "serial" else ("split" if mode == "split" else "branches")
         self._add_variant(first, fn, serial=first == "serial", split=first == "split")
-        if mode == "auto" and max(r.lanes for r, _ in self.variants[0][2]) > 1:
+        if mode == "auto" and max((r.lanes for r, _ in self.variants[0][2] if r is not None), default=1) > 1:
             self._add_variant("serial", fn, serial=True, split=False)
             # the branch capture also replayed as per-stream segment graphs (no second capture):
             # ~GPU time of the branch graph at the serial graph's host cost where it has few
@@ -481,11 +489,16 @@ class GraphedStep:
                 self._graph = torch.cuda.CUDAGraph(keep_graph=True)
                 self._graph.capture_begin(pool=self._pool, capture_error_mode=CAPTURE_MODE)
                 _capture["step"] = self
+                self._cap_stream = cap_stream
                 try:
                     outputs = fn()
                 finally:
                     _capture["step"] = None
-                    self._graph.capture_end()
+                    empty = capture_nodes(cap_stream) == 0
+                    with warnings.catch_warnings():
+                        if empty:  # a collective ended the iteration: dropped below, no warning
+                            warnings.filterwarnings("ignore", message="The CUDA Graph is empty")
+                        self._graph.capture_end()
                 if graph_nodes(self._graph) > 0 or not self.segments:
                     self.segments.append((self._graph, []))
         finally:
@@ -499,12 +512,18 @@ class GraphedStep:
     def _use(self, i):
         self.variant = self.variants[i][0]
         self.segments, self.runners, self.outputs = self.variants[i][1], self.variants[i][2], self.variants[i][3]
-        self.graph = self.segments[0][0]
+        self.graph = next((g for g, _ in self.segments if g is not None), None)
 
     def _break(self, coll):
-        """End the current segment at a collective.  An empty capture (two collectives back to
-        back, or one at the very start) is dropped: its collective joins the previous segment's
-        list, so a replay launches no empty graph."""
+        """End the current segment at a collective.  Nothing captured since the last break (two
+        collectives back to back, or one at the very start): the capture stays open and the
+        collective joins the previous segment's list, so no empty graph is captured or launched."""
+        if capture_nodes(self._cap_stream) == 0:
+            if self.segments:
+                self.segments[-1][1].append(coll)
+            else:
+                self.segments.append((None, [coll]))
+            return
         self._graph.capture_end()
         if graph_nodes(self._graph) > 0:
             self.segments.append((self._graph, [coll]))
@@ -525,6 +544,9 @@ class GraphedStep:
             vi = self._calls // int(SUBMIT["trial_calls"])
             self._use(vi)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            # drained queues: the host time below is the submission's own CPU work, not the
+            # back-pressure of a previous replay still filling the hardware queues
+            torch.cuda.synchronize()
             e0.record()
         t0 = time.perf_counter()
         for r, colls in self.runners:
@@ -544,13 +566,18 @@ class GraphedStep:
         return outputs
 
     def _decide(self):
-        """Keep the multi-stream graph ("branches") unless its host submission is within 10 % of
-        its GPU time (host-bound); otherwise the variant with the smallest max(host submission,
-        GPU) time per step (the first trial replay of each is a warm-up).  The trials replay
-        each variant in isolation; sustained, consecutive branch-graph replays overlap each
-        other's head and tail, which the per-stream segment graphs of "split" do not (bench:
-        BiSeNet seg 5.45 ms/step branches vs 5.66 split with near-equal trials; DeepLab DA 53.6
-        branches vs 55.1 split with the branches host at 45 of 55 ms)."""
+        """Keep the multi-stream graph ("branches") unless its host submission takes more than
+        half its GPU time (SUBMIT["host_frac"]); otherwise the variant with the smallest
+        max(host submission, GPU) time per step (the first trial replay of each is a warm-up).
+        Each trial replay starts on drained queues, so its host time is the submission's CPU
+        work: back to back, the node-by-node submission of a multi-stream graph fills the
+        hardware queues and then waits for the GPU (DeepLab DA: 41.8 of 50.3 ms "host" per step
+        in round 4, nearly all of it that wait), which says nothing about whether the host can
+        keep up -- under data parallelism it is the CPU work that delays the collectives issued
+        between segments.  The trials replay each variant in isolation; sustained, consecutive
+        branch-graph replays overlap each other's head and tail, which the per-stream segment
+        graphs of "split" do not (bench: BiSeNet seg 5.45 ms/step branches vs 5.66 split with
+        near-equal trials)."""
         torch.cuda.synchronize()
         costs, hosts, names = [], [], []
         for (name, *_), rec in zip(self.variants, self._trial):
@@ -561,8 +588,9 @@ class GraphedStep:
             costs.append(max(host, gpu))
             hosts.append(host)
             names.append(name)
-        if "branches" in names and hosts[names.index("branches")] <= 0.9 * costs[names.index("branches")]:
-            best = names.index("branches")
+        bi = names.index("branches") if "branches" in names else -1
+        if bi >= 0 and hosts[bi] <= float(SUBMIT["host_frac"]) * costs[bi]:
+            best = bi
         else:
             best = min(range(len(costs)), key=costs.__getitem__)
         # drop the variants not chosen: their graphs, split-replay clones and the captured

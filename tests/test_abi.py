@@ -41,6 +41,13 @@ def test_ctypes_signature_matches_header(name):
     assert (res is _lib.c_size_t) == (ret == "size_t"), name
 
 
+def test_abi_version_matches_header():
+    """The loader refuses a library of another ABI revision (stale A/B variant builds)."""
+    m = re.search(r"#define RTSDS_ABI_VERSION (\d+)", open(HDR).read())
+    assert m and int(m.group(1)) == _lib.ABI_VERSION
+    assert _lib.load().rtsds_abi_version() == _lib.ABI_VERSION
+
+
 def test_errors_raise_without_fallback():
     # the product path refuses CPU tensors instead of silently computing elsewhere
     import torch

@@ -164,7 +164,7 @@ def _wire_worker(rank, world, port, out):
     """The same sharded DA iteration twice, with the gradient all-reduce on an fp32 wire and on
     an fp16 wire (BASELINE configs[4]: "fp16+fp32 grad all-reduce").  Saves, per rank, the local
     gradients handed to the all-reduce (recorded by wrapping optim.allreduce_start /
-    allreduce_flat), the reduced gradients (the arenas keep them after step()) and the updated
+    allreduce_flat), the reduced gradients (Arena.reduced_grad after step()) and the updated
     parameters."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
@@ -176,9 +176,9 @@ def _wire_worker(rank, world, port, out):
     rec = []
 
     def spy(orig):
-        def f(bufs):
+        def f(bufs, wires=None):
             rec.extend((b.data_ptr(), b.detach().clone()) for b in bufs)
-            return orig(bufs)
+            return orig(bufs, wires)
         return f
     optim.allreduce_start = spy(optim.allreduce_start)
     optim.allreduce_flat = spy(optim.allreduce_flat)
@@ -186,8 +186,8 @@ def _wire_worker(rank, world, port, out):
     def flat(opt, local):
         parts = []
         for a in opt.arenas():
-            if not local:
-                parts.append(a.gflat.cpu())
+            if not local:  # the summed gradients the update applied (the wire copy for fp16)
+                parts.append(a.reduced_grad().cpu())
                 continue
             loc, base = torch.zeros_like(a.gflat), a.gflat.data_ptr()
             for ptr, v in rec:

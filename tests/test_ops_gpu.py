@@ -693,7 +693,7 @@ def test_adam_matches_torch():
         opt.step()
         gd = gr.to(DEV)
         lib.rtsds_adam_step(pd.data_ptr(), gd.data_ptr(), m.data_ptr(), v.data_ptr(), sh.data_ptr(),
-                            10007, 1e-3, 0.9, 0.999, 1e-8, 1e-4, i, 1.0, stream())
+                            10007, 1e-3, 0.9, 0.999, 1e-8, 1e-4, i, 1.0, 0, stream())
     _close(pd, pr, torch.float32, "param", 1e-6)
     _close(sh.float(), pr.detach().bfloat16().float(), torch.float32, "shadow", 1e-2)
 
@@ -1043,3 +1043,92 @@ def test_stem_conv_bn_maxpool_eval_fused(hw, ceil):
     assert fused is not None and fused.shape == ref.shape, (None if fused is None else fused.shape, ref.shape)
     assert torch.equal(fused.float(), ref.float())
     assert torch.equal(mod.float(), ref.float())
+
+
+@pytest.mark.parametrize("geo", [(2, 18, 120), (1, 7, 56)])
+def test_tapconv_partial_tiles(geo):
+    """The register-weight direct 3x3 64 -> 64 conv (tapconv.hip, ResNet layer1) through the C ABI
+    on geometries with partial tiles: widths with w % 64 in 49..63 (a last column tile with
+    valid columns < 64) and heights that end inside a 4-row tile, so the edge columns / rows, the
+    out-of-range buffer stores and the Chan merge of the statistics over tiles with unequal
+    counts all run.  Every epilogue the networks launch, against float64 on the bf16 operands:
+    forward (plain, ReLU, BatchNorm statistics, eval BN scale / shift + residual + ReLU) and data
+    gradient (plain, accumulate, ReLU mask, BatchNorm-backward statistics)."""
+    import ctypes
+    from rtsds_amd._lib import lib
+    from rtsds_amd.functional import _conv_desc, _P
+    from rtsds_amd.runtime import stream, workspace
+
+    n, h, w = geo
+    c = 64
+    g = torch.Generator().manual_seed(n * 1000 + h * 10 + w)
+    bf = torch.bfloat16
+
+    def rnd(*shape, scale=1.0):
+        return (torch.randn(*shape, generator=g, dtype=torch.float64) * scale).bfloat16().double()
+    x, wt, dy, res, aux = rnd(n, c, h, w), rnd(c, c, 3, 3, scale=(9 * c) ** -0.5), rnd(n, c, h, w), rnd(n, c, h, w), \
+        rnd(n, c, h, w)
+    bias, scale, shift = torch.randn(c, generator=g).double(), torch.rand(c, generator=g).double() + 0.5, \
+        torch.randn(c, generator=g).double()
+    xd, wd, dyd, resd, auxd = (_dev(t, bf) for t in (x, wt, dy, res, aux))
+    d = _conv_desc(xd, c, 3, 3, (1, 1), (1, 1), (1, 1))
+    st = stream()
+    wsf = workspace(lib.rtsds_conv2d_fwd_workspace(ctypes.byref(d)), xd.device)
+    wsd = workspace(lib.rtsds_conv2d_dgrad_workspace(ctypes.byref(d)), xd.device)
+    conv = TF.conv2d(x, wt, None, 1, 1)
+    dgr = TF.conv_transpose2d(dy, wt, padding=1)
+    f32 = lambda t: t.float().to(DEV).contiguous()  # noqa: E731
+
+    def fwd(b, act, stats=None):
+        y = torch.empty_like(xd)
+        assert lib.rtsds_conv2d_fwd(ctypes.byref(d), _P(xd), _P(wd), None if b is None else _P(b), _P(y), act,
+                                    None if stats is None else _P(stats), _P(wsf), wsf.numel(), st) == 0
+        return y
+    _close(fwd(None, 0), conv, bf, "fwd plain", tol=1e-2)
+    _close(fwd(f32(bias), 1), TF.relu(conv + bias.view(1, -1, 1, 1)), bf, "fwd bias relu", tol=1e-2)
+    tiles = lib.rtsds_conv2d_fwd_stats_tiles(ctypes.byref(d))
+    stats = torch.zeros(c, tiles, 4, device=DEV)
+    _close(fwd(None, 0, stats), conv, bf, "fwd stats y", tol=1e-2)
+    s = stats.double().cpu()
+    cnt = s[:, :, 0]
+    tot = cnt.sum(1)
+    mean = (cnt * s[:, :, 1]).sum(1) / tot
+    m2 = (s[:, :, 2] + cnt * (s[:, :, 1] - mean[:, None]) ** 2).sum(1)
+    assert torch.all(tot == n * h * w), tot
+    _close(mean, conv.mean(dim=(0, 2, 3)), bf, "stats mean", tol=1e-4)
+    _close(m2 / tot, conv.var(dim=(0, 2, 3), unbiased=False), bf, "stats var", tol=1e-4)
+    y = torch.empty_like(xd)
+    assert lib.rtsds_conv2d_fwd_bn(ctypes.byref(d), _P(xd), _P(wd), _P(f32(scale)), _P(f32(shift)), _P(resd), _P(y), 1,
+                                   _P(wsf), wsf.numel(), st) == 0
+    _close(y, TF.relu(conv * scale.view(1, -1, 1, 1) + shift.view(1, -1, 1, 1) + res), bf, "fwd bn res relu",
+           tol=1e-2)
+
+    dx = torch.empty_like(xd)
+    assert lib.rtsds_conv2d_dgrad(ctypes.byref(d), _P(dyd), _P(wd), _P(dx), 0, _P(wsd), wsd.numel(), st) == 0
+    _close(dx, dgr, bf, "dgrad", tol=1e-2)
+    dxa = auxd.clone()
+    assert lib.rtsds_conv2d_dgrad(ctypes.byref(d), _P(dyd), _P(wd), _P(dxa), 1, _P(wsd), wsd.numel(), st) == 0
+    _close(dxa, dgr + aux, bf, "dgrad accumulate", tol=1e-2)
+    dxm = torch.empty_like(xd)
+    assert lib.rtsds_conv2d_dgrad_act(ctypes.byref(d), _P(dyd), _P(wd), _P(dxm), _P(auxd), 1, _P(wsd), wsd.numel(),
+                                      st) == 0
+    _close(dxm, dgr * (aux > 0), bf, "dgrad relu mask", tol=1e-2)
+    btiles = lib.rtsds_conv2d_dgrad_bnstats_tiles(ctypes.byref(d))
+    assert btiles > 0
+    gamma, beta = torch.rand(c, generator=g).double() + 0.5, torch.randn(c, generator=g).double() * 0.2
+    bmean, binv = torch.randn(c, generator=g).double() * 0.1, torch.rand(c, generator=g).double() + 0.5
+    part = torch.zeros(c, btiles, 2, device=DEV)
+    dxb = torch.empty_like(xd)
+    assert lib.rtsds_conv2d_dgrad_bnstats(ctypes.byref(d), _P(dyd), _P(wd), _P(dxb), _P(auxd), _P(f32(gamma)),
+                                          _P(f32(beta)), _P(f32(bmean)), _P(f32(binv)), 1, _P(part), _P(wsd),
+                                          wsd.numel(), st) == 0
+    torch.cuda.synchronize()
+    _close(dxb, dgr, bf, "dgrad bnstats dx", tol=1e-2)
+    # the statistics are taken from the stored (bf16-rounded) dx values
+    dxs = dxb.double().cpu()
+    sc = (gamma * binv).view(1, -1, 1, 1)
+    pre = aux * sc + (beta.view(1, -1, 1, 1) - bmean.view(1, -1, 1, 1) * sc)
+    gg = dxs * (pre > 0)
+    p = part.double().cpu().sum(1)
+    _close(p[:, 0], gg.sum(dim=(0, 2, 3)), bf, "bnstats sum g", tol=1e-4)
+    _close(p[:, 1], (gg * (aux - bmean.view(1, -1, 1, 1))).sum(dim=(0, 2, 3)), bf, "bnstats sum g(x-mean)", tol=1e-4)

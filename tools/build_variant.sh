@@ -5,10 +5,10 @@
 # linked from the main build's objects (make -C rtsds_amd/csrc first).  Default: all units.
 set -e
 cd "$(dirname "$0")/../rtsds_amd/csrc"
-name=$1; flags=$2; units=${3:-"conv hconv imgconv tapconv pw bn ew upce data graph"}
+name=$1; flags=$2; units=${3:-"conv conv_gemm_fwd conv_gemm_dgrad conv_gemm_wgrad hconv imgconv tapconv pw bn ew upce data graph"}
 out=build/var_$name
 rm -rf $out && mkdir -p $out
-for f in conv hconv imgconv tapconv pw bn ew upce data graph; do
+for f in conv conv_gemm_fwd conv_gemm_dgrad conv_gemm_wgrad hconv imgconv tapconv pw bn ew upce data graph; do
   if [[ " $units " == *" $f "* ]]; then
     /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-function -Wno-unused-variable $flags -c $f.hip -o $out/$f.o &
   else
