@@ -156,7 +156,8 @@ template <typename T> RT_DEV typename VecT<T>::v16 vzero() {
 //       swizzled unpadded image above, the next K-tile's DMA in flight across the barrier
 //       (counted vmcnt, raw s_barrier); 0 = register-staged double buffer.
 template <typename T, int MODE, int BM, int BN, int BK, int WM, int WN, int ALA, int ALB, int GL>
-__global__ void __launch_bounds__(256, (GL && BM >= 128 && BN >= 128) ? 2 : 1) conv_gemm_kernel(const ConvArgs P0) {
+__global__ void __launch_bounds__(64 * WM * WN, (GL && WM * WN == 4 && BM >= 128 && BN >= 128) ? 2 : 1)
+conv_gemm_kernel(const ConvArgs P0) {
   ConvArgs P = P0;
   if (MODE == MODE_DGRAD && P0.nph > 1) {
     const ConvArgs::Phase& q = P0.phs[blockIdx.z];
@@ -176,10 +177,11 @@ __global__ void __launch_bounds__(256, (GL && BM >= 128 && BN >= 128) ? 2 : 1) c
   constexpr int A_EL = RC ? BK * PA : BM * PA;
   constexpr int B_EL = RC ? BK * PB : BN * PB;
   constexpr int CA = BM * BK / V, CB = BN * BK / V;      // 16-B chunks per tile
-  constexpr int NA = (CA + 255) / 256, NB = (CB + 255) / 256;
+  constexpr int NW = WM * WN, NT = 64 * NW;  // waves / threads per workgroup (4 or 8 waves)
+  constexpr int NA = (CA + NT - 1) / NT, NB = (CB + NT - 1) / NT;
   constexpr int WTM = BM / WM, WTN = BN / WN, FM = WTM / 16, FN = WTN / 16;
   constexpr int KS = Mma<T>::KS;
-  static_assert(WM * WN == 4, "4 waves");
+  static_assert(NW == 4 || NW == 8, "4 or 8 waves");
   static_assert(BK % KS == 0, "BK");
   static_assert(!RC || BK % (sizeof(T) == 2 ? 32 : 16) == 0, "RC BK");
 
@@ -235,7 +237,7 @@ __global__ void __launch_bounds__(256, (GL && BM >= 128 && BN >= 128) ? 2 : 1) c
   if (!RC) {
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
-      const int id = tid + 256 * i;
+      const int id = tid + NT * i;
       const int row = id / (BK / V);
       const int m = m0 + row;
       a_ok[i] = (id < CA) && (m < P.M);
@@ -284,7 +286,7 @@ __global__ void __launch_bounds__(256, (GL && BM >= 128 && BN >= 128) ? 2 : 1) c
     rs_b = make_rsrc(gb, P.N * P.K * 2);
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
-      const int row = i * 32 + wave * 8 + (lane >> 3);
+      const int row = i * (8 * NW) + wave * 8 + (lane >> 3);
       const int ch = gl_swz(row, lane & 7) * V;
       gba_base[i] = MODE == MODE_FWD ? (int)a_off[i] + (a_h[i] * P.w + a_w[i]) * P.c + ch
                                      : (int)a_off[i] + ((a_h[i] >> gsh) * P.wo + (a_w[i] >> gsh)) * P.k + ch;
@@ -295,7 +297,7 @@ __global__ void __launch_bounds__(256, (GL && BM >= 128 && BN >= 128) ? 2 : 1) c
     }
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
-      const int row = i * 32 + wave * 8 + (lane >> 3);
+      const int row = i * (8 * NW) + wave * 8 + (lane >> 3);
       const int nrow = n0 + row;
       gbb_off[i] = nrow < P.N ? (nrow * P.K + gl_swz(row, lane & 7) * V) * 2 : (int)0x80000000;
     }
@@ -310,7 +312,7 @@ __global__ void __launch_bounds__(256, (GL && BM >= 128 && BN >= 128) ? 2 : 1) c
     constexpr int CPB = BN / V, RPB = 64 / CPB;
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
-      const int row = (i * 4 + wave) * RPB + lane / CPB;
+      const int row = (i * NW + wave) * RPB + lane / CPB;
       gb_dh[i] = P.wo >= 64 ? 0 : row / P.wo;
       gb_dw[i] = P.wo >= 64 ? row : row - gb_dh[i] * P.wo;
       const int nn = n0 + ((lane % CPB) ^ rc_swz<BN>(row)) * V;
@@ -332,7 +334,7 @@ __global__ void __launch_bounds__(256, (GL && BM >= 128 && BN >= 128) ? 2 : 1) c
       constexpr int CPA = BM / V, RPA = 64 / CPA, CPB = BN / V, RPB = 64 / CPB;
 #pragma unroll
       for (int i = 0; i < NA; ++i) {
-        const int row = (i * 4 + wave) * RPA + lane / CPA;
+        const int row = (i * NW + wave) * RPA + lane / CPA;
         const int co = m0 + ((lane % CPA) ^ rc_swz<BM>(row)) * V;
         wga_off[i] = co < P.M ? (row * P.k + co) * 2 : (int)0x80000000;
       }
@@ -369,7 +371,7 @@ __global__ void __launch_bounds__(256, (GL && BM >= 128 && BN >= 128) ? 2 : 1) c
       }
 #pragma unroll
       for (int i = 0; i < NA; ++i) {
-        const int id = tid + 256 * i;
+        const int id = tid + NT * i;
         const int kc = id % (BK / V);
         V16 v = vzero<T>();
         if (ALA >= 1) {
@@ -432,7 +434,7 @@ __global__ void __launch_bounds__(256, (GL && BM >= 128 && BN >= 128) ? 2 : 1) c
       // ---- B (KC rows of the [N][K] weight matrix)
 #pragma unroll
       for (int i = 0; i < NB; ++i) {
-        const int id = tid + 256 * i;
+        const int id = tid + NT * i;
         const int row = id / (BK / V), kc = id % (BK / V);
         const int nrow = n0 + row, kk = k0 + kc * V;
         V16 v = vzero<T>();
@@ -452,7 +454,7 @@ __global__ void __launch_bounds__(256, (GL && BM >= 128 && BN >= 128) ? 2 : 1) c
       // ---- WGRAD A: dY rows (pixels) x Cout columns
 #pragma unroll
       for (int i = 0; i < NA; ++i) {
-        const int id = tid + 256 * i;
+        const int id = tid + NT * i;
         const int kk = id / (BM / V), cc = id % (BM / V);
         const int q = k0 + kk, co = m0 + cc * V;
         V16 v = vzero<T>();
@@ -471,7 +473,7 @@ __global__ void __launch_bounds__(256, (GL && BM >= 128 && BN >= 128) ? 2 : 1) c
       // ---- WGRAD B: input patches, rows = output pixels, columns = (r, s, ci)
 #pragma unroll
       for (int i = 0; i < NB; ++i) {
-        const int id = tid + 256 * i;
+        const int id = tid + NT * i;
         const int kk = id / (BN / V), cc = id % (BN / V);
         const int q = k0 + kk;
         V16 v = vzero<T>();
@@ -514,7 +516,7 @@ __global__ void __launch_bounds__(256, (GL && BM >= 128 && BN >= 128) ? 2 : 1) c
       constexpr int CPB = BN / V, RPB = 64 / CPB;
       if (P.gbuf && P.wg_rows) {
 #pragma unroll
-        for (int i = 0; i < NA; ++i) buf_lds16(rs_a, sa + (i * 4 + wave) * RPA * BM, wga_off[i], k0 * P.k * 2);
+        for (int i = 0; i < NA; ++i) buf_lds16(rs_a, sa + (i * NW + wave) * RPA * BM, wga_off[i], k0 * P.k * 2);
         const int t_img = fdiv(k0, P.f_howo), t_rem = k0 - t_img * P.ho * P.wo;
         const int t_oh = fdiv(t_rem, P.f_wo), t_ow = t_rem - t_oh * P.wo;
         const int uh = t_oh * P.sh, uw = t_ow * P.sw;
@@ -522,13 +524,13 @@ __global__ void __launch_bounds__(256, (GL && BM >= 128 && BN >= 128) ? 2 : 1) c
 #pragma unroll
         for (int i = 0; i < NB; ++i) {
           const bool ok = (unsigned)(uh + wgb_ch[i]) < (unsigned)P.h && (unsigned)(uw + wgb_cw[i]) < (unsigned)P.w;
-          buf_lds16(rs_b, sb + (i * 4 + wave) * RPB * BN, ok ? ub + wgb_cb[i] : (int)0x80000000, 0);
+          buf_lds16(rs_b, sb + (i * NW + wave) * RPB * BN, ok ? ub + wgb_cb[i] : (int)0x80000000, 0);
         }
         return;
       }
 #pragma unroll
       for (int i = 0; i < NA; ++i) {  // dY rows (pixels) x Cout columns
-        const int rb = (i * 4 + wave) * RPA, row = rb + lane / CPA;
+        const int rb = (i * NW + wave) * RPA, row = rb + lane / CPA;
         const int chunk = (lane % CPA) ^ rc_swz<BM>(row);
         const int q = k0 + row, co = m0 + chunk * V;
         const T* src = (q < P.K && co < P.M) ? ga + (long)q * P.k + co : g_conv_zero;
@@ -540,7 +542,7 @@ __global__ void __launch_bounds__(256, (GL && BM >= 128 && BN >= 128) ? 2 : 1) c
       const T* t_base = gb + (long)t_img * P.h * P.w * P.c;
 #pragma unroll
       for (int i = 0; i < NB; ++i) {  // input patches: rows = output pixels, columns = (r, s, ci)
-        const int rb = (i * 4 + wave) * RPB, row = rb + lane / CPB;
+        const int rb = (i * NW + wave) * RPB, row = rb + lane / CPB;
         const int q = k0 + row;
         const T* src = g_conv_zero;
         if (P.wg_rows) {
@@ -588,11 +590,11 @@ __global__ void __launch_bounds__(256, (GL && BM >= 128 && BN >= 128) ? 2 : 1) c
         const int ww = MODE == MODE_FWD ? a_w[i] + dww : (a_w[i] >> gsh) - dww;
         const bool ok = a_ok[i] && (unsigned)hh < lim_h && (unsigned)ww < lim_w;
         const int voff = ok ? gba_base[i] + toff2 : (int)0x80000000;
-        buf_lds16(rs_a, sa + (i * 32 + wave * 8) * BK, voff, 0);
+        buf_lds16(rs_a, sa + (i * (8 * NW) + wave * 8) * BK, voff, 0);
       }
 #pragma unroll
       for (int i = 0; i < NB; ++i)
-        buf_lds16(rs_b, sb + (i * 32 + wave * 8) * BK, gbb_off[i], kb * 2);
+        buf_lds16(rs_b, sb + (i * (8 * NW) + wave * 8) * BK, gbb_off[i], kb * 2);
     } else if constexpr (G) {
       typedef __attribute__((address_space(3))) void* lds_t;
       typedef const __attribute__((address_space(1))) void* glb_t;
@@ -616,7 +618,7 @@ __global__ void __launch_bounds__(256, (GL && BM >= 128 && BN >= 128) ? 2 : 1) c
       }
 #pragma unroll
       for (int i = 0; i < NA; ++i) {
-        const int row = i * 32 + wave * 8 + (lane >> 3);
+        const int row = i * (8 * NW) + wave * 8 + (lane >> 3);
         const int chunk = gl_swz(row, lane & 7);
         int ci = ci_u + chunk * V, r = r_u, sx = s_u;
         bool okk = true;
@@ -647,15 +649,15 @@ __global__ void __launch_bounds__(256, (GL && BM >= 128 && BN >= 128) ? 2 : 1) c
           if (ok && (unsigned)hn < (unsigned)P.ho && (unsigned)wn < (unsigned)P.wo)
             src = ga + a_off[i] + ((long)hn * P.wo + wn) * P.k + ci;
         }
-        __builtin_amdgcn_global_load_lds((glb_t)src, (lds_t)(sa + (i * 32 + wave * 8) * BK), 16, 0, 0);
+        __builtin_amdgcn_global_load_lds((glb_t)src, (lds_t)(sa + (i * (8 * NW) + wave * 8) * BK), 16, 0, 0);
       }
 #pragma unroll
       for (int i = 0; i < NB; ++i) {
-        const int row = i * 32 + wave * 8 + (lane >> 3);
+        const int row = i * (8 * NW) + wave * 8 + (lane >> 3);
         const int nrow = n0 + row;
         const int kk = k0 + gl_swz(row, lane & 7) * V;
         const T* src = (nrow < P.N && kk < P.K) ? gb + (long)nrow * P.K + kk : g_conv_zero;
-        __builtin_amdgcn_global_load_lds((glb_t)src, (lds_t)(sb + (i * 32 + wave * 8) * BK), 16, 0, 0);
+        __builtin_amdgcn_global_load_lds((glb_t)src, (lds_t)(sb + (i * (8 * NW) + wave * 8) * BK), 16, 0, 0);
       }
     }
   };
@@ -667,7 +669,7 @@ __global__ void __launch_bounds__(256, (GL && BM >= 128 && BN >= 128) ? 2 : 1) c
     if (!RC) {
 #pragma unroll
       for (int i = 0; i < NA; ++i) {
-        const int id = tid + 256 * i;
+        const int id = tid + NT * i;
         if (id >= CA) break;
         const int row = id / (BK / V), kc = id % (BK / V);
         T* dst = sa + row * PA + kc * V;
@@ -679,7 +681,7 @@ __global__ void __launch_bounds__(256, (GL && BM >= 128 && BN >= 128) ? 2 : 1) c
       }
 #pragma unroll
       for (int i = 0; i < NB; ++i) {
-        const int id = tid + 256 * i;
+        const int id = tid + NT * i;
         if (id >= CB) break;
         const int row = id / (BK / V), kc = id % (BK / V);
         T* dst = sb + row * PB + kc * V;
@@ -692,14 +694,14 @@ __global__ void __launch_bounds__(256, (GL && BM >= 128 && BN >= 128) ? 2 : 1) c
     } else {
 #pragma unroll
       for (int i = 0; i < NA; ++i) {
-        const int id = tid + 256 * i;
+        const int id = tid + NT * i;
         if (id >= CA) break;
         const int kk = id / (BM / V), cc = id % (BM / V);
         *(V16*)(sa + kk * PA + cc * V) = ra[i];
       }
 #pragma unroll
       for (int i = 0; i < NB; ++i) {
-        const int id = tid + 256 * i;
+        const int id = tid + NT * i;
         if (id >= CB) break;
         const int kk = id / (BN / V), cc = id % (BN / V);
         *(V16*)(sb + kk * PB + cc * V) = rb[i];
@@ -762,22 +764,22 @@ __global__ void __launch_bounds__(256, (GL && BM >= 128 && BN >= 128) ? 2 : 1) c
       }
     }
   } else if (G && kt0 < kt1) {
-   // the pipelined one-barrier loop where it measured faster: FWD and WGRAD tiles of >= 128 x 128
-   // (the stride-1 ResNet layer2-4 convs and their weight gradients, -3 to -5 %).  Narrower
-   // tiles (64-row WGRAD of 64-channel layers, the superpixel image-conv WGRAD, 64 x 64 / 128 x 64
-   // FWD and DGRAD, the stride-2 parity phases) and DGRAD 128 x 128 keep the two-barrier loop
-   // below: there the next tile's DMA, issued before the wait for the current one, has a
-   // barrier and a DMA issue more time to land than behind one tile's few MFMAs, and that
-   // measured 5-35 % faster (profiles/r5d_conv_loop_ab.txt).
+   // LDS-DMA K loop.  The MFMA fragments are read by inline asm from per-lane bases (immediate
+   // offsets) into two register sets: K-substep ks+1's reads are in flight during ks's MFMAs
+   // behind a counted lgkmcnt.  (Left to the compiler, the schedule re-used one fragment pair per
+   // operand and waited on each read right after issuing it: the LDS latency was exposed four
+   // times per K-tile and wave.)  Two DMA schedules (profiles/r5_conv_loop_ab.txt):
+   //  1 (FWD / WGRAD tiles >= 128 x 128): an NBUF-deep ring with ONE barrier per K-tile -- the
+   //    barrier at the top of tile kt (after this wave's DMA of kt has landed) also retires every
+   //    wave's reads of tile kt-1, so tile kt+NBUF-1's DMA goes into that buffer right after it;
+   //    ResNet layer2-4 convs and weight gradients -3 to -5 %;
+   //  2 (everything else, and DGRAD 128 x 128): two barriers per K-tile, the next tile's DMA
+   //    issued before the wait for this one -- a barrier and a DMA issue more time to land than
+   //    behind one tile's few MFMAs: the ring schedule was 5-35 % slower on these tiles, this one
+   //    is 1-8 % faster than compiler-scheduled reads (layer1 weight gradients -8.5 %).
    constexpr bool PIPE = BM >= 128 && BN >= 128 && MODE != MODE_DGRAD;
-   if constexpr (G && PIPE) {
-    // Two LDS buffers, ONE barrier per K-tile: the barrier at the top of tile kt (after this
-    // wave's DMA of kt has landed) also retires every wave's reads of tile kt-1, so tile kt+1's
-    // DMA goes into that buffer right after it and lands while kt is consumed.  The MFMA
-    // fragments are read by inline asm from per-lane bases (immediate offsets) into two register
-    // sets: K-substep ks+1's reads are in flight during ks's MFMAs behind a counted lgkmcnt.
-    // (Left to the compiler, the schedule re-used one fragment pair per operand and waited on each
-    // read right after issuing it: the LDS latency exposed four times per K-tile and wave.)
+   constexpr int SCHED = PIPE ? 1 : 2;
+   if constexpr (G) {
     constexpr int NKS = BK / 32;
     constexpr int BUFB = (A_EL + B_EL) * (int)sizeof(T);
     constexpr int NRD = RC ? 2 * (FM + FN) : FM + FN;  // LDS read instructions per K-substep
@@ -858,14 +860,21 @@ __global__ void __launch_bounds__(256, (GL && BM >= 128 && BN >= 128) ? 2 : 1) c
       // orders only against other asm: the scheduler sank the MFMAs below the final wait)
       __builtin_amdgcn_sched_barrier(0);
     };
-    gl_issue(kt0, 0);
+   if constexpr (SCHED == 1) {
+    // NBUF-deep ring: tiles kt+1 .. kt+NBUF-2 stay in flight while tile kt is consumed
+#pragma unroll
+    for (int p2 = 0; p2 < NBUF - 1; ++p2)
+      if (kt0 + p2 < kt1) gl_issue(kt0 + p2, p2);
+    int buf = 0;  // buffer of tile kt
     for (int kt = kt0; kt < kt1; ++kt) {
-      const int buf = (kt - kt0) & 1;
       const uint32_t bo = buf * BUFB;
-      wait_vmcnt<0>();  // this wave's DMA of tile kt (issued one tile earlier) has landed
-      gl_barrier();     // ... every wave's; and every wave is done reading the other buffer
+      // this wave's DMA of tile kt has landed (the younger tiles' stay in flight) ...
+      if (kt + NBUF - 2 < kt1) wait_vmcnt<(NBUF - 2) * (NA + NB)>();
+      else wait_vmcnt<0>();
+      gl_barrier();  // ... every wave's; and every wave is done reading tile kt-1's buffer
       rd(bo, std::integral_constant<int, 0>(), std::integral_constant<int, 0>());
-      if (kt + 1 < kt1) gl_issue(kt + 1, buf ^ 1);
+      if (kt + NBUF - 1 < kt1) gl_issue(kt + NBUF - 1, buf == 0 ? NBUF - 1 : buf - 1);
+      buf = buf + 1 == NBUF ? 0 : buf + 1;
       sfor<NKS>([&](auto kc) {
         constexpr int K = decltype(kc)::value;
         if constexpr (K + 1 < NKS) {
@@ -877,7 +886,9 @@ __global__ void __launch_bounds__(256, (GL && BM >= 128 && BN >= 128) ? 2 : 1) c
         mm(std::integral_constant<int, K & 1>());
       });
     }
-   } else {
+   } else if constexpr (SCHED == 2) {
+    // two-barrier schedule (the next tile's DMA issued before the wait for this one) with the
+    // look-ahead fragment reads of the ring schedule
     gl_issue(kt0, 0);
     for (int kt = kt0; kt < kt1; ++kt) {
       const int buf = (kt - kt0) & 1;
@@ -888,42 +899,21 @@ __global__ void __launch_bounds__(256, (GL && BM >= 128 && BN >= 128) ? 2 : 1) c
         wait_vmcnt<0>();
       }
       gl_barrier();
-      const T* sa = smem + buf * (A_EL + B_EL);
-      const T* sb = sa + A_EL;
-#pragma unroll
-      for (int ks = 0; ks < BK / KS; ++ks) {
-        bf16x8 fa[FM], fb[FN];
-        if constexpr (RC) {
-          s16x4 ta[FM][2], tb[FN][2];
-#pragma unroll
-          for (int i = 0; i < FM; ++i) frag_rc_gl_issue<BM>((const bf16*)sa, wm0 + i * 16, ks, lane, ta[i][0], ta[i][1]);
-#pragma unroll
-          for (int j = 0; j < FN; ++j) frag_rc_gl_issue<BN>((const bf16*)sb, wn0 + j * 16, ks, lane, tb[j][0], tb[j][1]);
-          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll
-          for (int i = 0; i < FM; ++i) {
-            asm volatile("" : "+v"(ta[i][0]), "+v"(ta[i][1]));
-            fa[i] = rc_gl_frag(ta[i][0], ta[i][1]);
-          }
-#pragma unroll
-          for (int j = 0; j < FN; ++j) {
-            asm volatile("" : "+v"(tb[j][0]), "+v"(tb[j][1]));
-            fb[j] = rc_gl_frag(tb[j][0], tb[j][1]);
-          }
+      const uint32_t bo = buf * BUFB;
+      rd(bo, std::integral_constant<int, 0>(), std::integral_constant<int, 0>());
+      sfor<NKS>([&](auto kc) {
+        constexpr int K = decltype(kc)::value;
+        if constexpr (K + 1 < NKS) {
+          rd(bo, std::integral_constant<int, K + 1>(), std::integral_constant<int, (K + 1) & 1>());
+          wait_lgkmcnt<NRD>();
         } else {
-#pragma unroll
-          for (int i = 0; i < FM; ++i) fa[i] = frag_kc_gl((const bf16*)sa, wm0 + i * 16, ks, lane);
-#pragma unroll
-          for (int j = 0; j < FN; ++j) fb[j] = frag_kc_gl((const bf16*)sb, wn0 + j * 16, ks, lane);
+          wait_lgkmcnt<0>();
         }
-#pragma unroll
-        for (int i = 0; i < FM; ++i)
-#pragma unroll
-          for (int j = 0; j < FN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
-      }
+        mm(std::integral_constant<int, K & 1>());
+      });
       gl_barrier();  // every wave is done reading buf before it is refilled
     }
+   }
    }
   } else if (kt0 < kt1) {
     load_tile(kt0);
@@ -976,7 +966,7 @@ __global__ void __launch_bounds__(256, (GL && BM >= 128 && BN >= 128) ? 2 : 1) c
               for (int e = 0; e < 4; ++e) cs[(i * 16 + er + e) * CP + wn0 + j * 16 + ec] = acc[i][j][e];
         }
         __syncthreads();
-        for (int c = tid; c < WTM * CPR; c += 256) {
+        for (int c = tid; c < WTM * CPR; c += NT) {
           const int row = c / CPR, cc = c - row * CPR;
           const int gm = m0 + band * WTM + row, gn = n0 + cc * 4;
           if (gm < P.M && gn < P.N) *(f32x4*)(out + (long)gm * P.N + gn) = *(const f32x4*)(cs + row * CP + cc * 4);
@@ -1036,7 +1026,7 @@ __global__ void __launch_bounds__(256, (GL && BM >= 128 && BN >= 128) ? 2 : 1) c
         static_assert(BM * CP <= NBUF * (A_EL + B_EL), "epilogue staging fits the operand LDS");
         T* cs = smem;
         const bool post = has_res || P.accum || has_mask;
-        const bool bnb = MODE == MODE_DGRAD && P.bnb_part != nullptr;  // (host: CPR divides 256)
+        const bool bnb = MODE == MODE_DGRAD && P.bnb_part != nullptr;  // (host: CPR divides NT)
         float bg[V], bgx[V], bmu[V], bsc[V], bsh[V];
         if (bnb) {
           const int ch0 = n0 + (tid % CPR) * V;  // this thread's fixed channel chunk
@@ -1056,7 +1046,7 @@ __global__ void __launch_bounds__(256, (GL && BM >= 128 && BN >= 128) ? 2 : 1) c
         // behind it (the compiler cannot reorder them past the possibly-aliasing store).  The
         // 160-row tiles (10 chunks per thread) preload half of them (registers: 2 groups per
         // CU) and the other half as one batch after the first half's stores.
-        constexpr int NIT = (BM * CPR + 255) / 256;
+        constexpr int NIT = (BM * CPR + NT - 1) / NT;
         constexpr int NPL = NIT > 8 ? (NIT + 1) / 2 : NIT;
         constexpr int NXP = MODE == MODE_DGRAD ? NPL : 1;
         V16 xpre[NXP];
@@ -1064,7 +1054,7 @@ __global__ void __launch_bounds__(256, (GL && BM >= 128 && BN >= 128) ? 2 : 1) c
         const bool ppre_on = pmask || P.accum;
         V16 ppre[NPL];
         auto chunk_ok = [&](int it, long& o) {
-          const int c = tid + it * 256;
+          const int c = tid + it * NT;
           const int row = c / CPR, cc = c - row * CPR;
           const int gm = m0 + row, gn = n0 + cc * V;
           const bool ok = c < BM * CPR && gm < P.M && gn < P.N;
@@ -1108,7 +1098,7 @@ __global__ void __launch_bounds__(256, (GL && BM >= 128 && BN >= 128) ? 2 : 1) c
         }
         __syncthreads();
         auto process = [&](int it, const V16& pp, const V16& xr) {
-          const int c = tid + it * 256;
+          const int c = tid + it * NT;
           if (c >= BM * CPR) return;
           const int row = c / CPR, cc = c - row * CPR;
           const int gm = m0 + row, gn = n0 + cc * V;
@@ -1166,17 +1156,17 @@ __global__ void __launch_bounds__(256, (GL && BM >= 128 && BN >= 128) ? 2 : 1) c
         if (bnb) {
           // threads tid = cc + CPR * k share chunk cc: sum their partials in a fixed order
           __syncthreads();
-          float* red = (float*)smem;  // [256][2 V]
+          float* red = (float*)smem;  // [NT][2 V]
 #pragma unroll
           for (int q = 0; q < V; ++q) {
             red[tid * 2 * V + q] = bg[q];
             red[tid * 2 * V + V + q] = bgx[q];
           }
           __syncthreads();
-          for (int e = tid; e < CPR * V; e += 256) {
+          for (int e = tid; e < CPR * V; e += NT) {
             const int cc = e / V, q = e - cc * V, ch = n0 + cc * V + q;
             float a = 0.f, b = 0.f;
-            for (int t = cc; t < 256; t += CPR) {
+            for (int t = cc; t < NT; t += CPR) {
               a += red[t * 2 * V + q];
               b += red[t * 2 * V + V + q];
             }
@@ -1264,7 +1254,7 @@ __global__ void __launch_bounds__(256, (GL && BM >= 128 && BN >= 128) ? 2 : 1) c
 template <typename T, int MODE, int BM, int BN, int BK, int WM, int WN, int ALA, int ALB, int GL = 0>
 static void launch(const ConvArgs& p, int splits, hipStream_t st) {
   dim3 grid(rt_cdiv(p.M, BM), rt_cdiv(p.N, BN), MODE == MODE_DGRAD && p.nph > 1 ? p.nph : splits);
-  hipLaunchKernelGGL((conv_gemm_kernel<T, MODE, BM, BN, BK, WM, WN, ALA, ALB, GL>), grid, dim3(256), 0, st, p);
+  hipLaunchKernelGGL((conv_gemm_kernel<T, MODE, BM, BN, BK, WM, WN, ALA, ALB, GL>), grid, dim3(64 * WM * WN), 0, st, p);
 }
 
 // BK per tile: 64 where the tile is MFMA-dense (128x128, 64x64: one barrier per 64-deep
@@ -1278,8 +1268,10 @@ void launch_al(const ConvArgs& p, int cr, hipStream_t st, int splits) {
     if (cr % 32 == 0 && p.K % 8 == 0) {
       // ALA 2 (buffer-offset DMA): DGRAD only at stride 1 or in the stride-2 parity phases
       const bool gb_ok = p.gbuf && (MODE != MODE_DGRAD || (p.sh == p.sw && (p.sh == 1 || (p.sh == 2 && p.psh == 2))));
-      if (cr % 64 == 0 && gb_ok) launch<T, MODE, BM, BN, 64, WM, WN, 2, 1, 2>(p, splits, st);
-      else launch<T, MODE, BM, BN, 64, WM, WN, 1, 1, 2>(p, splits, st);
+      // 8-wave tiles (one workgroup per CU): a 3-deep LDS ring (144 KB for 256 x 128)
+      constexpr int GLV = WM * WN == 8 ? 3 : 2;
+      if (cr % 64 == 0 && gb_ok) launch<T, MODE, BM, BN, 64, WM, WN, 2, 1, GLV>(p, splits, st);
+      else launch<T, MODE, BM, BN, 64, WM, WN, 1, 1, GLV>(p, splits, st);
       return;
     }
   }

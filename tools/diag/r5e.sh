@@ -13,3 +13,8 @@ for v in base head base head; do
   RTSDS_LIB=$PWD/$lib timeout -k 10 300 python3 bench.py --no-cpu-baseline --no-conv-profile > gpurun_out/r5e_bench_$v.json 2>/dev/null || exit 1
   python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).readline()); print(sys.argv[2], d['value'], d['ms_per_step'], d.get('inference_fps_bs8'), d.get('inference_fps_bs1'))" gpurun_out/r5e_bench_$v.json $v | tee -a gpurun_out/r5e_ab.txt
 done
+# operand-bytes diagnostic (timing only, wrong results): FWD without the A / without the B DMA
+for v in librtsds_hip var_noa var_nob; do
+  echo "== $v" >> gpurun_out/r5e_bytes.txt
+  timeout -k 10 300 bash tools/conv_suite.sh $PWD/rtsds_amd/$v.so 2>/dev/null | grep fwd >> gpurun_out/r5e_bytes.txt || exit 1
+done
