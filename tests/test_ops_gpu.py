@@ -1052,8 +1052,9 @@ def test_tapconv_partial_tiles(geo):
     valid columns < 64) and heights that end inside a 4-row tile, so the edge columns / rows, the
     out-of-range buffer stores and the Chan merge of the statistics over tiles with unequal
     counts all run.  Every epilogue the networks launch, against float64 on the bf16 operands:
-    forward (plain, ReLU, BatchNorm statistics, eval BN scale / shift + residual + ReLU) and data
-    gradient (plain, accumulate, ReLU mask, BatchNorm-backward statistics)."""
+    forward (plain, ReLU, BatchNorm statistics, eval BN scale / shift + residual + ReLU), data
+    gradient (plain, accumulate, ReLU mask, BatchNorm-backward statistics) and the direct weight
+    gradient (tapwgrad_kernel: 2 x 64 tiles, per-workgroup slabs; plain and accumulating)."""
     import ctypes
     from rtsds_amd._lib import lib
     from rtsds_amd.functional import _conv_desc, _P
@@ -1132,3 +1133,15 @@ def test_tapconv_partial_tiles(geo):
     p = part.double().cpu().sum(1)
     _close(p[:, 0], gg.sum(dim=(0, 2, 3)), bf, "bnstats sum g", tol=1e-4)
     _close(p[:, 1], (gg * (aux - bmean.view(1, -1, 1, 1))).sum(dim=(0, 2, 3)), bf, "bnstats sum g(x-mean)", tol=1e-4)
+    # weight gradient (the direct kernel: per-workgroup slabs + the split reduce), plain and
+    # accumulating into an existing gradient
+    wsw = workspace(lib.rtsds_conv2d_wgrad_workspace(ctypes.byref(d)), xd.device)
+    dwr = torch.nn.grad.conv2d_weight(x, wt.shape, dy, padding=1).permute(0, 2, 3, 1)  # [k][kh][kw][c]
+    dw = torch.empty(c, 3, 3, c, device=DEV)
+    assert lib.rtsds_conv2d_wgrad(ctypes.byref(d), _P(xd), _P(dyd), _P(dw), None, 0, _P(wsw), wsw.numel(), st) == 0
+    dw0 = torch.randn(c, 3, 3, c, generator=g).to(DEV)
+    dwa = dw0.clone()
+    assert lib.rtsds_conv2d_wgrad(ctypes.byref(d), _P(xd), _P(dyd), _P(dwa), None, 1, _P(wsw), wsw.numel(), st) == 0
+    torch.cuda.synchronize()
+    _close(dw, dwr, torch.float32, "wgrad", tol=1e-4)
+    _close(dwa, dwr + dw0.double().cpu(), torch.float32, "wgrad accumulate", tol=1e-4)
