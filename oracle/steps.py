@@ -70,8 +70,8 @@ def da_step(G, D, optG, optD, ce, bce, src, lbl, tgt, lambda_, iterations):
     optG.step()
     optD.step()
     correct = int(src_feat.argmax(1).eq(lbl).sum())
-    return {"loss_gen_source": float(l_seg), "loss_adversarial": float(l_adv),
-            "loss_disc_source": float(l_ds), "loss_disc_target": float(l_dt),
+    return {"loss_gen_source": float(l_seg.detach()), "loss_adversarial": float(l_adv.detach()),
+            "loss_disc_source": float(l_ds.detach()), "loss_disc_target": float(l_dt.detach()),
             "correct": correct, "total": lbl.numel()}
 
 

@@ -604,14 +604,16 @@ __global__ void __launch_bounds__(512, 1) tapwgrad_kernel(const TapWArgs P) {
     s16x8 r = {t0[0], t0[1], t0[2], t0[3], t1[0], t1[1], t1[2], t1[3]};
     return __builtin_bit_cast(bf16x8, r);
   };
-  // MFMAs of output-channel block CB on register set S
+  // MFMAs of output-channel block CB on register set S.  The halo window is the MFMA's A operand,
+  // so a lane's accumulator holds 4 consecutive input channels of one output channel (one
+  // 16-byte store per block in the epilogue)
   auto mm = [&](auto sc, auto cbc) {
     constexpr int S = decltype(sc)::value, CB = decltype(cbc)::value;
     const bf16x8 a = frag(fa[S][CB][0], fa[S][CB][1]);
 #pragma unroll
     for (int tap = 0; tap < 9; ++tap) {
       asm volatile("" : "+v"(fb[S][tap][0]), "+v"(fb[S][tap][1]));
-      acc[CB][tap] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, frag(fb[S][tap][0], fb[S][tap][1]), acc[CB][tap], 0, 0, 0);
+      acc[CB][tap] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag(fb[S][tap][0], fb[S][tap][1]), a, acc[CB][tap], 0, 0, 0);
     }
     __builtin_amdgcn_sched_barrier(0);
   };
@@ -646,15 +648,13 @@ __global__ void __launch_bounds__(512, 1) tapwgrad_kernel(const TapWArgs P) {
       mm(IS(), I1());
     });
   }
-  // partial dW of this workgroup: acc[cb][tap][e] = dW[co0 + 16 cb + 4 g + e][tap][ci0 + (lane & 15)]
+  // partial dW of this workgroup: acc[cb][tap][e] = dW[co0 + 16 cb + (lane & 15)][tap][ci0 + 4 g + e]
   float* out = P.slab + (long)blockIdx.x * (kC * 9 * kC);
 #pragma unroll
   for (int cb = 0; cb < 2; ++cb)
 #pragma unroll
     for (int tap = 0; tap < 9; ++tap)
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-        out[((co0 + 16 * cb + 4 * g + e) * 9 + tap) * kC + ci0 + (lane & 15)] = acc[cb][tap][e];
+      *(f32x4*)(out + ((co0 + 16 * cb + (lane & 15)) * 9 + tap) * kC + ci0 + 4 * g) = acc[cb][tap];
 }
 
 // tiles of 2 x 64 output pixels; one workgroup per CU walking a contiguous run of them

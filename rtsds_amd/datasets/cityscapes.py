@@ -31,7 +31,7 @@ def read_png(path, rgb=False):
     with Image.open(path) as im:
         if rgb and im.mode != "RGB":
             im = im.convert("RGB")
-        a = np.asarray(im)
+        a = np.array(im)  # a writable copy (np.asarray of a PIL image is read-only)
     return torch.from_numpy(np.ascontiguousarray(a))
 
 
