@@ -556,9 +556,6 @@ void imgconv_fwd(const rtsds_conv_desc* d, const void* x4, const void* w, const 
 void pw_dgrad(const rtsds_conv_desc* d, const void* dy, const void* w, void* dx, int accum, hipStream_t st);
 // Register-resident-weight direct conv for 3x3 64 -> 64 stride-1 convs (tapconv.hip).
 bool tapconv_ok(const rtsds_conv_desc* d);
-bool tapwgrad_ok(const rtsds_conv_desc* d);
-int tapwgrad_splits(const rtsds_conv_desc* d);
-void tapwgrad(const rtsds_conv_desc* d, const void* x, const void* dy, float* slab, hipStream_t st);
 int tapconv_rows(const rtsds_conv_desc* d, int dgrad);
 void tapconv_fwd(const rtsds_conv_desc* d, const void* x, const void* w, const float* bias, const float* scale, const void* res,
                  void* y, int act, float* stats, hipStream_t st);
@@ -1251,8 +1248,6 @@ extern "C" size_t rtsds_conv2d_wgrad_workspace(const rtsds_conv_desc* d) {
     return w.slab_bytes + w.colsum_bytes + sp_x4_bytes(d) + al256((size_t)v.k * v.kh * v.kw * 8 * 4);
   }
   const WgradPlan w = wgrad_plan(d);
-  if (tapwgrad_ok(d))  // the direct 3x3 64 -> 64 weight gradient: one slab per workgroup
-    return al256((size_t)tapwgrad_splits(d) * d->k * d->kh * d->kw * d->c * 4) + w.colsum_bytes;
   return w.slab_bytes + w.dyp_bytes + w.xp_bytes + w.colsum_bytes;
 }
 
@@ -1353,23 +1348,12 @@ static int wgrad_impl(const rtsds_conv_desc* d0, const void* x, const void* dy, 
   }
   const bool sp = sp_path(d0);
   const rtsds_conv_desc dv = sp ? sp_desc(d0) : *d0;
-  const WgradPlan pl0 = wgrad_plan(&dv);
-  const long R = (long)d0->n * d0->ho * d0->wo;
-  // the direct 3x3 64 -> 64 weight gradient (tapconv.hip): its per-workgroup slabs go through the
-  // same split reduce (and dbias through the same column sums) as the GEMM's
-  const bool tapw = !sp && tapwgrad_ok(d0) && !x_padded;
-  WgradPlan pl = pl0;
-  if (tapw) {
-    pl.splits = tapwgrad_splits(d0);
-    pl.slab_bytes = al256((size_t)pl.splits * d0->k * d0->kh * d0->kw * d0->c * 4);
-    pl.kp = d0->k;
-    pl.cp = d0->c;
-    pl.dyp_bytes = pl.xp_bytes = 0;
-  }
+  const WgradPlan pl = wgrad_plan(&dv);
   char* slab = (char*)ws;
   char* dyp = slab + pl.slab_bytes;
   char* xp = dyp + pl.dyp_bytes;
   float* part = (float*)(xp + pl.xp_bytes);
+  const long R = (long)d0->n * d0->ho * d0->wo;
   rtsds_conv_desc d = dv;
   const void* dyk = dy;
   float* dws = nullptr;  // superpixel path: dW' [k][kh][kwp][8] before the unpack
@@ -1401,8 +1385,7 @@ static int wgrad_impl(const rtsds_conv_desc* d0, const void* x, const void* dy, 
   p.tiles_per_split = pl.tps;
   p.split_stride = (long)p.M * p.N;
   p.out = slab;
-  if (tapw) tapwgrad(d0, x, dy, (float*)slab, st);
-  else if (d.dtype == RTSDS_BF16) wgrad_launch<bf16>(p, pl.bm, pl.bn, pl.splits, st);
+  if (d.dtype == RTSDS_BF16) wgrad_launch<bf16>(p, pl.bm, pl.bn, pl.splits, st);
   else wgrad_launch<float>(p, pl.bm, pl.bn, pl.splits, st);
   if (sp) {
     const int nv = dv.k * dv.kh * dv.kw * 2;

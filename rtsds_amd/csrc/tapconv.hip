@@ -24,7 +24,6 @@
 // (GradJoin), the LeakyReLU / ReLU backward of the input's activation (mask), or the backward
 // statistics (sum g, sum g (x - mean)) of the BatchNorm + activation that produced the input.
 #include "common.h"
-#include <utility>
 
 namespace {
 constexpr int kC = 64;                    // input = output channels
@@ -466,221 +465,4 @@ void tapconv_dgrad(const rtsds_conv_desc* d, const void* dy, const void* wt, voi
   else if (mask) epi = (!accumulate && mask_act == RTSDS_ACT_RELU) ? 2 : -1;
   else epi = accumulate ? 3 : 0;
   tap_launch<1>(epi, grid, a, st);
-}
-
-// ---- weight gradient --------------------------------------------------------------------------
-// dW[co][r][s][ci] = sum_px dY[px][co] X[px + (r - 1, s - 1)][ci] for the same 3x3 64 -> 64
-// stride-1 convs.  As a split-K GEMM (M = 64 output channels, N = 9 taps x 64, K = pixels) the
-// weight gradient re-gathers every input pixel once per N tile and tap and every dY row once per
-// N tile: ~40 flop per staged byte, 46 us per layer1 conv at bs 8.  Here a workgroup walks a
-// contiguous run of 2 x 64-pixel output tiles; per tile the dY tile (128 pixels) and the
-// 4 x 66-pixel input halo are staged ONCE by LDS-DMA (double-buffered) and all 9 taps read
-// shifted windows of the halo: ~190 flop per staged byte.  Wave w owns output channels
-// 32 (w & 1) .. + 32 (two 16-row blocks) x input channels 16 (w >> 1) .. + 16 x the 9 taps: 18
-// accumulator blocks, held across the run.  Both MFMA operands are pixel-major in LDS (K =
-// pixels) and read with ds_read_b64_tr_b16 (16-B chunk c of pixel f at slot c ^ (f & 7):
-// conflict-free for every window shift); every read is an immediate offset from one of 10
-// per-lane bases (the chunk swizzle of a halo window depends only on (2 row + column) mod 8).
-// Each workgroup writes its partial dW (fp32 [64][9][64]) as one split-K slab; the weight-gradient
-// split reduce sums them in workgroup order (deterministic, no atomics).
-namespace {
-constexpr int kGTH = 2, kGTW = 64, kGHC = kGTW + 2, kGHalo = (kGTH + 2) * kGHC;  // 264 halo pixels
-constexpr int kGHIns = kGHalo / 8;                                  // 33 wave-instructions of 8 pixels
-constexpr int kGDIns = kGTH * kGTW / 8;                             // 16 (the dY tile)
-constexpr int kGInsW = (kGHIns + kGDIns + kWaves - 1) / kWaves;     // 7 per wave
-constexpr int kGStage = kGInsW * kWaves * 1024;                     // 56 KB per stage
-constexpr int kGDOff = kGHIns * 1024;                               // dY tile offset in a stage
-}  // namespace
-
-struct TapWArgs {
-  const bf16* x;   // NHWC [n][h][w][64]
-  const bf16* dy;  // NHWC [n][h][w][64]
-  float* slab;     // [gridDim.x][64][9][64] fp32 partial weight gradients
-  int n, h, w, tiles, per;
-  FastDiv f_tpi, f_tw;  // tiles per image, tile columns per row
-};
-
-RT_DEV uint32_t lds_addr_tw(const void* p) {
-  return (uint32_t)(size_t)(const __attribute__((address_space(3))) void*)p;
-}
-template <int OFF> RT_DEV void tw_rd(s16x4& d, uint32_t a) {
-  static_assert(OFF >= 0 && OFF < 65536, "ds offset");
-  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(d) : "v"(a), "i"(OFF));
-}
-template <typename F, int... I> RT_DEV void tw_for_i(F&& f, std::integer_sequence<int, I...>) {
-  (f(std::integral_constant<int, I>()), ...);
-}
-template <int N, typename F> RT_DEV void tw_for(F&& f) { tw_for_i(f, std::make_integer_sequence<int, N>()); }
-
-__global__ void __launch_bounds__(512, 1) tapwgrad_kernel(const TapWArgs P) {
-  __shared__ __attribute__((aligned(16))) unsigned char lds[2 * kGStage];
-  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int co0 = 32 * (wave & 1), ci0 = 16 * (wave >> 1);
-  int bid;
-  {  // XCD-aware bijective remap: the workgroups of one XCD take adjacent runs of tiles
-    const int nwg = gridDim.x, b = blockIdx.x;
-    const int xcd = b & 7, q = nwg >> 3, r = nwg & 7;
-    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
-  }
-  const int t0 = bid * P.per, t1 = min(P.tiles, t0 + P.per);
-  const int npix = P.n * P.h * P.w;
-  const rsrc_t rx = make_rsrc(P.x, npix * kC * 2);
-  const rsrc_t rdy = make_rsrc(P.dy, npix * kC * 2);
-  auto tile_xy = [&](int t, int& img, int& oh0, int& ow0) {
-    img = (int)fdiv((uint32_t)t, P.f_tpi);
-    const int rem = t - img * (int)P.f_tpi.d, trow = (int)fdiv((uint32_t)rem, P.f_tw);
-    oh0 = trow * kGTH;
-    ow0 = (rem - trow * (int)P.f_tw.d) * kGTW;
-  };
-  // wave-instruction ins (1 KB: 8 pixels x 128 B) of a stage: halo pixels 8 ins .. (ins < 33),
-  // then the dY tile's pixels; lane l writes slot l & 7 of pixel l >> 3 with source chunk
-  // (l & 7) ^ (pixel & 7); pixels outside the image get an offset past num_records (zeros)
-  auto issue = [&](int t, int b) {
-    int img, oh0, ow0;
-    tile_xy(t, img, oh0, ow0);
-    int lz = lane;
-    asm volatile("" : "+v"(lz));
-#pragma unroll
-    for (int u = 0; u < kGInsW; ++u) {
-      const int ins = wave + kWaves * u;
-      unsigned char* dst = lds + b * kGStage + ins * 1024;
-      if (ins < kGHIns) {
-        const int f = 8 * ins + (lz >> 3), hr = f / kGHC, hc = f - hr * kGHC;
-        const int ih = oh0 - 1 + hr, iw = ow0 - 1 + hc;
-        const bool ok = (unsigned)ih < (unsigned)P.h && (unsigned)iw < (unsigned)P.w;
-        buf_lds16(rx, dst, ok ? ((img * P.h + ih) * P.w + iw) * (kC * 2) + (((lz & 7) ^ (f & 7)) << 4) : (int)0x80000000, 0);
-      } else if (ins < kGHIns + kGDIns) {
-        const int q = 8 * (ins - kGHIns) + (lz >> 3), oh = oh0 + (q >> 6), ow = ow0 + (q & 63);
-        const bool ok = oh < P.h && ow < P.w;
-        buf_lds16(rdy, dst, ok ? ((img * P.h + oh) * P.w + ow) * (kC * 2) + (((lz & 7) ^ (q & 7)) << 4) : (int)0x80000000, 0);
-      }
-    }
-  };
-  if (t0 < t1) issue(t0, 0);
-
-  // per-lane read bases.  Lane 16 g + 4 qq + p reads pixel rows (base + 4 g + qq) and + 16,
-  // columns 4 p .. 4 p + 3 of its 16-column block: L = 4 g + qq.
-  const int g = lane >> 4, qq = (lane >> 2) & 3, p = lane & 3, L = 4 * g + qq;
-  uint32_t abase[2], bbase[8];
-#pragma unroll
-  for (int cb = 0; cb < 2; ++cb) {  // dY tile rows 32 kk + L (+ 16): (row & 7) = L & 7
-    const int col = co0 + 16 * cb + 4 * p;
-    abase[cb] = lds_addr_tw(lds) + kGDOff + L * 128 + ((((col >> 3) ^ (L & 7))) << 4) + ((col >> 2) & 1) * 8;
-  }
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {  // halo window with (2 row + column) mod 8 = j: (f & 7) = (j + L) & 7
-    const int col = ci0 + 4 * p;
-    bbase[j] = lds_addr_tw(lds) + L * 128 + ((((col >> 3) ^ ((j + L) & 7))) << 4) + ((col >> 2) & 1) * 8;
-  }
-  f32x4 acc[2][9];
-#pragma unroll
-  for (int cb = 0; cb < 2; ++cb)
-#pragma unroll
-    for (int tap = 0; tap < 9; ++tap) acc[cb][tap] = f32x4{0.f, 0.f, 0.f, 0.f};
-  s16x4 fa[2][2][2], fb[2][9][2];  // [register set][block][half]
-  // reads of K-step KK (32 pixels: tile row KK >> 1, columns 32 (KK & 1) ..) into set S, buffer
-  // offset bo; the halo window of tap (r, s) starts at pixel (row + r) * 66 + col + s
-  auto rd_a = [&](uint32_t bo, auto kkc, auto sc) {
-    constexpr int KK = decltype(kkc)::value, S = decltype(sc)::value;
-    tw_for<2>([&](auto cbc) {
-      constexpr int CB = decltype(cbc)::value;
-      tw_rd<32 * KK * 128>(fa[S][CB][0], abase[CB] + bo);
-      tw_rd<(32 * KK + 16) * 128>(fa[S][CB][1], abase[CB] + bo);
-    });
-  };
-  auto rd_b = [&](uint32_t bo, auto kkc, auto sc, auto t0c, auto t1c) {
-    constexpr int KK = decltype(kkc)::value, S = decltype(sc)::value;
-    constexpr int PR = KK >> 1, PC = 32 * (KK & 1);
-    tw_for<decltype(t1c)::value - decltype(t0c)::value>([&](auto ic) {
-      constexpr int TAP = decltype(t0c)::value + decltype(ic)::value, R = TAP / 3, SC = TAP % 3;
-      constexpr int F0 = (PR + R) * kGHC + PC + SC, J = (2 * (PR + R) + SC) & 7;
-      tw_rd<F0 * 128>(fb[S][TAP][0], bbase[J] + bo);
-      tw_rd<(F0 + 16) * 128>(fb[S][TAP][1], bbase[J] + bo);
-    });
-  };
-  auto frag = [](s16x4& t0, s16x4& t1) {
-    asm volatile("" : "+v"(t0), "+v"(t1));
-    typedef __attribute__((ext_vector_type(8))) short s16x8;
-    s16x8 r = {t0[0], t0[1], t0[2], t0[3], t1[0], t1[1], t1[2], t1[3]};
-    return __builtin_bit_cast(bf16x8, r);
-  };
-  // MFMAs of output-channel block CB on register set S.  The halo window is the MFMA's A operand,
-  // so a lane's accumulator holds 4 consecutive input channels of one output channel (one
-  // 16-byte store per block in the epilogue)
-  auto mm = [&](auto sc, auto cbc) {
-    constexpr int S = decltype(sc)::value, CB = decltype(cbc)::value;
-    const bf16x8 a = frag(fa[S][CB][0], fa[S][CB][1]);
-#pragma unroll
-    for (int tap = 0; tap < 9; ++tap) {
-      asm volatile("" : "+v"(fb[S][tap][0]), "+v"(fb[S][tap][1]));
-      acc[CB][tap] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag(fb[S][tap][0], fb[S][tap][1]), a, acc[CB][tap], 0, 0, 0);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-  };
-  using I0 = std::integral_constant<int, 0>;
-  using I1 = std::integral_constant<int, 1>;
-  for (int t = t0; t < t1; ++t) {
-    const int b = (t - t0) & 1;
-    const uint32_t bo = b * kGStage;
-    // tile t landed (this wave's DMA, then everyone's) and every wave is done reading the other
-    // buffer: refill it with tile t + 1
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    rd_a(bo, I0(), I0());
-    rd_b(bo, I0(), I0(), I0(), std::integral_constant<int, 9>());
-    if (t + 1 < t1) issue(t + 1, b ^ 1);
-    // 4 K-steps; the next step's 22 reads are issued in two halves between this step's two MFMA
-    // groups (lgkmcnt counts to 15), so each group's operands have landed behind the other's MFMAs
-    tw_for<4>([&](auto kkc) {
-      constexpr int KK = decltype(kkc)::value, S = KK & 1, N = S ^ 1;
-      using IS = std::integral_constant<int, S>;
-      using IN = std::integral_constant<int, N>;
-      using INX = std::integral_constant<int, KK + 1>;
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      if constexpr (KK + 1 < 4) {
-        rd_a(bo, INX(), IN());
-        rd_b(bo, INX(), IN(), I0(), std::integral_constant<int, 4>());
-      }
-      mm(IS(), I0());
-      if constexpr (KK + 1 < 4) rd_b(bo, INX(), IN(), std::integral_constant<int, 4>(), std::integral_constant<int, 9>());
-      mm(IS(), I1());
-    });
-  }
-  // partial dW of this workgroup: acc[cb][tap][e] = dW[co0 + 16 cb + (lane & 15)][tap][ci0 + 4 g + e]
-  float* out = P.slab + (long)blockIdx.x * (kC * 9 * kC);
-#pragma unroll
-  for (int cb = 0; cb < 2; ++cb)
-#pragma unroll
-    for (int tap = 0; tap < 9; ++tap)
-      *(f32x4*)(out + ((co0 + 16 * cb + (lane & 15)) * 9 + tap) * kC + ci0 + 4 * g) = acc[cb][tap];
-}
-
-// tiles of 2 x 64 output pixels; one workgroup per CU walking a contiguous run of them
-static int tapw_tiles(const rtsds_conv_desc* d) { return d->n * ((d->h + kGTH - 1) / kGTH) * ((d->w + kGTW - 1) / kGTW); }
-static void tapw_grid(const rtsds_conv_desc* d, int& grid, int& per) {
-  static int cus = 0;
-  if (!cus && (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0) != hipSuccess || cus < 1)) cus = 256;
-  const int tiles = tapw_tiles(d);
-  per = (tiles + cus - 1) / cus;
-  grid = (tiles + per - 1) / per;
-}
-bool tapwgrad_ok(const rtsds_conv_desc* d) { return tap_geom(d); }
-// split-K slabs of the launch (one per workgroup)
-int tapwgrad_splits(const rtsds_conv_desc* d) {
-  int grid, per;
-  tapw_grid(d, grid, per);
-  return grid;
-}
-void tapwgrad(const rtsds_conv_desc* d, const void* x, const void* dy, float* slab, hipStream_t st) {
-  TapWArgs a = {};
-  a.x = (const bf16*)x; a.dy = (const bf16*)dy; a.slab = slab; a.n = d->n; a.h = d->h; a.w = d->w;
-  a.tiles = tapw_tiles(d);
-  const int tw = (d->w + kGTW - 1) / kGTW, th = (d->h + kGTH - 1) / kGTH;
-  a.f_tpi = fastdiv_make(th * tw);
-  a.f_tw = fastdiv_make(tw);
-  int grid;
-  tapw_grid(d, grid, a.per);
-  hipLaunchKernelGGL(tapwgrad_kernel, dim3(grid), dim3(64 * kWaves), 0, st, a);
 }

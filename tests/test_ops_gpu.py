@@ -1053,8 +1053,8 @@ def test_tapconv_partial_tiles(geo):
     out-of-range buffer stores and the Chan merge of the statistics over tiles with unequal
     counts all run.  Every epilogue the networks launch, against float64 on the bf16 operands:
     forward (plain, ReLU, BatchNorm statistics, eval BN scale / shift + residual + ReLU), data
-    gradient (plain, accumulate, ReLU mask, BatchNorm-backward statistics) and the direct weight
-    gradient (tapwgrad_kernel: 2 x 64 tiles, per-workgroup slabs; plain and accumulating)."""
+    gradient (plain, accumulate, ReLU mask, BatchNorm-backward statistics), and the same convs'
+    weight gradient (split-K implicit GEMM + split reduce; plain and accumulating)."""
     import ctypes
     from rtsds_amd._lib import lib
     from rtsds_amd.functional import _conv_desc, _P
@@ -1133,8 +1133,8 @@ def test_tapconv_partial_tiles(geo):
     p = part.double().cpu().sum(1)
     _close(p[:, 0], gg.sum(dim=(0, 2, 3)), bf, "bnstats sum g", tol=1e-4)
     _close(p[:, 1], (gg * (aux - bmean.view(1, -1, 1, 1))).sum(dim=(0, 2, 3)), bf, "bnstats sum g(x-mean)", tol=1e-4)
-    # weight gradient (the direct kernel: per-workgroup slabs + the split reduce), plain and
-    # accumulating into an existing gradient
+    # weight gradient (split-K slabs + the split reduce), plain and accumulating into an
+    # existing gradient
     wsw = workspace(lib.rtsds_conv2d_wgrad_workspace(ctypes.byref(d)), xd.device)
     dwr = torch.nn.grad.conv2d_weight(x, wt.shape, dy, padding=1).permute(0, 2, 3, 1)  # [k][kh][kw][c]
     dw = torch.empty(c, 3, 3, c, device=DEV)
