@@ -177,8 +177,14 @@ def _run_geometry(g, seed):
         # only on these full-size grids)
         with torch.no_grad():
             y2 = F.conv2d(x, wp, None, _shadow(wp, torch.bfloat16), (sh, sw), (ph, pw), (dh, dw), 0)
+        # and the weight gradient (split-K slabs, K-team workgroups, the split reduce)
+        gw = wp.grad.detach().clone()
+        wp.grad = None
+        F.conv2d(x.clone().requires_grad_(True), wp, None, _shadow(wp, torch.bfloat16), (sh, sw), (ph, pw), (dh, dw),
+                 0).backward(dy)
     torch.cuda.synchronize()
     assert torch.equal(y.detach(), y2), ("non-deterministic fwd", g, int((y.detach() != y2).sum()))
+    assert torch.equal(gw, wp.grad), ("non-deterministic wgrad", g, int((gw != wp.grad).sum()))
     ho_n, wo_n = y.shape[2], y.shape[3]
     P = 384
     sel = lambda hi_, m: torch.randint(0, m, (P,), device=DEV, generator=gen)  # noqa: E731
