@@ -2,7 +2,10 @@
 reference's DataParallel step on the gathered batch -- per-replica BatchNorm statistics, but
 ONE cross-entropy mean over every rank's non-ignored pixels (reference
 utils.forModel -> nn.DataParallel, train.py:86-92).  The two shards get very different
-ignore fractions, so a mean of per-rank means would fail this test."""
+ignore fractions, so a mean of per-rank means would fail this test.  Both generators: BiSeNet
+(one backward bucket cut) and a short DeepLabV2 (ResNetMulti with [1, 1, 3, 1] Bottlenecks: the
+same three grad_cut points as the full [3, 4, 23, 3] net, so G's gradient is all-reduced in four
+buckets while the backward proceeds, runtime.grad_cut / train.py)."""
 import os
 import socket
 
@@ -32,16 +35,23 @@ def _data():
     return x, y
 
 
-def _model():
+KINDS = ("bisenet", "deeplab")
+
+
+def _model(kind="bisenet"):
     from oracle.weights import recipe_state_dict
-    from rtsds_amd.models.bisenet.build_bisenet import BiSeNet
-    net = BiSeNet(19, "resnet18")
+    if kind == "bisenet":
+        from rtsds_amd.models.bisenet.build_bisenet import BiSeNet
+        net = BiSeNet(19, "resnet18")
+    else:
+        from rtsds_amd.models.deeplabv2.deeplabv2 import Bottleneck, ResNetMulti
+        net = ResNetMulti(Bottleneck, [1, 1, 3, 1], 19)
     sd = net.state_dict()
     net.load_state_dict(recipe_state_dict({k: tuple(v.shape) for k, v in sd.items()}, 1))
     return net.to(DEV).train()
 
 
-def _worker(rank, world, port, out):
+def _worker(rank, world, port, out, kind):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
     import torch.distributed as dist
@@ -49,47 +59,57 @@ def _worker(rank, world, port, out):
     from rtsds_amd import losses, optim
     from rtsds_amd.train import seg_step
     dist.init_process_group("gloo")
+    starts = []
+    orig = optim.allreduce_start
+
+    def spy(bufs, wires=None):  # one call per gradient bucket
+        starts.append(len(bufs))
+        return orig(bufs, wires)
+    optim.allreduce_start = spy
     try:
         x, y = _data()
         xs, ys = x[2 * rank:2 * rank + 2].to(DEV), y[2 * rank:2 * rank + 2].to(DEV)
         with rtsds_amd.precision(torch.float32):
-            net = _model()
+            net = _model(kind)
             opt = optim.Adam(net.parameters(), lr=1e-4)
             loss, corr = seg_step(net, losses.CrossEntropyLoss(ignore_index=19), opt, xs, ys)
             t = torch.stack([loss.double(), corr[0].double()])
             dist.all_reduce(t)
         if rank == 0:
-            torch.save({"loss": float(t[0]), "correct": int(t[1]),
+            torch.save({"loss": float(t[0]), "correct": int(t[1]), "buckets": len(starts),
                         "params": {k: v.detach().cpu() for k, v in net.named_parameters()}}, out)
     finally:
         dist.destroy_process_group()
 
 
-def test_two_rank_seg_step_equals_gathered_batch(tmp_path):
+@pytest.mark.parametrize("kind", KINDS)
+def test_two_rank_seg_step_equals_gathered_batch(tmp_path, kind):
     out = str(tmp_path / "rank0.pt")
     ctx = mp.get_context("spawn")
     port = _port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, out)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, out, kind)) for r in range(2)]
     for p in procs:
         p.start()
     for p in procs:
         p.join(timeout=300)
         assert p.exitcode == 0
     got = torch.load(out, weights_only=True)
+    # the phased backward: a bucket per cut plus the rest (BiSeNet 1 cut, DeepLab 3)
+    assert got["buckets"] >= (2 if kind == "bisenet" else 4), got["buckets"]
 
     # single device, DataParallel semantics: each replica's forward on its own half (its own
-    # BatchNorm statistics), the three losses over the gathered outputs
+    # BatchNorm statistics), the losses (three heads / one) over the gathered outputs
     import rtsds_amd
     from rtsds_amd import functional as F
     from rtsds_amd import optim
     x, y = _data()
     with rtsds_amd.precision(torch.float32):
-        net = _model()
+        net = _model(kind)
         opt = optim.Adam(net.parameters(), lr=1e-4)
         opt.zero_grad()
         halves = [net.forward_lowres(x[i:i + 2].to(DEV)) for i in (0, 2)]
         heads = [torch.cat([halves[0][h][0], halves[1][h][0]]).contiguous(memory_format=torch.channels_last)
-                 for h in range(3)]
+                 for h in range(len(halves[0]))]
         correct = torch.zeros(1, dtype=torch.int64, device=DEV)
         loss = F.upsample_cross_entropy(heads, y.to(DEV), halves[0][0][1], 19, correct)
         loss.backward()
@@ -123,17 +143,17 @@ def _da_data():
 SHARDS = ((0, 2), (2, 5))
 
 
-def _models():
+def _models(kind="bisenet"):
     from oracle.weights import recipe_state_dict
     from rtsds_amd.models.domain_shift.adversarial.model import TinyDomainDiscriminator
-    g = _model()
+    g = _model(kind)
     d = TinyDomainDiscriminator(19)
     sd = d.state_dict()
     d.load_state_dict(recipe_state_dict({k: tuple(v.shape) for k, v in sd.items()}, 2))
     return g, d.to(DEV).train()
 
 
-def _da_worker(rank, world, port, out):
+def _da_worker(rank, world, port, out, kind):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
     import torch.distributed as dist
@@ -145,7 +165,7 @@ def _da_worker(rank, world, port, out):
         x, y, xt = _da_data()
         lo, hi = SHARDS[rank]
         with rtsds_amd.precision(torch.float32):
-            g, d = _models()
+            g, d = _models(kind)
             og = optim.Adam(g.parameters(), lr=1e-4)
             od = optim.Adam(d.parameters(), lr=1e-4, weight_decay=1e-4)
             res = da_step(g, d, og, od, losses.CrossEntropyLoss(ignore_index=19), losses.BCEWithLogitsLoss(),
@@ -286,7 +306,7 @@ def _gathered_da_step(g, d, og, od, x, y, xt, lam, it):
     correct = torch.zeros(1, dtype=torch.int64, device=DEV)
     parts = [g.forward_lowres(x[lo:hi]) for lo, hi in SHARDS]
     geo = parts[0][0][1]
-    heads = [cat([p[h][0] for p in parts]) for h in range(3)]
+    heads = [cat([p[h][0] for p in parts]) for h in range(len(parts[0]))]
     loss_seg = F.upsample_cross_entropy(heads, y, geo, 19, correct) / it
     loss_seg.backward()
     src = F.interpolate_geometry(heads[0].detach(), geo)
@@ -310,7 +330,8 @@ def _gathered_da_step(g, d, og, od, x, y, xt, lam, it):
     return [float(v) for v in (loss_seg, loss_adv, loss_ds, loss_dt)] + [int(correct)]
 
 
-def test_two_rank_da_step_equals_gathered_batch(tmp_path):
+@pytest.mark.parametrize("kind", KINDS)
+def test_two_rank_da_step_equals_gathered_batch(tmp_path, kind):
     """A sharded adversarial_train iteration (2 ranks, UNEQUAL shards of 2 and 3 source +
     target images) equals the DataParallel iteration on the gathered batch: the four losses,
     the pixel-accuracy count, and G and D after both Adam steps (D gradients summed over
@@ -318,7 +339,7 @@ def test_two_rank_da_step_equals_gathered_batch(tmp_path):
     out = str(tmp_path / "rank0_da.pt")
     ctx = mp.get_context("spawn")
     port = _port()
-    procs = [ctx.Process(target=_da_worker, args=(r, 2, port, out)) for r in range(2)]
+    procs = [ctx.Process(target=_da_worker, args=(r, 2, port, out, kind)) for r in range(2)]
     for p in procs:
         p.start()
     for p in procs:
@@ -330,7 +351,7 @@ def test_two_rank_da_step_equals_gathered_batch(tmp_path):
     from rtsds_amd import optim
     x, y, xt = _da_data()
     with rtsds_amd.precision(torch.float32):
-        g, d = _models()
+        g, d = _models(kind)
         og = optim.Adam(g.parameters(), lr=1e-4)
         od = optim.Adam(d.parameters(), lr=1e-4, weight_decay=1e-4)
         want = _gathered_da_step(g, d, og, od, x.to(DEV), y.to(DEV), xt.to(DEV), 0.1, 2)
