@@ -1,0 +1,10 @@
+#!/bin/bash
+# round-5 (end of session) evidence, part A: GPU suite, smoke, default bench line, BiSeNet train + inference profiles
+set -e
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+timeout -k 10 900 python -u -m pytest tests -m gpu -q -x --timeout 300 --timeout-method thread > gpurun_out/r5z_gpu_pytest.log 2>&1
+timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r5z_smoke.txt 2>&1
+timeout -k 10 300 python3 -u bench.py > gpurun_out/r5z_bench_default.json 2> gpurun_out/r5z_bench_default.err
+bash tools/profile_all.sh r5z bisenet-seg
+bash tools/profile_infer.sh r5z
+echo ok
