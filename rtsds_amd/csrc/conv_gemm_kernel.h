@@ -811,13 +811,8 @@ conv_gemm_kernel(const ConvArgs P0) {
     bf16x8 fa[2][FM], fb[2][FN];
     s16x4 ta[2][FM][2], tb[2][FN][2];
     // issue the reads of K-substep K into register set S; bo: byte offset of the tile's buffer
-    // a wave whose whole sub-tile lies past the GEMM's M or N edge (the weight gradients of the
-    // 19-class convs: Cout = 19 in a 64-row tile) skips its fragment reads and MFMAs; it still
-    // stages its share of the tiles and takes part in every barrier
-    const bool wact = m0 + wm0 < P.M && n0 + wn0 < P.N;
     auto rd = [&](uint32_t bo, auto kc, auto sc) {
       constexpr int K = decltype(kc)::value, S = decltype(sc)::value;
-      if (!wact) return;
       if constexpr (!RC) {
         const uint32_t a = ka[K] + bo, b = kb[K] + bo;
         sfor<FM>([&](auto ic) { lds_rd128<decltype(ic)::value * 2048>(fa[S][decltype(ic)::value], a); });
@@ -838,7 +833,6 @@ conv_gemm_kernel(const ConvArgs P0) {
     // the MFMAs of register set S (its reads waited for by the caller)
     auto mm = [&](auto sc) {
       constexpr int S = decltype(sc)::value;
-      if (!wact) return;
       bf16x8 xa[FM], xb[FN];
       if constexpr (!RC) {
 #pragma unroll
