@@ -1194,6 +1194,60 @@ __global__ void bilinear_bwd_h_tab_kernel(const float* __restrict__ tmp, T* __re
     dx[i] = from_f<T>(acc);
   }
 }
+// Both passes in one kernel for 16-B channel vectors: a thread owns V channels of one input
+// pixel and forms each output row's W-pass sum t (the W kernel's taps, order and zero skipping,
+// fp32) right before the H-pass FMA that consumes it -- the same two fp32 FMA chains, so dx is
+// bit-identical to the two-pass kernels, without the fp32 [ho][wi] intermediate's write and
+// re-read.  Neighbouring input pixels re-read dY rows through L2 (XCD-aware block order).
+template <typename T>
+__global__ void __launch_bounds__(256) bilinear_bwd_fused_vec_kernel(const T* __restrict__ dy, T* __restrict__ dx, int hi, int wi,
+                                                                     int c, int ho, int wo, float sh, float sw, int dyld, int dyoff,
+                                                                     int maxh, int maxw, long total, FastDiv f_cv, FastDiv f_wi,
+                                                                     FastDiv f_hi) {
+  extern __shared__ float tab[];
+  float* wtab = tab;
+  int* wlo = (int*)(wtab + wi * maxw);
+  float* htab = (float*)(wlo + wi);
+  int* hlo = (int*)(htab + hi * maxh);
+  bil_table_build(wtab, wlo, wi, wo, sw, maxw);
+  bil_table_build(htab, hlo, hi, ho, sh, maxh);
+  typedef typename VecT<T>::v16 V16;
+  constexpr int V = VecT<T>::N;
+  const int cv = c / V;
+  GRID_STRIDE_XCD(i, total) {  // total < 2^31 (host)
+    const uint32_t q = fdiv((uint32_t)i, f_cv), r = fdiv(q, f_wi);
+    const int ch = ((int)((uint32_t)i - q * cv)) * V, iw = (int)(q - r * wi);
+    const uint32_t img = fdiv(r, f_hi);
+    const int ih = (int)(r - img * hi);
+    const float* wx = wtab + iw * maxw;
+    const float* wy = htab + ih * maxh;
+    const T* base = dy + ((long)img * ho + hlo[ih]) * wo * dyld + (long)wlo[iw] * dyld + dyoff + ch;
+    float acc[V];
+#pragma unroll
+    for (int e = 0; e < V; ++e) acc[e] = 0.f;
+    for (int k = 0; k < maxh; ++k) {
+      const float yk = wy[k];
+      if (yk == 0.f) continue;
+      const T* row = base + (long)k * wo * dyld;
+      float t[V];
+#pragma unroll
+      for (int e = 0; e < V; ++e) t[e] = 0.f;
+      for (int j = 0; j < maxw; ++j) {
+        const float xj = wx[j];
+        if (xj == 0.f) continue;
+        const V16 v = *(const V16*)(row + (long)j * dyld);
+#pragma unroll
+        for (int e = 0; e < V; ++e) t[e] = fmaf(xj, to_f(v[e]), t[e]);
+      }
+#pragma unroll
+      for (int e = 0; e < V; ++e) acc[e] = fmaf(yk, t[e], acc[e]);
+    }
+    V16 o;
+#pragma unroll
+    for (int e = 0; e < V; ++e) o[e] = from_f<T>(acc[e]);
+    *(V16*)(dx + (((long)img * hi + ih) * wi + iw) * c + ch) = o;
+  }
+}
 // most outputs any input index of an axis receives from (bil_wsum_range, host float math)
 static int bil_maxw(int in, int out, float s) {
   int m = 0;
@@ -1215,6 +1269,14 @@ static void bilinear_bwd_launch(const T* dy, float* tmp, T* dx, int n, int hi, i
   const long tw = (long)n * ho * wi * c, th = (long)n * hi * wi * c;
   const int mw = bil_maxw(wi, wo, sw), mh = bil_maxw(hi, ho, sh);
   const size_t bw = bil_tab_bytes(wi, mw), bh = bil_tab_bytes(hi, mh);
+  constexpr int V = VecT<T>::N;
+  if (c % V == 0 && dyld % V == 0 && dyoff % V == 0 && th < (1L << 31) && bw + bh <= (size_t)kBilTabLds &&
+      (long)n * ho * wo * dyld < (1L << 40)) {
+    const long tv = th / V;
+    hipLaunchKernelGGL(bilinear_bwd_fused_vec_kernel<T>, dim3(ew_blocks(tv)), dim3(256), bw + bh, st, dy, dx, hi, wi, c, ho, wo, sh,
+                       sw, dyld, dyoff, mh, mw, tv, fastdiv_make(c / V), fastdiv_make(wi), fastdiv_make(hi));
+    return;
+  }
   if (tw < (1L << 31) && bw <= (size_t)kBilTabLds)
     hipLaunchKernelGGL(bilinear_bwd_w_tab_kernel<T>, dim3(ew_blocks(tw)), dim3(256), bw, st, dy, tmp, n, wi, c, ho, wo, sw, dyld,
                        dyoff, mw, fastdiv_make(c), fastdiv_make(wi));

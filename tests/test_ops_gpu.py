@@ -352,6 +352,43 @@ def test_bilinear(geo, dt):
 
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("geo", [(16, 32, 64, 128, 64), (32, 64, 64, 128, 256), (13, 17, 97, 129, 16), (8, 8, 8, 8, 8)])
+def test_bilinear_bwd_fused_bit_identical(geo, dt):
+    """The one-pass vector backward (bilinear_bwd_fused_vec_kernel: channel counts, dY pitch and
+    offset multiples of 16 B) equals the two-pass W / H kernels bit for bit: the same dY read
+    through a row pitch of c + 1 (not a vector multiple) takes the two-pass route.  And both
+    match torch fp64."""
+    import ctypes
+    from rtsds_amd._lib import lib
+    from rtsds_amd.functional import _P, dcode
+    from rtsds_amd.runtime import workspace
+    hi, wi, ho, wo, c = geo
+    n = 2
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn(n, c, hi, wi, generator=g, dtype=torch.float64)
+    gy = torch.randn(n, c, ho, wo, generator=g, dtype=torch.float64)
+    if dt == torch.bfloat16:
+        gy = gy.bfloat16().double()
+    xr = x.clone().requires_grad_()
+    TF.interpolate(xr, size=(ho, wo), mode="bilinear").backward(gy)
+    geo_t = F.upsample_geometry(_dev(x, dt), size=(ho, wo))
+    sh, sw = geo_t[2], geo_t[3]
+    dy = gy.permute(0, 2, 3, 1).contiguous().to(DEV, dt)                      # pitch c
+    dyp = torch.zeros(n, ho, wo, c + 1, dtype=dt, device=DEV)
+    dyp[..., :c] = dy                                                         # pitch c + 1
+    ws = workspace(lib.rtsds_bilinear_bwd_workspace(n, hi, wi, c, ho, wo), dy.device)
+    st = torch.cuda.current_stream().cuda_stream
+    outs = []
+    for src, ld in ((dy, c), (dyp, c + 1)):
+        dx = torch.empty(n, hi, wi, c, dtype=dt, device=DEV)
+        assert lib.rtsds_bilinear_bwd(_P(src), _P(dx), n, hi, wi, c, ho, wo, sh, sw, ld, 0, dcode(dy), _P(ws), ws.numel(), st) == 0
+        outs.append(dx)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1]), int((outs[0] != outs[1]).sum())
+    _close(outs[0].permute(0, 3, 1, 2), xr.grad, dt, "dx", 1e-5 if dt == torch.float32 else 2e-2)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("geo", [((8, 16), None, 8), ((13, 17), (97, 129), None), ((64, 128), (512, 1024), None),
                                  ((9, 9), (9, 9), None), ((7, 5), (20, 31), None)])
 def test_bilinear_narrow_channels(geo, dt):
