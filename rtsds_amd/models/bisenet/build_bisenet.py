@@ -171,7 +171,7 @@ class BiSeNet(torch.nn.Module):
             side = branch_stream(x.device)
             box = []
 
-            def fork():  # after the context path's layer2: beside its narrow late layers
+            def fork():  # after the context path's layer1 (_ContextPath.fork_after): beside its later layers
                 side.wait_stream(main)
                 x.record_stream(side)  # read (and saved for backward) on the branch stream
                 with torch.cuda.stream(side):

@@ -120,14 +120,21 @@ class _ContextPath(nn.Module):
         self.layer1, self.layer2 = trunk.layer1, trunk.layer2
         self.layer3, self.layer4 = trunk.layer3, trunk.layer4
 
+    # where ``mid`` runs: after the stem (0), layer1 (1) or layer2 (2)
+    fork_after = 1  # bs-8 train step: 1 vs 2 +0.5 % (profiles/r5ae_fork_point_ab.txt)
+
     def forward(self, x, mid=None, tail_join=None):
         """x: NHWC compute-dtype batch -> (1/16 features, 1/32 features, GAP(1/32)).  ``mid``:
-        called after layer2 (BiSeNet forks its spatial path there, beside the narrow late
-        layers).  ``tail_join``: GradJoin of the 1/32 features' readers (the GAP here and the
-        caller's attention scale)."""
+        called after stage ``fork_after`` (BiSeNet forks its spatial path there).  ``tail_join``:
+        GradJoin of the 1/32 features' readers (the GAP here and the caller's attention scale)."""
+        if mid is not None and self.fork_after < 0:
+            mid()
         t = conv_bn_relu_maxpool(self.conv1, self.bn1, self.maxpool1, x)
-        t = self.layer2(self.layer1(t))
-        if mid is not None:
+        for i, layer in enumerate((self.layer1, self.layer2)):
+            if mid is not None and self.fork_after == i:
+                mid()
+            t = layer(t)
+        if mid is not None and self.fork_after >= 2:
             mid()
         f3 = grad_cut(self.layer3(t))  # data-parallel two-phase backward (runtime.grad_cut)
         f4 = self.layer4(f3)
