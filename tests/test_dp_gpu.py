@@ -114,7 +114,8 @@ def test_two_rank_seg_step_equals_gathered_batch(tmp_path, kind):
         loss = F.upsample_cross_entropy(heads, y.to(DEV), halves[0][0][1], 19, correct)
         loss.backward()
         opt.step()
-    assert abs(got["loss"] - float(loss)) <= 1e-5 * abs(float(loss)), (got["loss"], float(loss))
+    lv = float(loss.detach())
+    assert abs(got["loss"] - lv) <= 1e-5 * abs(lv), (got["loss"], lv)
     assert got["correct"] == int(correct)
     lr, n, bad, worst = 1e-4, 0, 0, 0.0
     for k, p in net.named_parameters():
