@@ -1213,7 +1213,9 @@ static WgradPlan wgrad_plan(const rtsds_conv_desc* d) {
   const int M = w.kp, N = d->kh * d->kw * w.cp;
   const long R = (long)d->n * d->ho * d->wo;
   const int BK = b16 ? 64 : 16;
-  w.bm = b16 ? (M <= 64 ? 64 : 128) : 64;
+  // Cout <= 32 (the 19-class convs, padded to 32): a 32-row tile (register-staged) instead of
+  // half a 64-row one
+  w.bm = b16 ? (M <= 32 && N > 64 ? 32 : (M <= 64 ? 64 : 128)) : 64;
   w.bn = b16 ? (N <= 64 ? 64 : 128) : 64;
   const long tiles = (long)rt_cdiv(M, w.bm) * rt_cdiv(N, w.bn);
   const long nk = (R + BK - 1) / BK;
@@ -1223,8 +1225,8 @@ static WgradPlan wgrad_plan(const rtsds_conv_desc* d) {
   // tiles x 3) take ~2 full rounds of splits instead when every split keeps >= 64 K-tiles
   // (373 -> 325 us); short reductions (BiSeNet layer4, 64 K-tiles) would pay it in slab traffic.
 static constexpr auto kWgradWant = 512;
-  long want = std::max<long>(1, (w.bm == 64 && M <= 32 ? 1536 : kWgradWant) / tiles);
-  if (!(w.bm == 64 && M <= 32) && tiles >= 64 && tiles * want < 480) {
+  long want = std::max<long>(1, (w.bm <= 64 && M <= 32 ? 1536 : kWgradWant) / tiles);
+  if (!(w.bm <= 64 && M <= 32) && tiles >= 64 && tiles * want < 480) {
     const long w2 = 1024 / tiles;
     if (tiles * w2 >= 922 && nk / w2 >= 64) want = w2;
   }

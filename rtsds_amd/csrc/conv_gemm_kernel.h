@@ -83,8 +83,10 @@ RT_DEV bf16x8 frag_kc_gl(const bf16* s, int row0, int ks, int lane) {
 // GL image of the RC (WGRAD) tiles: [64 pixel rows][COLS] bf16, unpadded, 16-B chunk c of row r
 // at physical chunk c ^ rc_swz(r).  The transposed fragment read (ds_read_b64_tr_b16: 8 rows
 // x 32 B per 32-lane group) then touches 16 distinct chunks = all 64 banks for 256-B rows.
+// 64-B rows (32 columns: the 19-class weight gradients' Cout): rows r and r + 4 share banks, so
+// rows 4-7 of every 8 take the other 32-B half of their row.
 template <int COLS> RT_DEV int rc_swz(int row) {
-  return COLS >= 128 ? (row & 7) << 1 : ((row >> 1) & 3) << 1;
+  return COLS >= 128 ? (row & 7) << 1 : COLS == 32 ? ((row >> 2) & 1) << 1 : ((row >> 1) & 3) << 1;
 }
 // Issued as inline asm: hipcc cannot tell the transposed-read builtin apart from the LDS-DMA
 // writes still in flight and would drain vmcnt(0) before every K-step's first read (losing the
@@ -170,7 +172,7 @@ conv_gemm_kernel(const ConvArgs P0) {
   constexpr bool RC = (MODE == MODE_WGRAD);
   constexpr bool G = GL != 0;
   static_assert(!G || (sizeof(T) == 2 && BK == 64 && ALA >= 1 && ALB == 1 && BM % 32 == 0 && BN % 32 == 0 &&
-                       (MODE != MODE_WGRAD || (BM >= 64 && BN >= 64))), "GL staging");
+                       (MODE != MODE_WGRAD || (BM >= 32 && BN >= 64))), "GL staging");
   constexpr int KCP = G ? BK : KCPitch<T, BK>::v;
   constexpr int PA = RC ? (G ? BM : RCPitch<BM>::v) : KCP;
   constexpr int PB = RC ? (G ? BN : RCPitch<BN>::v) : KCP;
@@ -1301,7 +1303,8 @@ void wgrad_launch(const ConvArgs& p, int bm, int bn, int splits, hipStream_t st)
   constexpr int BK = sizeof(T) == 2 ? 64 : 16;
   if constexpr (sizeof(T) == 2) {
     // LDS-DMA staging (swizzled RC images)
-    if (bm == 64 && bn == 64) launch<T, MODE_WGRAD, 64, 64, BK, 2, 2, 1, 1, 2>(p, splits, st);
+    if (bm == 32) launch<T, MODE_WGRAD, 32, 128, BK, 1, 4, 1, 1, 2>(p, splits, st);
+    else if (bm == 64 && bn == 64) launch<T, MODE_WGRAD, 64, 64, BK, 2, 2, 1, 1, 2>(p, splits, st);
     else if (bm == 64) launch<T, MODE_WGRAD, 64, 128, BK, 2, 2, 1, 1, 2>(p, splits, st);
     else if (bn == 64) launch<T, MODE_WGRAD, 128, 64, BK, 2, 2, 1, 1, 2>(p, splits, st);
     else launch<T, MODE_WGRAD, 128, 128, BK, 2, 2, 1, 1, 2>(p, splits, st);
