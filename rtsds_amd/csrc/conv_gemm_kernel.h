@@ -506,6 +506,20 @@ conv_gemm_kernel(const ConvArgs P0) {
     }
   };
 
+  // GB: (channel chunk, tap row, tap column) of the next K-tile gl_issue stages.  K-tiles are
+  // staged strictly in order, so the decomposition advances by one per call instead of costing
+  // three scalar integer divisions (~100 SALU instructions) per K-tile.
+  unsigned gw_q = 0, gw_tap = 0, gw_ntap = 1;
+  int gw_rr = 0, gw_cc = 0, gw_tkw = 1;
+  if constexpr (GB) {
+    gw_ntap = (unsigned)(P.K / (MODE == MODE_FWD ? P.c : P.k));
+    gw_tkw = MODE == MODE_FWD ? P.kw : P.tkw;
+    gw_q = (unsigned)kt0 / gw_ntap;
+    gw_tap = (unsigned)kt0 - gw_q * gw_ntap;
+    gw_rr = (int)gw_tap / gw_tkw;
+    gw_cc = (int)gw_tap - gw_rr * gw_tkw;
+  }
+
   // ---- GL: global -> LDS DMA of K-tile kt into buffer buf (NA + NB instructions per thread)
   auto gl_issue = [&](int kt, int buf) {
     if constexpr (G && RC) {
@@ -569,18 +583,20 @@ conv_gemm_kernel(const ConvArgs P0) {
       // taps instead of being re-fetched from MALL/HBM once per tap (the channel-major order
       // streams the whole Cin between two taps: 16 MB per XCD for the 1024-channel FFM conv).
       const int Cr = (MODE == MODE_FWD) ? P.c : P.k;
-      const unsigned ntap = (unsigned)(P.K / Cr);
-      const unsigned q = (unsigned)kt / ntap;
-      const int tap = (int)((unsigned)kt - q * ntap), ci = (int)q * BK;
+      (void)kt;  // == the walker's K-tile: q * ntap + tap
+      const int tap = (int)gw_tap, ci = (int)gw_q * BK;
       const int kb = tap * Cr + ci;  // B column of this K-tile
-      int r, sx;
-      if (MODE == MODE_FWD) {
-        r = tap / P.kw;
-        sx = tap - r * P.kw;
-      } else {
-        const int rr = tap / P.tkw;
-        r = P.r0h + rr * P.rstep;
-        sx = P.r0w + (tap - rr * P.tkw) * P.rstep;
+      const int r = MODE == MODE_FWD ? gw_rr : P.r0h + gw_rr * P.rstep;
+      const int sx = MODE == MODE_FWD ? gw_cc : P.r0w + gw_cc * P.rstep;
+      if (++gw_cc == gw_tkw) {
+        gw_cc = 0;
+        ++gw_rr;
+      }
+      if (++gw_tap == gw_ntap) {
+        gw_tap = 0;
+        gw_rr = 0;
+        gw_cc = 0;
+        ++gw_q;
       }
       const int dhh = (r * P.dh) >> gsh, dww = (sx * P.dw) >> gsh;
       const int toff = MODE == MODE_FWD ? (dhh * P.w + dww) * P.c + ci : ci - (dhh * P.wo + dww) * P.k;
