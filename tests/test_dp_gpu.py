@@ -328,7 +328,7 @@ def _gathered_da_step(g, d, og, od, x, y, xt, lam, it):
     loss_dt.backward()
     og.step()
     od.step()
-    return [float(v) for v in (loss_seg, loss_adv, loss_ds, loss_dt)] + [int(correct)]
+    return [float(v.detach()) for v in (loss_seg, loss_adv, loss_ds, loss_dt)] + [int(correct)]
 
 
 @pytest.mark.parametrize("kind", KINDS)
