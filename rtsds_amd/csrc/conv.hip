@@ -543,6 +543,9 @@ int hconv_tiles(const rtsds_conv_desc* d);
 void hconv_fwd(const rtsds_conv_desc* d, const void* x, const void* w, const float* bias, const float* scale, const void* res, void* y,
                int act, float* stats, hipStream_t st);
 bool hconv_dgrad_ok(const rtsds_conv_desc* d);
+bool nwgrad_ok(const rtsds_conv_desc* d);
+int nwgrad_splits(const rtsds_conv_desc* d);
+void nwgrad(const rtsds_conv_desc* d, const void* x, const void* dyp, float* slab, hipStream_t st);
 void hconv_dgrad(const rtsds_conv_desc* d, const void* dyp, int kp, const void* wt, void* dx, int accumulate, hipStream_t st);
 bool pw_ok(const rtsds_conv_desc* d);
 // Direct MFMA conv for the 3-channel stride-2 image convs (imgconv.hip).
@@ -1205,6 +1208,9 @@ struct WgradPlan {
   int kp, cp, bm, bn, splits, tps;
   size_t slab_bytes, dyp_bytes, xp_bytes, colsum_bytes;
 };
+// the halo-direct weight gradient of a narrow-output 3x3 conv (hconv.hip nwgrad): dY padded to 32
+// channels, one slab per run of tiles, the same split reduce
+static bool nw_path(const rtsds_conv_desc* d) { return pad_c(d->k, d->dtype) == 32 && nwgrad_ok(d); }
 static WgradPlan wgrad_plan(const rtsds_conv_desc* d) {
   WgradPlan w;
   const bool b16 = d->dtype == RTSDS_BF16;
@@ -1212,6 +1218,16 @@ static WgradPlan wgrad_plan(const rtsds_conv_desc* d) {
   w.cp = pad_c(d->c, d->dtype);
   const int M = w.kp, N = d->kh * d->kw * w.cp;
   const long R = (long)d->n * d->ho * d->wo;
+  if (nw_path(d)) {
+    w.bm = w.bn = 0;
+    w.splits = nwgrad_splits(d);
+    w.tps = 0;
+    w.slab_bytes = al256((size_t)w.splits * M * N * 4);
+    w.dyp_bytes = w.kp != d->k ? al256((size_t)R * w.kp * 2) : 0;
+    w.xp_bytes = 0;
+    w.colsum_bytes = al256((size_t)kColsumRB * d->k * 4);
+    return w;
+  }
   const int BK = b16 ? 64 : 16;
   // Cout <= 32 (the 19-class convs, padded to 32): a 32-row tile (register-staged) instead of
   // half a 64-row one
@@ -1387,7 +1403,11 @@ static int wgrad_impl(const rtsds_conv_desc* d0, const void* x, const void* dy, 
   p.tiles_per_split = pl.tps;
   p.split_stride = (long)p.M * p.N;
   p.out = slab;
-  if (d.dtype == RTSDS_BF16) wgrad_launch<bf16>(p, pl.bm, pl.bn, pl.splits, st);
+  if (!sp && nw_path(d0)) {  // (dyk: 32-channel pitch; the slab rows co >= k stay unwritten)
+    rtsds_conv_desc dn = d;
+    dn.k = d0->k;
+    nwgrad(&dn, x, dyk, (float*)slab, st);
+  } else if (d.dtype == RTSDS_BF16) wgrad_launch<bf16>(p, pl.bm, pl.bn, pl.splits, st);
   else wgrad_launch<float>(p, pl.bm, pl.bn, pl.splits, st);
   if (sp) {
     const int nv = dv.k * dv.kh * dv.kw * 2;

@@ -18,6 +18,7 @@
 // per-tile partial statistics (count, mean, M2 -- the exact two-pass form, as the GEMM
 // epilogue), scalar bf16 stores of the Cout valid channels.
 #include "common.h"
+#include <utility>
 
 namespace {
 // A tile is 256 output pixels: 4 rows x 64 columns, or 8 x 32 for 32-wide maps (ResNet layer4
@@ -271,6 +272,189 @@ __global__ void __launch_bounds__(256, 1) hconv_fwd_kernel(const HconvArgs P) {
   }
 }
 
+// ---- weight gradient of the narrow-output conv ------------------------------------------------
+// dW[co][r][s][ci] = sum_px dY[px][co] X[px + (r - 1, s - 1)][ci] for Cout <= 32 (dY channel-padded
+// to 32), Cin a multiple of 128.  As a split-K GEMM (M = 32 rows of Cout, N = 9 taps x Cin,
+// K = pixels) every input pixel is re-gathered once per tap: 1.2 GB of LDS-DMA for the FFM conv's
+// 19 x 9216 weights at bs 8, 121 us.  Here a workgroup owns 128 input channels (blockIdx.y) and
+// walks a contiguous run of 2 x 64-pixel output tiles (blockIdx.x); per tile the 4 x 66-pixel
+// input halo (its 128 channels) and the dY tile (128 pixels x 32 channels) are staged ONCE by
+// LDS-DMA (double-buffered) and all 9 taps read shifted windows of the halo.  Wave w owns input
+// channels 16 w .. + 16 x both 16-row blocks of Cout x the 9 taps: 18 accumulator blocks, held
+// across the run.  Both MFMA operands are pixel-major in LDS (K = pixels) and read with
+// ds_read_b64_tr_b16 (lane 16 g + 4 q + p reads pixel 4 g + q, channels 4 p .. 4 p + 3 of its
+// 16-channel block); 16-B chunk c of halo pixel f sits at slot c ^ 2 (f & 7) (256-B rows: the
+// 8 pixels of a 32-lane group cover all 64 banks for every tap shift), chunk c of dY pixel q at
+// c ^ 2 ((q >> 2) & 1) (64-B rows: pixels q and q + 4 take different halves).  Every read is an
+// immediate offset from one of 10 per-lane bases (the halo swizzle of a window depends only on
+// (2 row + column) mod 8).  Each workgroup writes its partial dW rows co < Cout as one split-K
+// slab [32][9][Cin]; the weight-gradient split reduce sums them in split order (deterministic).
+namespace {
+constexpr int kNwTH = 2, kNwTW = 64, kNwHC = kNwTW + 2, kNwHalo = (kNwTH + 2) * kNwHC;  // 264 halo pixels
+constexpr int kNwCI = 128, kNwWaves = 8;
+constexpr int kNwHIns = kNwHalo * kNwCI * 2 / 1024;                   // 66 wave-instructions (4 pixels each)
+constexpr int kNwDIns = kNwTH * kNwTW * 64 / 1024;                    // 8 (the dY tile, 16 pixels each)
+constexpr int kNwInsW = (kNwHIns + kNwDIns + kNwWaves - 1) / kNwWaves;  // 10 per wave
+constexpr int kNwStage = (kNwHIns + kNwDIns) * 1024;                  // 74 KB per stage
+constexpr int kNwDOff = kNwHIns * 1024;                               // dY tile offset in a stage
+}  // namespace
+
+struct NwArgs {
+  const bf16* x;   // NHWC [n][h][w][c]
+  const bf16* dy;  // NHWC [n][h][w][32]
+  float* slab;     // [gridDim.x][32][9][c] fp32 partial weight gradients (rows co < k written)
+  int n, h, w, c, k, tiles, per;
+  FastDiv f_tpi, f_tw;  // tiles per image, tile columns per row
+};
+
+RT_DEV uint32_t nw_lds_addr(const void* p) { return (uint32_t)(size_t)(const __attribute__((address_space(3))) void*)p; }
+template <int OFF> RT_DEV void nw_rd(s16x4& d, uint32_t a) {
+  static_assert(OFF >= 0 && OFF < 65536, "ds offset");
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(d) : "v"(a), "i"(OFF));
+}
+template <typename F, int... I> RT_DEV void nw_for_i(F&& f, std::integer_sequence<int, I...>) { (f(std::integral_constant<int, I>()), ...); }
+template <int N, typename F> RT_DEV void nw_for(F&& f) { nw_for_i(f, std::make_integer_sequence<int, N>()); }
+
+__global__ void __launch_bounds__(512, 1) nwgrad_kernel(const NwArgs P) {
+  __shared__ __attribute__((aligned(16))) unsigned char lds[2 * kNwStage];
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int ci0 = blockIdx.y * kNwCI;
+  const int t0 = blockIdx.x * P.per, t1 = min(P.tiles, t0 + P.per);
+  const int npix = P.n * P.h * P.w;
+  const rsrc_t rx = make_rsrc(P.x, npix * P.c * 2);
+  const rsrc_t rdy = make_rsrc(P.dy, npix * 64);
+  auto tile_xy = [&](int t, int& img, int& oh0, int& ow0) {
+    img = (int)fdiv((uint32_t)t, P.f_tpi);
+    const int rem = t - img * (int)P.f_tpi.d, trow = (int)fdiv((uint32_t)rem, P.f_tw);
+    oh0 = trow * kNwTH;
+    ow0 = (rem - trow * (int)P.f_tw.d) * kNwTW;
+  };
+  // wave-instruction ins (1 KB) of a stage: halo pixels 4 ins .. 4 ins + 3 (ins < 66; lane l writes
+  // slot l & 15 of pixel l >> 4 with source chunk (l & 15) ^ 2 (f & 7)), then the dY tile's pixels
+  // (16 per instruction; slot l & 3 of pixel l >> 2, source chunk (l & 3) ^ 2 ((q >> 2) & 1));
+  // pixels outside the image get an offset past num_records (zeros)
+  auto issue = [&](int t, int b) {
+    int img, oh0, ow0;
+    tile_xy(t, img, oh0, ow0);
+    int lz = lane;
+    asm volatile("" : "+v"(lz));
+#pragma unroll
+    for (int u = 0; u < kNwInsW; ++u) {
+      const int ins = wave + kNwWaves * u;
+      unsigned char* dst = lds + b * kNwStage + ins * 1024;
+      if (ins < kNwHIns) {
+        const int f = 4 * ins + (lz >> 4), hr = f / kNwHC, hc = f - hr * kNwHC;
+        const int ih = oh0 - 1 + hr, iw = ow0 - 1 + hc;
+        const bool ok = (unsigned)ih < (unsigned)P.h && (unsigned)iw < (unsigned)P.w;
+        const int ch = (lz & 15) ^ ((f & 7) << 1);
+        buf_lds16(rx, dst, ok ? ((img * P.h + ih) * P.w + iw) * (P.c * 2) + ci0 * 2 + (ch << 4) : (int)0x80000000, 0);
+      } else if (ins < kNwHIns + kNwDIns) {
+        const int q = 16 * (ins - kNwHIns) + (lz >> 2), oh = oh0 + (q >> 6), ow = ow0 + (q & 63);
+        const bool ok = oh < P.h && ow < P.w;
+        const int ch = (lz & 3) ^ (((q >> 2) & 1) << 1);
+        buf_lds16(rdy, dst, ok ? ((img * P.h + oh) * P.w + ow) * 64 + (ch << 4) : (int)0x80000000, 0);
+      }
+    }
+  };
+  if (t0 < t1) issue(t0, 0);
+
+  // per-lane read bases: lane 16 g + 4 qq + p reads pixel rows (base + L) and + 16, L = 4 g + qq,
+  // channels 4 p .. 4 p + 3 of its 16-channel block
+  const int g = lane >> 4, qq = (lane >> 2) & 3, p = lane & 3, L = 4 * g + qq;
+  uint32_t abase[2], bbase[8];
+#pragma unroll
+  for (int cb = 0; cb < 2; ++cb)  // dY pixel rows 32 kk + L (+ 16): (row >> 2) & 1 = (L >> 2) & 1
+    abase[cb] = nw_lds_addr(lds) + kNwDOff + L * 64 + (((2 * cb + (p >> 1)) ^ (((L >> 2) & 1) << 1)) << 4) + (p & 1) * 8;
+#pragma unroll
+  for (int j = 0; j < 8; ++j)  // halo window with (2 row + column) mod 8 = j: (f & 7) = (j + L) & 7
+    bbase[j] = nw_lds_addr(lds) + L * 256 + (((2 * wave + (p >> 1)) ^ (((j + L) & 7) << 1)) << 4) + (p & 1) * 8;
+  f32x4 acc[2][9];
+#pragma unroll
+  for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) acc[cb][tap] = f32x4{0.f, 0.f, 0.f, 0.f};
+  s16x4 fa[2][2][2], fb[2][9][2];  // [register set][block or tap][half]
+  // reads of K-step KK (32 pixels: tile row KK >> 1, columns 32 (KK & 1) ..) into set S, buffer
+  // offset bo; the halo window of tap (r, s) starts at pixel (row + r) * 66 + col + s
+  auto rd_a = [&](uint32_t bo, auto kkc, auto sc) {
+    constexpr int KK = decltype(kkc)::value, S = decltype(sc)::value;
+    nw_for<2>([&](auto cbc) {
+      constexpr int CB = decltype(cbc)::value;
+      nw_rd<32 * KK * 64>(fa[S][CB][0], abase[CB] + bo);
+      nw_rd<(32 * KK + 16) * 64>(fa[S][CB][1], abase[CB] + bo);
+    });
+  };
+  auto rd_b = [&](uint32_t bo, auto kkc, auto sc, auto t0c, auto t1c) {
+    constexpr int KK = decltype(kkc)::value, S = decltype(sc)::value;
+    constexpr int PR = KK >> 1, PC = 32 * (KK & 1);
+    nw_for<decltype(t1c)::value - decltype(t0c)::value>([&](auto ic) {
+      constexpr int TAP = decltype(t0c)::value + decltype(ic)::value, R = TAP / 3, SC = TAP % 3;
+      constexpr int F0 = (PR + R) * kNwHC + PC + SC, J = (2 * (PR + R) + SC) & 7;
+      nw_rd<F0 * 256>(fb[S][TAP][0], bbase[J] + bo);
+      nw_rd<(F0 + 16) * 256>(fb[S][TAP][1], bbase[J] + bo);
+    });
+  };
+  auto frag = [](s16x4& u0, s16x4& u1) {
+    asm volatile("" : "+v"(u0), "+v"(u1));
+    typedef __attribute__((ext_vector_type(8))) short s16x8;
+    s16x8 r = {u0[0], u0[1], u0[2], u0[3], u1[0], u1[1], u1[2], u1[3]};
+    return __builtin_bit_cast(bf16x8, r);
+  };
+  // MFMAs of Cout block CB on register set S.  The halo window is the MFMA's A operand, so a
+  // lane's accumulator holds 4 consecutive input channels of one output channel (one 16-B store
+  // per block in the epilogue)
+  auto mm = [&](auto sc, auto cbc) {
+    constexpr int S = decltype(sc)::value, CB = decltype(cbc)::value;
+    const bf16x8 a = frag(fa[S][CB][0], fa[S][CB][1]);
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+      asm volatile("" : "+v"(fb[S][tap][0]), "+v"(fb[S][tap][1]));
+      acc[CB][tap] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag(fb[S][tap][0], fb[S][tap][1]), a, acc[CB][tap], 0, 0, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  for (int t = t0; t < t1; ++t) {
+    const int b = (t - t0) & 1;
+    const uint32_t bo = b * kNwStage;
+    // tile t landed (this wave's DMA, then everyone's) and every wave is done reading the other
+    // buffer: refill it with tile t + 1
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    rd_a(bo, I0(), I0());
+    rd_b(bo, I0(), I0(), I0(), std::integral_constant<int, 9>());
+    if (t + 1 < t1) issue(t + 1, b ^ 1);
+    // 4 K-steps; the next step's 22 reads are issued in two halves between this step's two MFMA
+    // groups, so each group's operands have landed behind the other's MFMAs
+    nw_for<4>([&](auto kkc) {
+      constexpr int KK = decltype(kkc)::value, S = KK & 1, N = S ^ 1;
+      using IS = std::integral_constant<int, S>;
+      using IN = std::integral_constant<int, N>;
+      using INX = std::integral_constant<int, KK + 1>;
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if constexpr (KK + 1 < 4) {
+        rd_a(bo, INX(), IN());
+        rd_b(bo, INX(), IN(), I0(), std::integral_constant<int, 4>());
+      }
+      mm(IS(), I0());
+      if constexpr (KK + 1 < 4) rd_b(bo, INX(), IN(), std::integral_constant<int, 4>(), std::integral_constant<int, 9>());
+      mm(IS(), I1());
+    });
+  }
+  // partial dW of this workgroup: acc[cb][tap][e] = dW[16 cb + (lane & 15)][tap][ci0 + 16 wave + 4 g + e]
+  float* out = P.slab + (long)blockIdx.x * (32 * 9) * P.c;
+#pragma unroll
+  for (int cb = 0; cb < 2; ++cb) {
+    const int co = 16 * cb + (lane & 15);
+    if (co >= P.k) continue;
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) *(f32x4*)(out + (long)(co * 9 + tap) * P.c + ci0 + 16 * wave + 4 * g) = acc[cb][tap];
+  }
+}
+
 // ---- host -------------------------------------------------------------------------------
 // tile width: 64 columns, or 32 for 32-wide maps
 static int hconv_tc(const rtsds_conv_desc* d) {
@@ -338,4 +522,40 @@ void hconv_dgrad(const rtsds_conv_desc* d, const void* dyp, int kp, const void* 
   a.stats = nullptr;
   a.n = d->n; a.h = d->h; a.w = d->w; a.c = kp; a.k = d->c; a.act = 0; a.accum = accumulate ? 1 : 0;
   hconv_launch(a, hconv_tc(d), hconv_tiles(d), (d->c + 31) / 32, st);
+}
+
+// weight gradient (nwgrad_kernel): Cout <= 32 (dY padded to 32 channels by the caller), Cin a
+// multiple of 128, 3x3 same-padding stride 1; any h, w (partial tiles read zeros)
+bool nwgrad_ok(const rtsds_conv_desc* d) {
+  return d->dtype == RTSDS_BF16 && d->kh == 3 && d->kw == 3 && d->sh == 1 && d->sw == 1 && d->ph == 1 && d->pw == 1 &&
+         d->dh == 1 && d->dw == 1 && d->k <= 32 && d->c % kNwCI == 0 && (long)d->n * d->h * d->w * d->c * 2 < (1L << 31);
+}
+static int nw_tiles(const rtsds_conv_desc* d) { return d->n * ((d->h + kNwTH - 1) / kNwTH) * ((d->w + kNwTW - 1) / kNwTW); }
+// one workgroup per CU: the Cin / 128 channel chunks x runs of tiles
+static void nw_grid(const rtsds_conv_desc* d, int& runs, int& per) {
+  static int cus = 0;
+  if (!cus && (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0) != hipSuccess || cus < 1)) cus = 256;
+  const int tiles = nw_tiles(d), chunks = d->c / kNwCI;
+  const int want = std::max(1, cus / chunks);
+  per = (tiles + want - 1) / want;
+  runs = (tiles + per - 1) / per;
+}
+// split-K slabs of the launch (one per run of tiles)
+int nwgrad_splits(const rtsds_conv_desc* d) {
+  int runs, per;
+  nw_grid(d, runs, per);
+  return runs;
+}
+// slab [runs][32][9][c]: the partial dW of every run (rows co < k)
+void nwgrad(const rtsds_conv_desc* d, const void* x, const void* dyp, float* slab, hipStream_t st) {
+  NwArgs a = {};
+  a.x = (const bf16*)x; a.dy = (const bf16*)dyp; a.slab = slab;
+  a.n = d->n; a.h = d->h; a.w = d->w; a.c = d->c; a.k = d->k;
+  a.tiles = nw_tiles(d);
+  const int tw = (d->w + kNwTW - 1) / kNwTW, th = (d->h + kNwTH - 1) / kNwTH;
+  a.f_tpi = fastdiv_make(th * tw);
+  a.f_tw = fastdiv_make(tw);
+  int runs;
+  nw_grid(d, runs, a.per);
+  hipLaunchKernelGGL(nwgrad_kernel, dim3(runs, d->c / kNwCI), dim3(64 * kNwWaves), 0, st, a);
 }

@@ -61,6 +61,8 @@ CONV_CASES = [
     (2, 128, 8, 128, 19, 3, 1, 1, 1, False),   # halo direct conv (hconv.hip): Cout 19, w % 64 == 0
     (1, 64, 12, 64, 32, 3, 1, 1, 1, True),     # hconv with bias, Cout 32, edge tiles on 3 row-blocks
     (1, 256, 8, 64, 64, 3, 1, 1, 1, True),     # hconv N-tiled (Cin >= 256, Cout 2 x 32), fwd and dgrad
+    (2, 256, 6, 100, 19, 3, 1, 1, 1, False),   # halo weight gradient (nwgrad): 2 channel chunks, partial column tiles
+    (1, 128, 5, 64, 32, 3, 1, 1, 1, True),     # nwgrad: Cout 32 (no dY pad), odd rows, dbias
     (2, 512, 16, 32, 512, 3, 1, 1, 1, False),  # layer4-like: DGRAD split-K (128x128 tiles, fp32 slabs)
     (2, 512, 16, 32, 512, 3, 1, 2, 2, False),  # dilated (DeepLab layer3-like, small M): DGRAD split-K
     (2, 256, 16, 32, 19, 3, 1, 2, 2, True),    # ASPP-like narrow output, few M tiles: FWD split-K slabs
