@@ -18,6 +18,7 @@
 // per-tile partial statistics (count, mean, M2 -- the exact two-pass form, as the GEMM
 // epilogue), scalar bf16 stores of the Cout valid channels.
 #include "common.h"
+#include <algorithm>
 #include <utility>
 
 namespace {
@@ -272,6 +273,136 @@ __global__ void __launch_bounds__(256, 1) hconv_fwd_kernel(const HconvArgs P) {
   }
 }
 
+// ---- data gradient of the narrow-output conv, persistent over output-channel tiles ------------
+// dX = conv(dY_p, W flipped / transposed) with dY_p the 32-channel-padded gradient (ONE channel
+// chunk): hconv_fwd_kernel re-stages the dY halo for every 32-wide tile of the Cin outputs (32
+// workgroups per spatial tile for the FFM's 1024 channels) and each short workgroup's DMA ->
+// 72 MFMAs -> LDS-staged stores run back to back.  Here a workgroup stages the halo ONCE and
+// walks nt output-channel tiles with their weights double-buffered (tile j + 1's DMA in flight
+// behind tile j's MFMAs and stores); the MFMA computes C^T = W X^T, so a lane ends with 4
+// consecutive channels of one pixel and stores 8 B straight from the accumulators (no LDS
+// staging: 68 KB of LDS, two workgroups per CU).
+template <int TC>
+__global__ void __launch_bounds__(256, 2) hconv_dgrad_nt_kernel(const HconvArgs P, int nt) {
+  using G = HTile<TC>;
+  constexpr int kTR = G::TR, kHC = G::HC, kHaloPix = G::HaloPix, kHaloInstr = G::HaloInstr, kHaloBytes = G::HaloBytes;
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];  // halo | 2 weight stages
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tw_n = P.w / TC, th_n = P.h / kTR;
+  int bid;
+  {  // XCD-aware bijective remap: each XCD gets a contiguous run of tiles (shared halo rows)
+    const int nwg = gridDim.x, b = blockIdx.x;
+    const int xcd = b & 7, q = nwg >> 3, r = nwg & 7;
+    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
+  }
+  const int img = bid / (th_n * tw_n), rem = bid - img * th_n * tw_n;
+  const int trow = rem / tw_n, tcol = rem - trow * tw_n;
+  const int oh0 = trow * kTR, ow0 = tcol * TC;
+  const int C = P.c;  // == kCK: one channel chunk
+  const rsrc_t rx = make_rsrc(P.x, P.n * P.h * P.w * C * 2);
+  const rsrc_t rw = make_rsrc(P.wt, P.k * 9 * C * 2);
+#pragma unroll
+  for (int u = 0; u < kHaloInstr / 4; ++u) {
+    const int piece = (wave + 4 * u) * 64 + lane, hp = piece >> 2, slot = piece & 3;
+    int v = (int)0x80000000;
+    if (hp < kHaloPix) {
+      const int hr = hp / kHC, hc = hp - hr * kHC;
+      const int ih = oh0 - 1 + hr, iw = ow0 - 1 + hc;
+      const int ch = slot ^ ((hp >> 2) & 3);
+      if ((unsigned)ih < (unsigned)P.h && (unsigned)iw < (unsigned)P.w) v = (((img * P.h + ih) * P.w + iw) * C + ch * 8) * 2;
+    }
+    buf_lds16(rx, lds + (wave + 4 * u) * 1024, v, 0);
+  }
+  int woff[kWInstr / 4];
+#pragma unroll
+  for (int u = 0; u < kWInstr / 4; ++u) {
+    const int piece = (wave + 4 * u) * 64 + lane;
+    int v = (int)0x80000000;
+    if (piece < 9 * 32 * 4) {
+      const int tap = piece >> 7, n = (piece >> 2) & 31, slot = piece & 3;
+      v = ((n * 9 + tap) * C + (slot ^ ((n >> 2) & 3)) * 8) * 2;  // + the tile's rows as soffset
+    }
+    woff[u] = v;
+  }
+  const int j0 = blockIdx.y * nt, j1 = min(P.k / 32, j0 + nt);
+  auto issue_w = [&](int j, int st) {
+    unsigned char* wb = lds + kHaloBytes + st * kWBytes;
+#pragma unroll
+    for (int u = 0; u < kWInstr / 4; ++u) buf_lds16(rw, wb + (wave + 4 * u) * 1024, woff[u], j * (32 * 9 * 2) * C);
+  };
+  if (j0 < j1) issue_w(j0, 0);
+  const int fr = lane & 15, fc = lane >> 4;
+  int bslot[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int n = 16 * j + fr;
+    bslot[j] = (n * 4 + (fc ^ ((n >> 2) & 3))) * 16;
+  }
+  constexpr int kSt = 8;  // 8-B stores per lane and tile
+  for (int j = j0; j < j1; ++j) {
+    const int st = (j - j0) & 1;
+    // tile j's weights (and, first, the halo) landed -- all but this wave's stores of tile j - 1 --
+    // then everyone's, and every wave is done reading the other weight stage: refill it
+    if (j == j0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kSt) : "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (j + 1 < j1) issue_w(j + 1, st ^ 1);
+    const unsigned char* wb = lds + kHaloBytes + st * kWBytes;
+    auto rd = [&](int tap, bf16x8* fa, bf16x8* fb) {
+      const int r = tap / 3, s = tap - 3 * r;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int p0 = 64 * wave + 16 * i;
+        const int hp = (p0 / TC + r) * kHC + p0 % TC + fr + s;
+        fa[i] = *(const bf16x8*)(lds + hp * 64 + ((fc ^ ((hp >> 2) & 3)) << 4));
+      }
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) fb[jj] = *(const bf16x8*)(wb + tap * 32 * 64 + bslot[jj]);
+    };
+    f32x4 acc[4][2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) acc[i][jj] = f32x4{0.f, 0.f, 0.f, 0.f};
+    bf16x8 fa_s[3][4], fb_s[3][2];
+    rd(0, fa_s[0], fb_s[0]);
+    rd(1, fa_s[1], fb_s[1]);
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+      bf16x8* fa = fa_s[tap % 3];
+      bf16x8* fb = fb_s[tap % 3];
+      if (tap + 2 < 9) rd(tap + 2, fa_s[(tap + 2) % 3], fb_s[(tap + 2) % 3]);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj) acc[i][jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[jj], fa[i], acc[i][jj], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // C^T: acc[i][jj][e] = dX[pixel 64 wave + 16 i + fr][channel 32 j + 16 jj + 4 fc + e]
+    const int px_r = (64 * wave) / TC;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int pc = (64 * wave) % TC + 16 * i + fr;
+      const long o = (((long)img * P.h + oh0 + px_r + pc / TC) * P.w + ow0 + pc % TC) * P.k + 32 * j + 4 * fc;
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) {
+        bf16x4 t;
+        if (P.accum) {
+          const bf16x4 old = *(const bf16x4*)(P.y + o + 16 * jj);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) t[e] = (bf16)(acc[i][jj][e] + (float)old[e]);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) t[e] = (bf16)acc[i][jj][e];
+        }
+        *(bf16x4*)(P.y + o + 16 * jj) = t;
+      }
+    }
+  }
+}
+
 // ---- weight gradient of the narrow-output conv ------------------------------------------------
 // dW[co][r][s][ci] = sum_px dY[px][co] X[px + (r - 1, s - 1)][ci] for Cout <= 32 (dY channel-padded
 // to 32), Cin a multiple of 128.  As a split-K GEMM (M = 32 rows of Cout, N = 9 taps x Cin,
@@ -516,11 +647,29 @@ void hconv_fwd(const rtsds_conv_desc* d, const void* x, const void* w, const flo
   hconv_launch(a, hconv_tc(d), hconv_tiles(d), (d->k + 31) / 32, st);
 }
 // dx (+)= conv(dy_p, wt_flipped): dy_p [n][h][w][kp] (kp % 32 == 0), wt [c][3][3][kp]
+template <int TC>
+static void hconv_dgrad_nt_launch(const HconvArgs& a, int tiles, hipStream_t st) {
+  constexpr int lds = HTile<TC>::HaloBytes + 2 * kWBytes;
+  static const bool lds_ok =
+      hipFuncSetAttribute((const void*)hconv_dgrad_nt_kernel<TC>, hipFuncAttributeMaxDynamicSharedMemorySize, lds) == hipSuccess;
+  (void)lds_ok;
+  static int cus = 0;
+  if (!cus && (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0) != hipSuccess || cus < 1)) cus = 256;
+  // output-channel tiles per workgroup: one round of two workgroups per CU
+  const int ntn = a.k / 32;
+  const int nt = std::max(1, (int)(((long)ntn * tiles + 2 * cus - 1) / (2 * cus)));
+  hipLaunchKernelGGL(hconv_dgrad_nt_kernel<TC>, dim3(tiles, (ntn + nt - 1) / nt), dim3(256), lds, st, a, nt);
+}
 void hconv_dgrad(const rtsds_conv_desc* d, const void* dyp, int kp, const void* wt, void* dx, int accumulate, hipStream_t st) {
   HconvArgs a;
   a.x = (const bf16*)dyp; a.wt = (const bf16*)wt; a.bias = nullptr; a.scale = nullptr; a.res = nullptr; a.y = (bf16*)dx;
   a.stats = nullptr;
   a.n = d->n; a.h = d->h; a.w = d->w; a.c = kp; a.k = d->c; a.act = 0; a.accum = accumulate ? 1 : 0;
+  if (kp == kCK && d->c % 32 == 0) {  // one channel chunk: the halo stays, the weight tiles stream
+    if (hconv_tc(d) == 64) hconv_dgrad_nt_launch<64>(a, hconv_tiles(d), st);
+    else hconv_dgrad_nt_launch<32>(a, hconv_tiles(d), st);
+    return;
+  }
   hconv_launch(a, hconv_tc(d), hconv_tiles(d), (d->c + 31) / 32, st);
 }
 

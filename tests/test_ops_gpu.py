@@ -128,6 +128,32 @@ def test_dgrad_split_k_accumulate():
     _close(dx, dx0.double() + fresh.double(), torch.bfloat16, "dx accum", tol=1e-2)
 
 
+@pytest.mark.parametrize("geo", [(1, 128, 8, 64, 19), (1, 96, 16, 32, 32)])
+def test_hconv_dgrad_accumulate(geo):
+    """Narrow-output data gradient (hconv_dgrad_nt_kernel: the dY halo staged once, the output
+    channel tiles streamed; 64- and 32-wide maps) with and without the accumulate flag."""
+    import ctypes
+    from rtsds_amd._lib import lib
+    from rtsds_amd.functional import _conv_desc, _P
+    from rtsds_amd.runtime import stream, workspace
+
+    n, c, h, w, k = geo
+    g = torch.Generator().manual_seed(11)
+    dy = _dev(torch.randn(n, k, h, w, generator=g), torch.bfloat16)
+    wq = _dev(torch.randn(k, c, 3, 3, generator=g) / (9 * c) ** 0.5, torch.bfloat16)
+    x = _dev(torch.zeros(n, c, h, w), torch.bfloat16)
+    d = _conv_desc(x, k, 3, 3, (1, 1), (1, 1), (1, 1))
+    dx0 = _dev(torch.randn(n, c, h, w, generator=g), torch.bfloat16)
+    dx, fresh = dx0.clone(), torch.empty_like(dx0)
+    ws = workspace(lib.rtsds_conv2d_dgrad_workspace(ctypes.byref(d)), x.device)
+    for out, acc in ((dx, 1), (fresh, 0)):
+        assert lib.rtsds_conv2d_dgrad(ctypes.byref(d), _P(dy), _P(wq), _P(out), acc, _P(ws), ws.numel(), stream()) == 0
+    torch.cuda.synchronize()
+    ref = TF.conv_transpose2d(dy.double().cpu(), wq.double().cpu(), padding=1)
+    _close(fresh, ref, torch.bfloat16, "dx")
+    _close(dx, dx0.double() + fresh.double(), torch.bfloat16, "dx accum", tol=1e-2)
+
+
 def test_fwd_split_k_accumulate():
     """FWD split-K (narrow output, few M tiles: DeepLab's ASPP branches) with bias and the
     accumulate flag (ConvSum: y += conv + bias), against the non-accumulating call."""
