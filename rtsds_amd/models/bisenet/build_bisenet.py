@@ -117,6 +117,12 @@ class BiSeNet(torch.nn.Module):
     # training: spatial path on runtime.branch_stream beside the context path (bs 8 train step
     # +2.5 %; at inference the fork / join edges cost more than the overlap gains)
     branch_parallel = True
+    # the spatial path starts at the fork point (an event after layer1) but is enqueued after the
+    # whole context path: its autograd nodes then carry the highest sequence numbers, so the
+    # engine enqueues its backward right after the fusion module's, ahead of the context path's
+    # layer4..2 backward (the graph's dependencies are the same either way; the multi-queue
+    # replay submits nodes in capture order): bs-8 step +0.25 % (profiles/r5ar_spatial_order_ab.txt)
+    spatial_enqueued_last = True
     # inference (eval, no autograd): resizes written into the fusion module's concatenated input
     # and the attention tail + final 1x1 conv fused (False: the separate ops, for A/B tests)
     inference_fusions = True
@@ -171,12 +177,23 @@ class BiSeNet(torch.nn.Module):
             side = branch_stream(x.device)
             box = []
 
-            def fork():  # after the context path's layer1 (_ContextPath.fork_after): beside its later layers
-                side.wait_stream(main)
+            def run_spatial():
                 x.record_stream(side)  # read (and saved for backward) on the branch stream
                 with torch.cuda.stream(side):
                     box.append(BranchOut.apply(self.saptial_path(x), main, side))
+
+            def fork():  # after the context path's layer1 (_ContextPath.fork_after): beside its later layers
+                if self.spatial_enqueued_last:
+                    ev = torch.cuda.Event()
+                    ev.record(main)
+                    box.append(ev)
+                else:
+                    side.wait_stream(main)
+                    run_spatial()
             f3, f4, tail = self.context_path(x, mid=fork, tail_join=j4)
+            if self.spatial_enqueued_last:
+                side.wait_event(box.pop())
+                run_spatial()
             sx = box[0]
             main.wait_stream(side)
             sx.record_stream(main)
