@@ -36,9 +36,11 @@ for k, a in sorted(agg.items(), key=lambda x: -x[1]["dur"])[:40]:
     wc = a["SQ_WAVE_CYCLES"] or 1
     print(f"{k[:72]:72s} {a['n']:5d} {a['dur'] / 1e3 / steps:9.1f} {100 * a['dur'] / tot_dur:6.1f} {100 * u1:9.1f} "
           f"{100 * u2:9.1f} {100 * a['SQ_WAIT_ANY'] / wc:6.1f} {100 * a['SQ_WAIT_INST_ANY'] / wc:6.1f}")
-conv = [a for k, a in agg.items() if "conv_gemm" in k or "hconv" in k]
-busy = sum(a["SQ_VALU_MFMA_BUSY_CYCLES"] for a in conv)
-dur = sum(a["dur"] for a in conv)
-gui = sum(a["GRBM_GUI_ACTIVE"] for a in conv)
-print(f"conv family: {dur / 1e3 / steps:.1f} us/step, MFMA busy {100 * busy / (1024 * gui / 8):.1f} % of busy clocks, "
-      f"{100 * busy / (1024 * dur * 2.4):.1f} % at 2.4 GHz; MFMA busy cycles/step {busy / steps:.3g}")
+for label, fams in (("conv family", ("conv_gemm", "hconv")),
+                    ("conv family incl. tapconv / imgconv / nwgrad", ("conv_gemm", "hconv", "nwgrad", "tapconv", "imgconv"))):
+    conv = [a for k, a in agg.items() if any(f in k for f in fams)]
+    busy = sum(a["SQ_VALU_MFMA_BUSY_CYCLES"] for a in conv)
+    dur = sum(a["dur"] for a in conv)
+    gui = sum(a["GRBM_GUI_ACTIVE"] for a in conv)
+    print(f"{label}: {dur / 1e3 / steps:.1f} us/step, MFMA busy {100 * busy / (1024 * gui / 8):.1f} % of busy clocks, "
+          f"{100 * busy / (1024 * dur * 2.4):.1f} % at 2.4 GHz; MFMA busy cycles/step {busy / steps:.3g}")

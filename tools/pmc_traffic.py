@@ -63,7 +63,7 @@ def main():
     if len(sys.argv) > 3:
         # every conv-family launch (implicit GEMM, direct convs and their helpers), as the
         # live roofline's event-timed conv calls include them
-        fams = ("conv_gemm_kernel", "hconv_fwd_kernel", "tapconv_kernel", "tapwgrad_kernel", "imgconv_fwd_kernel", "imgconv_pool_kernel",
+        fams = ("conv_gemm_kernel", "hconv_fwd_kernel", "hconv_dgrad_nt_kernel", "nwgrad_kernel", "tapconv_kernel", "tapwgrad_kernel", "imgconv_fwd_kernel", "imgconv_pool_kernel",
                 "pw_dgrad_kernel", "pooled_fwd_vec_kernel", "pooled_dgrad_vec_kernel", "pooled_wgrad_kernel",
                 "split_reduce_many_kernel", "split_reduce_kernel", "dgrad_pack_kernel", "repack_wt_kernel",
                 "pad_channels_kernel", "dgrad_split_reduce_kernel", "fwd_split_reduce_kernel", "sp_repack_w_kernel",
