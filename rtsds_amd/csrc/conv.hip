@@ -246,10 +246,13 @@ static bool pooled_1x1(const rtsds_conv_desc* d) {
 }
 
 // y[m][k] = act(sum_c x[m][c] w[k][c] + bias[k]); one wave per output channel k.
+// scale (optional, [k]): the eval-mode BatchNorm fold, y = act(acc * scale + bias) (as the GEMM
+// epilogue of rtsds_conv2d_fwd_bn; fmaf(acc, 1, b) == acc + b without it)
 template <typename T, int MR>
 __global__ void __launch_bounds__(256) pooled_fwd_kernel(const T* __restrict__ x, const T* __restrict__ w,
                                                         const float* __restrict__ bias, T* __restrict__ y, int m_n, int c,
-                                                        int k_n, int act, int accum, float* __restrict__ stats) {
+                                                        int k_n, int act, int accum, float* __restrict__ stats,
+                                                        const float* __restrict__ scale) {
   const int k = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (k >= k_n) return;
   float acc[MR];
@@ -265,12 +268,12 @@ __global__ void __launch_bounds__(256) pooled_fwd_kernel(const T* __restrict__ x
   for (int m = 0; m < MR; ++m)
     if (m < m_n) acc[m] = wave_sum(acc[m]);
   if (lane != 0) return;
-  const float bv = bias ? bias[k] : 0.f;
+  const float bv = bias ? bias[k] : 0.f, sv = scale ? scale[k] : 1.f;
   float mean = 0.f;
 #pragma unroll
   for (int m = 0; m < MR; ++m)
     if (m < m_n) {
-      float v = acc[m] + bv;
+      float v = fmaf(acc[m], sv, bv);
       acc[m] = v;
       mean += v;
       if (accum) v += to_f(y[(long)m * k_n + k]);
@@ -339,7 +342,8 @@ __global__ void __launch_bounds__(256) pooled_wgrad_kernel(const T* __restrict__
 template <typename T, int MR>
 __global__ void __launch_bounds__(256) pooled_fwd_vec_kernel(const T* __restrict__ x, const T* __restrict__ w,
                                                             const float* __restrict__ bias, T* __restrict__ y, int m_n, int c,
-                                                            int k_n, int act, int accum, float* __restrict__ stats) {
+                                                            int k_n, int act, int accum, float* __restrict__ stats,
+                                                            const float* __restrict__ scale) {
   typedef typename VecT<T>::v16 V16;
   constexpr int V = VecT<T>::N;
   const int k = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
@@ -361,12 +365,12 @@ __global__ void __launch_bounds__(256) pooled_fwd_vec_kernel(const T* __restrict
   for (int m = 0; m < MR; ++m)
     if (m < m_n) acc[m] = wave_sum(acc[m]);
   if (lane != 0) return;
-  const float bv = bias ? bias[k] : 0.f;
+  const float bv = bias ? bias[k] : 0.f, sv = scale ? scale[k] : 1.f;
   float mean = 0.f;
 #pragma unroll
   for (int m = 0; m < MR; ++m)
     if (m < m_n) {
-      float v = acc[m] + bv;
+      float v = fmaf(acc[m], sv, bv);
       acc[m] = v;
       mean += v;
       if (accum) v += to_f(y[(long)m * k_n + k]);
@@ -438,22 +442,22 @@ __global__ void __launch_bounds__(256) pooled_dgrad_vec_kernel(const bf16* __res
 
 template <typename T>
 static void pooled_fwd_launch(const rtsds_conv_desc* d, const void* x, const void* w, const float* bias, void* y, int act,
-                              int accum, float* stats, hipStream_t st) {
+                              int accum, float* stats, hipStream_t st, const float* scale = nullptr) {
   if (d->c % VecT<T>::N == 0) {
     if (d->n <= 8)
       hipLaunchKernelGGL((pooled_fwd_vec_kernel<T, 8>), dim3(rt_cdiv(d->k, 4)), dim3(256), 0, st, (const T*)x, (const T*)w,
-                         bias, (T*)y, d->n, d->c, d->k, act, accum, stats);
+                         bias, (T*)y, d->n, d->c, d->k, act, accum, stats, scale);
     else
       hipLaunchKernelGGL((pooled_fwd_vec_kernel<T, kPooledMaxRows>), dim3(rt_cdiv(d->k, 4)), dim3(256), 0, st, (const T*)x,
-                         (const T*)w, bias, (T*)y, d->n, d->c, d->k, act, accum, stats);
+                         (const T*)w, bias, (T*)y, d->n, d->c, d->k, act, accum, stats, scale);
     return;
   }
   if (d->n <= 8)
     hipLaunchKernelGGL((pooled_fwd_kernel<T, 8>), dim3(rt_cdiv(d->k, 4)), dim3(256), 0, st, (const T*)x, (const T*)w, bias,
-                       (T*)y, d->n, d->c, d->k, act, accum, stats);
+                       (T*)y, d->n, d->c, d->k, act, accum, stats, scale);
   else
     hipLaunchKernelGGL((pooled_fwd_kernel<T, kPooledMaxRows>), dim3(rt_cdiv(d->k, 4)), dim3(256), 0, st, (const T*)x,
-                       (const T*)w, bias, (T*)y, d->n, d->c, d->k, act, accum, stats);
+                       (const T*)w, bias, (T*)y, d->n, d->c, d->k, act, accum, stats, scale);
 }
 template <typename T>
 static void pooled_dgrad_launch(const rtsds_conv_desc* d, const void* dy, const void* w, void* dx, int accum, hipStream_t st) {
@@ -747,6 +751,11 @@ extern "C" int rtsds_conv2d_fwd_bn(const rtsds_conv_desc* d0, const void* x, con
   const bool x_padded = (act & RTSDS_INPUT_PADDED) != 0;
   if (x_padded && input_pitch(d0) == d0->c) return RTSDS_ERR_UNSUPPORTED;
   hipStream_t st = (hipStream_t)stream;
+  if (pooled_1x1(d0) && !res && !x_padded) {  // the attention refinements' 1x1 convs on pooled vectors
+    if (d0->dtype == RTSDS_BF16) pooled_fwd_launch<bf16>(d0, x, w, shift, y, act & 0xff, 0, nullptr, st, scale);
+    else pooled_fwd_launch<float>(d0, x, w, shift, y, act & 0xff, 0, nullptr, st, scale);
+    return hipGetLastError() == hipSuccess ? RTSDS_OK : RTSDS_ERR_LAUNCH;
+  }
   if (tapconv_ok(d0)) {
     tapconv_fwd(d0, x, w, shift, scale, res, y, act & 0xff, nullptr, st);
     return hipGetLastError() == hipSuccess ? RTSDS_OK : RTSDS_ERR_LAUNCH;

@@ -779,7 +779,8 @@ FOLD_CASES = [
     (2, 3, 32, 48, 64, 7, 2, 3, False, 1, False),    # stem conv + bn1 + relu
     (2, 64, 16, 24, 64, 3, 1, 1, False, 1, True),    # BasicBlock conv2 + bn2 + identity + relu
     (2, 64, 16, 16, 128, 1, 2, 0, False, 0, False),  # downsample 1x1 s2 + bn
-    (8, 256, 1, 1, 256, 1, 1, 0, True, 3, False),    # ARM 1x1(bias) + bn + sigmoid
+    (8, 256, 1, 1, 256, 1, 1, 0, True, 3, False),    # ARM 1x1(bias) + bn + sigmoid (pooled-vector kernel)
+    (5, 19, 1, 1, 19, 1, 1, 0, True, 1, False),      # pooled, C % 8 != 0: scalar kernel with the fold
     (2, 1024, 8, 16, 19, 3, 1, 1, False, 1, False),  # FFM ConvBlock (N=19: scalar epilogue)
     (8, 128, 64, 64, 128, 3, 1, 1, False, 1, True),  # 128x128 LDS-DMA tile + residual
     (2, 256, 8, 64, 256, 3, 1, 1, False, 1, True),   # halo conv (bf16), 4 x 64 tiles + residual
