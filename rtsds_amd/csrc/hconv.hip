@@ -1,6 +1,8 @@
 // Halo-resident direct 3x3 convolution for narrow outputs (Cout <= 32) -- the BiSeNet feature
 // fusion ConvBlock, 1024 -> 19 channels at 1/8 resolution (build_bisenet.py:64-65 via
-// ConvBlock build_bisenet.py:9-18), forward only.
+// ConvBlock build_bisenet.py:9-18): forward (hconv_fwd_kernel, also the N-tiled deep 3x3 convs
+// and the data gradients over multi-chunk dY), the single-chunk data gradient
+// (hconv_dgrad_nt_kernel) and the weight gradient (nwgrad_kernel), each further below.
 //
 // As an implicit GEMM this conv is N = 19 wide: every input byte the im2col gathers feeds only
 // 19 outputs, and the 3x3 taps gather each input pixel 9 times, so the generic kernel is bound
