@@ -24,22 +24,19 @@ class CrossEntropyLoss(nn.Module):
 
 class BCEWithLogitsLoss(nn.Module):
     """Mean of the logistic loss.  Under data parallelism the mean runs over every rank's
-    elements.  D's logits have a data-independent size, so the global element count is
-    all-reduced once per local size and cached.  The cache miss is a collective, so every rank
-    must miss on the same calls: each rank's sequence of local sizes must be fixed from the
-    first iteration on -- equal shards (DistributedSampler pads its shards to equal length,
-    synthetic loaders are equal, main.py's loaders drop_last) or unequal but fixed shards
-    (those get the exact weighted mean).  A rank that meets a new local size while another
-    rank hits its cache would desynchronise the collectives, and that case is NOT detected: the
-    check on a miss (every rank taking part, equal cache lengths) only catches ranks that miss
-    together with different cache histories.  The missing rank's count all-reduce would pair
-    with the other rank's next collective."""
+    elements: every eager call all-reduces the local element count (a one-element collective,
+    issued by every rank on every call, so the collectives of the ranks always pair up) and
+    scales this rank's mean by n / total on the device (no host sync).  Under hipGraph capture
+    (runtime.GraphedStep) no collective may run inside the captured segment, so the call reuses
+    the scale of the last eager call with the same local size (the warm-up iterations before
+    capture); graph replays have static shapes, so that scale stays valid.  A capture that meets
+    a local size no eager call has seen raises instead of guessing."""
 
     def __init__(self, reduction="mean"):
         super().__init__()
         if reduction != "mean":
             raise NotImplementedError("rtsds_amd.BCEWithLogitsLoss: mean only (main.py:132)")
-        self._global = {}
+        self._scale = {}
 
     def forward(self, input, target):
         loss = F.bce_with_logits(input, target)
@@ -47,20 +44,19 @@ class BCEWithLogitsLoss(nn.Module):
             return loss
         # global-batch mean under data parallelism (see runtime.dp_world): this rank's mean
         # weighted by its share of the all-reduced element count, so shards of unequal size
-        # still sum to the gathered-batch mean (a graph-segment break under capture)
+        # still sum to the gathered-batch mean
         import torch.distributed as dist
         n = int(input.numel())
-        total = self._global.get((n, dp_world()))
-        if total is None:
-            if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
-                raise RuntimeError("rtsds_amd.BCEWithLogitsLoss: run an eager iteration before graph capture")
-            # [local count, 1, number of cached sizes]: the second slot counts the ranks taking
-            # part, the third must agree (all ranks miss together on the same call)
-            cnt = torch.tensor([float(n), 1.0, float(len(self._global))], dtype=torch.float64, device=input.device)
-            dist.all_reduce(cnt)  # eager, outside any graph capture: warm-up iterations fill the cache
-            w = dist.get_world_size()  # the ranks the collective actually ran over
-            if int(cnt[1].item()) != w or float(cnt[2].item()) != w * len(self._global):
-                raise RuntimeError("rtsds_amd.BCEWithLogitsLoss: ranks disagree on the global element count "
-                                   "cache (local batch sizes must follow the same pattern on every rank)")
-            total = self._global[(n, dp_world())] = float(cnt[0].item())
-        return loss * (n / total)
+        key = (n, dp_world())
+        if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
+            scale = self._scale.get(key)
+            if scale is None:
+                raise RuntimeError("rtsds_amd.BCEWithLogitsLoss: run an eager iteration with this local "
+                                   "batch size before graph capture")
+            return loss * scale
+        cnt = torch.full((1,), float(n), dtype=torch.float64, device=input.device)
+        dist.all_reduce(cnt)
+        # fp32(n / total): the rounding ATen applies to a Python-float multiplier
+        scale = (n / cnt).to(loss.dtype).reshape(())
+        self._scale[key] = scale
+        return loss * scale

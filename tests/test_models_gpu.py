@@ -81,6 +81,7 @@ def _check_adam(arrays, meta, name, tensors, lr, steps):
         worst = max(worst, float(d.max()))
         bad += int((d > 2e-6 + 1e-5 * np.abs(ref)).sum())
         n += d.size
+    print(f"adam {name}: {bad} of {n} sampled elements off by > 2e-6 (frac {bad / max(n, 1):.5f}), worst {worst:.3e}")
     assert worst <= 2.05 * lr * steps, (name, worst)
     assert bad <= 0.03 * n, (name, bad, n)
 
@@ -151,20 +152,43 @@ def test_bisenet_fp32_matches_oracle_and_reference(inputs, golden):
 
 
 def test_bisenet_bf16_close_to_oracle(inputs):
+    """bf16 train-mode forward at 2 x 3 x 128 x 256 vs the oracle, bounded by a CONTROL that
+    applies bf16's perturbations in fp32 arithmetic (tests/test_configs_gpu.py uses the same
+    rule at the bench shape): our fp32 mode on the bf16-rounded input with bf16-rounded conv
+    weights (bf16 mode reads the rounded weight shadow) and every ConvBlock / BasicBlock output
+    rounded to bf16.  The ARM BatchNorm over N=2 pooled vectors (build_bisenet.py:49) outputs
+    +-gamma+beta by the SIGN of the two images' difference, so bf16 rounding flips whole
+    attention channels: the network, not the kernels, sets the size of both errors (kernels:
+    tests/test_ops_gpu.py).  Required: relative Frobenius error <= max(2 %, 1.5x the control's)
+    and argmax agreement >= 1 - 1.5x the control's disagreement."""
     x, y, _ = inputs
     ref = _load(om.BiSeNet(19, "resnet18"), 1).train()
     net = _load(BiSeNet(19, "resnet18"), 1).to(DEV).train()
     ro, _, _ = ref(x)
+    ro = ro.detach().double()
     with rtsds_amd.precision(torch.bfloat16):
         o, _, _ = net(x.to(DEV))
     assert o.dtype == torch.bfloat16
-    fro = ((o.double().cpu() - ro.double()).norm() / ro.double().norm()).item()
-    agree = (o.float().cpu().argmax(1) == ro.argmax(1)).float().mean().item()
-    print(f"bf16 BiSeNet: frobenius rel err {fro:.4f}, argmax agreement {agree:.4f}")
-    # ARM BatchNorm over N=2 pooled vectors (build_bisenet.py:49) outputs +-gamma+beta by the
-    # SIGN of the two images' difference, so bf16 rounding flips whole attention channels:
-    # the network, not the kernels, sets this bound (kernels: tests/test_ops_gpu.py).
-    assert fro < 0.2 and agree > 0.85, (fro, agree)
+    sd = net.state_dict()
+    ctl = BiSeNet(19, "resnet18").to(DEV).train()
+    ctl.load_state_dict({k: (v.to(torch.bfloat16).float() if v.dim() == 4 else v) for k, v in sd.items()})
+    from tests.test_configs_gpu import _block_rounding
+    hooks = _block_rounding(ctl)
+    with rtsds_amd.precision(torch.float32), torch.no_grad():
+        oc, _, _ = ctl(x.to(torch.bfloat16).float().to(DEV))
+    for h in hooks:
+        h.remove()
+
+    def cmp(a):
+        a = a.detach().double().cpu()
+        return (((a - ro).norm() / ro.norm()).item(), (a.argmax(1) == ro.argmax(1)).float().mean().item())
+    fro, agree = cmp(o)
+    fro_c, agree_c = cmp(oc)
+    print(f"bf16 BiSeNet: frobenius rel err {fro:.4f} (control {fro_c:.4f}), argmax agreement {agree:.4f} "
+          f"(control {agree_c:.4f})")
+    assert torch.isfinite(o).all()
+    assert fro <= max(2e-2, 1.5 * fro_c), (fro, fro_c)
+    assert agree >= 1 - 1.5 * (1 - agree_c), (agree, agree_c)
 
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])

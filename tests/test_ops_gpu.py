@@ -70,6 +70,11 @@ CONV_CASES = [
     (2, 40, 32, 64, 32, 1, 1, 0, 1, True),     # pw.hip: Cout 32, 12 row groups
     (4, 19, 32, 32, 19, 1, 1, 0, 1, True),     # pw.hip: final 19->19, odd Cin (scalar lanes)
     (1, 1024, 64, 64, 16, 1, 1, 0, 1, False),  # pw.hip: two lane passes over 1024 channels
+    # persistent implicit-GEMM launches (more tiles than resident workgroups: a workgroup walks
+    # several tiles, the next tile's first K-tile DMA in flight during the epilogue):
+    (8, 128, 67, 131, 128, 3, 1, 1, 1, False),  # 549 ragged 128x128 FWD / DGRAD tiles
+    (24, 64, 161, 97, 128, 3, 2, 1, 1, False),  # stride 2, odd sizes: FWD 745 tiles; DGRAD's
+                                                # 4 parity phases of unequal rows (tile holes)
 ]
 
 
