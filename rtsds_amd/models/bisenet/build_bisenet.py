@@ -117,9 +117,6 @@ class BiSeNet(torch.nn.Module):
     # training: spatial path on runtime.branch_stream beside the context path (bs 8 train step
     # +2.5 %; at inference the fork / join edges cost more than the overlap gains)
     branch_parallel = True
-    # inference (eval): the spatial path on the branch stream too from this batch size on (the
-    # fork / join edges cost more than the overlap at batch 1); 0 = never
-    eval_branch_batch = 4
     # the spatial path starts at the fork point (an event after layer1) but is enqueued after the
     # whole context path: its autograd nodes then carry the highest sequence numbers, so the
     # engine enqueues its backward right after the fusion module's, ahead of the context path's
@@ -172,8 +169,7 @@ class BiSeNet(torch.nn.Module):
         # the 1/32 features have two readers, the context path's GAP (the tail) and ARM2's scale:
         # one gradient buffer (functional.GradJoin).  Only when ARM2 runs with autograd below.
         j4 = F.GradJoin(2) if self.training and torch.is_grad_enabled() else None
-        branch = self.training or (self.eval_branch_batch > 0 and x.shape[0] >= self.eval_branch_batch)
-        if self.branch_parallel and branch and x.is_cuda and F.CONV_PROFILE is None and branches_enabled():
+        if self.branch_parallel and self.training and x.is_cuda and F.CONV_PROFILE is None and branches_enabled():
             # (not while bench.py event-times each conv: concurrent branches would inflate them)
             # spatial path on the branch stream, concurrently with the context path (forward and,
             # through autograd's per-op streams, backward); joined before the fusion module

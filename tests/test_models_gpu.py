@@ -67,7 +67,8 @@ def _check_adam(arrays, meta, name, tensors, lr, steps):
     """Post-Adam parameters vs the reference capture.  Adam's early steps move each weight by
     ~lr*sign(m/sqrt(v)), so an element whose (near-zero) gradient has the opposite fp sign in
     the two implementations differs by up to 2*lr*steps; require that bound everywhere and
-    agreement to 2e-6 on >= 97% of the sampled elements."""
+    agreement to 2e-6 on >= 97.5% of the sampled elements (measured on MI355X: 1.96% of the 2,853 sampled
+    elements of the seg step differ, all within the 2*lr*steps bound)."""
     bad, n, worst = 0, 0, 0.0
     missing = sorted(set(meta[name]) ^ set(tensors))
     assert not missing, (name, "key sets differ", missing[:8])
@@ -83,7 +84,7 @@ def _check_adam(arrays, meta, name, tensors, lr, steps):
         n += d.size
     print(f"adam {name}: {bad} of {n} sampled elements off by > 2e-6 (frac {bad / max(n, 1):.5f}), worst {worst:.3e}")
     assert worst <= 2.05 * lr * steps, (name, worst)
-    assert bad <= 0.03 * n, (name, bad, n)
+    assert bad <= 0.025 * n, (name, bad, n)
 
 
 def _argmax_ok(got, ref_logits, rel=1e-3):
@@ -151,13 +152,25 @@ def test_bisenet_fp32_matches_oracle_and_reference(inputs, golden):
     assert mism == 0
 
 
+def _all_rounding(net):
+    """fp32-mode forward hooks rounding every submodule's floating-point output to bf16 (where
+    bf16 mode stores them)."""
+    def rnd(t):
+        return t.to(torch.bfloat16).float() if isinstance(t, torch.Tensor) and t.is_floating_point() else t
+
+    def hook(mod, args, o):
+        return tuple(rnd(t) for t in o) if isinstance(o, tuple) else rnd(o)
+    return [m.register_forward_hook(hook) for m in net.modules() if m is not net]
+
+
 def test_bisenet_bf16_close_to_oracle(inputs):
     """bf16 train-mode forward at 2 x 3 x 128 x 256 vs the oracle, bounded by a CONTROL that
     applies bf16's perturbations in fp32 arithmetic (tests/test_configs_gpu.py uses the same
     rule at the bench shape): our fp32 mode on the bf16-rounded input with bf16-rounded conv
     weights (bf16 mode reads the rounded weight shadow) and every ConvBlock / BasicBlock output
-    rounded to bf16.  The ARM BatchNorm over N=2 pooled vectors (build_bisenet.py:49) outputs
-    +-gamma+beta by the SIGN of the two images' difference, so bf16 rounding flips whole
+    rounded to bf16 -- here every module's output, not only the blocks', as this train-mode
+    forward also stores every intermediate (convolution, BatchNorm, attention) in bf16.  The
+    ARM BatchNorm over N=2 pooled vectors (build_bisenet.py:49) outputs +-gamma+beta by the SIGN of the two images' difference, so bf16 rounding flips whole
     attention channels: the network, not the kernels, sets the size of both errors (kernels:
     tests/test_ops_gpu.py).  Required: relative Frobenius error <= max(2 %, 1.5x the control's)
     and argmax agreement >= 1 - 1.5x the control's disagreement."""
@@ -172,8 +185,7 @@ def test_bisenet_bf16_close_to_oracle(inputs):
     sd = net.state_dict()
     ctl = BiSeNet(19, "resnet18").to(DEV).train()
     ctl.load_state_dict({k: (v.to(torch.bfloat16).float() if v.dim() == 4 else v) for k, v in sd.items()})
-    from tests.test_configs_gpu import _block_rounding
-    hooks = _block_rounding(ctl)
+    hooks = _all_rounding(ctl)
     with rtsds_amd.precision(torch.float32), torch.no_grad():
         oc, _, _ = ctl(x.to(torch.bfloat16).float().to(DEV))
     for h in hooks:
@@ -303,7 +315,7 @@ def test_da_iterations_match_reference_adversarial_train(inputs, golden, tmp_pat
     p0 = {k: v.detach() for k, v in list(g0.named_parameters()) + list(d0.named_parameters())}
     ours = {k: v.detach().cpu() - p0[k] for k, v in list(g.named_parameters()) + list(d.named_parameters())}
     print("DA param-update worst:", _noise_bounded(ours, upd[torch.float32], upd[torch.float64],
-                                                   "DA update", floor=1e-2))
+                                                   "DA update"))
 
 
 def test_da2_epochs_match_reference_adversarial_train_2(golden, tmp_path, monkeypatch):
@@ -357,7 +369,7 @@ def test_da2_epochs_match_reference_adversarial_train_2(golden, tmp_path, monkey
     p0 = {k: v.detach() for k, v in list(g0.named_parameters()) + list(d0.named_parameters())}
     ours = {k: v.detach().cpu() - p0[k] for k, v in list(g.named_parameters()) + list(d.named_parameters())}
     print("DA2 param-update worst:", _noise_bounded(ours, upd[torch.float32], upd[torch.float64],
-                                                    "DA2 update", floor=1e-2))
+                                                    "DA2 update"))
 
 
 @pytest.mark.parametrize("submit", ["auto", "branches", "serial", "split"])
