@@ -79,6 +79,13 @@ int rtsds_conv2d_fwd(const rtsds_conv_desc* d, const void* x, const void* w, con
 int rtsds_conv2d_fwd_bn(const rtsds_conv_desc* d, const void* x, const void* w, const float* scale,
                         const float* shift, const void* res, void* y, int act, void* ws, size_t ws_bytes,
                         void* stream);
+/* rtsds_conv2d_fwd_bn (no residual) writing y as a channel slice of a wider NHWC tensor: row
+ * pitch ldy elements (>= d->k; y 16-B aligned, ldy and d->k multiples of 8 for bf16 / 4 for f32)
+ * -- the inference spatial path writes its output straight into the fusion module's
+ * concatenated input (build_bisenet.py:153, :72).  RTSDS_ERR_UNSUPPORTED outside the
+ * implicit-GEMM route (the caller then writes a plain tensor and copies).                   */
+int rtsds_conv2d_fwd_bn_ld(const rtsds_conv_desc* d, const void* x, const void* w, const float* scale,
+                           const float* shift, void* y, long ldy, int act, void* ws, size_t ws_bytes, void* stream);
 /* Inference stem: eval conv + BatchNorm(running stats) + act + MaxPool2d(3, 2, pool_pad) in one
  * launch (torchvision ResNet conv1 -> bn1 -> relu -> maxpool, deeplabv2.py:106-110): y is the
  * pooled [n][hp][wp][k] NHWC output (hp / wp from the caller: floor or ceil mode); windows
@@ -437,7 +444,7 @@ int rtsds_graph_split_destroy(void* handle);
 /* ABI revision of this header (RTSDS_ABI_VERSION): bumped whenever an entry point's signature
  * changes.  The Python loader refuses a library whose revision differs (A/B variant libraries
  * built from older sources would otherwise be called with the wrong argument lists). */
-#define RTSDS_ABI_VERSION 6
+#define RTSDS_ABI_VERSION 7
 int rtsds_abi_version(void);
 
 #ifdef __cplusplus

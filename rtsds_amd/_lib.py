@@ -13,7 +13,7 @@ import torch  # noqa: F401  (must precede the dlopen below)
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # RTSDS_LIB: alternative in-tree build of the same ABI (kernel-variant A/B measurements)
 DEFAULT_LIB_PATH = os.path.join(_HERE, "librtsds_hip.so")
-ABI_VERSION = 6  # include/rtsds_hip.h RTSDS_ABI_VERSION
+ABI_VERSION = 7  # include/rtsds_hip.h RTSDS_ABI_VERSION
 LIB_PATH = os.environ.get("RTSDS_LIB") or DEFAULT_LIB_PATH
 
 F32, BF16 = 0, 1
@@ -46,6 +46,7 @@ SIGNATURES = {
     "rtsds_conv2d_fwd_stats_tiles": (c_int, [ctypes.POINTER(ConvDesc)]),
     "rtsds_conv2d_fwd": (c_int, [ctypes.POINTER(ConvDesc), P, P, P, P, c_int, P, P, c_size_t, P]),
     "rtsds_conv2d_fwd_bn": (c_int, [ctypes.POINTER(ConvDesc), P, P, P, P, P, P, c_int, P, c_size_t, P]),
+    "rtsds_conv2d_fwd_bn_ld": (c_int, [ctypes.POINTER(ConvDesc), P, P, P, P, P, c_long, c_int, P, c_size_t, P]),
     "rtsds_conv2d_fwd_bn_maxpool": (c_int, [ctypes.POINTER(ConvDesc), P, P, P, P, P, c_int, c_int, c_int, c_int, P,
                                             c_size_t, P]),
     "rtsds_conv2d_dgrad_workspace": (c_size_t, [ctypes.POINTER(ConvDesc)]),

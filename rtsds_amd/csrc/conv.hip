@@ -782,6 +782,35 @@ extern "C" int rtsds_conv2d_fwd_bn(const rtsds_conv_desc* d0, const void* x, con
   return hipGetLastError() == hipSuccess ? RTSDS_OK : RTSDS_ERR_LAUNCH;
 }
 
+extern "C" int rtsds_conv2d_fwd_bn_ld(const rtsds_conv_desc* d0, const void* x, const void* w, const float* scale,
+                                      const float* shift, void* y, long ldy, int act, void* ws, size_t ws_bytes,
+                                      void* stream) {
+  if (!scale || !shift || (act & RTSDS_ACCUMULATE)) return RTSDS_ERR_UNSUPPORTED;
+  int e = check_desc(d0);
+  if (e) return e;
+  if (ldy == d0->k) return rtsds_conv2d_fwd_bn(d0, x, w, scale, shift, nullptr, y, act, ws, ws_bytes, stream);
+  // a channel slice of a wider NHWC tensor: the implicit-GEMM route with 16-B row chunks only
+  const int vec = 16 / esize(d0->dtype);
+  if (ldy < d0->k || ldy % vec || d0->k % vec || ((uintptr_t)y & 15) || ldy > (1L << 30)) return RTSDS_ERR_UNSUPPORTED;
+  if (pooled_1x1(d0) || tapconv_ok(d0) || hconv_ok(d0) || imgconv_ok(d0)) return RTSDS_ERR_UNSUPPORTED;
+  if (ws_bytes < rtsds_conv2d_fwd_workspace(d0)) return RTSDS_ERR_WORKSPACE;
+  const bool x_padded = (act & RTSDS_INPUT_PADDED) != 0;
+  if (x_padded && input_pitch(d0) == d0->c) return RTSDS_ERR_UNSUPPORTED;
+  hipStream_t st = (hipStream_t)stream;
+  rtsds_conv_desc d;
+  fwd_prepare(d0, x, w, ws, d, st, x_padded);
+  ConvArgs p = make_args(&d);
+  p.a = x; p.b = w; p.bias = shift; p.scale = scale; p.res = nullptr; p.out = y;
+  p.act = act & 0xff;
+  p.ldo = (int)ldy;
+  p.M = d.n * d.ho * d.wo;
+  p.N = d.k;
+  p.K = d.kh * d.kw * d.c;
+  if (d.dtype == RTSDS_BF16) dispatch_align<bf16, MODE_FWD>(p, d.c, st);
+  else dispatch_align<float, MODE_FWD>(p, d.c, st);
+  return hipGetLastError() == hipSuccess ? RTSDS_OK : RTSDS_ERR_LAUNCH;
+}
+
 extern "C" int rtsds_conv2d_fwd_bn_maxpool(const rtsds_conv_desc* d0, const void* x, const void* w, const float* scale,
                                            const float* shift, void* y, int act, int hp, int wp, int pool_pad, void* ws,
                                            size_t ws_bytes, void* stream) {

@@ -42,6 +42,9 @@ struct ConvArgs {
   // layout as y (or null).
   const float* scale;
   const void* res;
+  // FWD: row pitch of y in elements when y is a channel slice of a wider NHWC tensor (0 = N);
+  // plain forward only (no residual / accumulate), checked by the host
+  int ldo;
   int gbuf;           // operand tensors < 2 GiB: buffer-resource DMA with 32-bit offsets allowed
   // DGRAD stride-2: the parity phases of one conv in ONE launch (blockIdx.z = phase); each
   // phase patches the phase-dependent fields below over the shared ones.

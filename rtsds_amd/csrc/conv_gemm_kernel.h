@@ -1121,7 +1121,7 @@ conv_gemm_kernel(const ConvArgs P0) {
           const int row = c / CPR, cc = c - row * CPR;
           const int gm = m0 + row, gn = n0 + cc * V;
           if (gm < P.M && gn < P.N) {
-            const long o = out_row(gm) * P.N + gn;
+            const long orow = out_row(gm), o = orow * P.N + gn;
             V16 v = *(const V16*)(cs + row * CP + cc * V);
             if (post) {
               float f[V];
@@ -1145,7 +1145,7 @@ conv_gemm_kernel(const ConvArgs P0) {
 #pragma unroll
               for (int q = 0; q < V; ++q) v[q] = from_f<T>(act_f(f[q]));
             }
-            *(V16*)(out + o) = v;
+            *(V16*)(out + (P.ldo ? orow * P.ldo + gn : o)) = v;  // (ldo: plain forward only, host-checked)
             if (MODE == MODE_DGRAD && bnb) {
 #pragma unroll
               for (int q = 0; q < V; ++q) {
@@ -1212,7 +1212,7 @@ conv_gemm_kernel(const ConvArgs P0) {
             if (has_mask) v = mask_f(to_f(from_f<T>(v)), to_f(((const T*)P.mask)[orow * P.N + gn]));
             if (has_res) v += to_f(((const T*)P.res)[orow * P.N + gn]);
             if (P.accum) v += to_f(out[orow * P.N + gn]);
-            out[orow * P.N + gn] = from_f<T>(act_f(v));
+            out[orow * (P.ldo ? P.ldo : P.N) + gn] = from_f<T>(act_f(v));
           }
       }
     }

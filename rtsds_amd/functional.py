@@ -388,11 +388,14 @@ def _bn_fold(gamma, beta, running_mean, running_var, bias, eps, k):
 
 
 def conv_bn_eval(x, weight, bias, wq, stride, padding, dilation, gamma, beta, running_mean, running_var,
-                 eps, act=0, residual=None):
+                 eps, act=0, residual=None, out=None):
     """Inference (no autograd) conv -> BatchNorm(running statistics) [-> + residual] [-> act]
     as ONE implicit-GEMM launch: the BN is folded into a per-channel scale / shift of the conv
     epilogue (rtsds_bn_fold + rtsds_conv2d_fwd_bn).  Same function as the unfused
-    conv2d -> batch_norm(training=False) chain, with the BN applied to the fp32 accumulators."""
+    conv2d -> batch_norm(training=False) chain, with the BN applied to the fp32 accumulators.
+    ``out = (buf, off)``: write y straight into channels [off, off + k) of the wider NHWC
+    tensor ``buf`` (rtsds_conv2d_fwd_bn_ld) and return that slice as a view; where the kernel
+    route does not support it, a plain y is returned (the caller copies)."""
     require_hip(x, weight)
     k, _, kh, kw = weight.shape
     flag = INPUT_PADDED if hasattr(x, "_rt_cpad") and \
@@ -405,8 +408,21 @@ def conv_bn_eval(x, weight, bias, wq, stride, padding, dilation, gamma, beta, ru
         residual = nhwc(residual)
         if residual.dtype != x.dtype or tuple(residual.shape) != (d.n, k, d.ho, d.wo):
             raise RuntimeError("rtsds_amd.conv_bn_eval: residual must match the conv output")
-    y = empty_nhwc(d.n, k, d.ho, d.wo, x.dtype, x.device)
     ws = workspace(lib.rtsds_conv2d_fwd_workspace(ctypes.byref(d)), x.device)
+    if out is not None and residual is None:
+        buf, off = out
+        if tuple(buf.shape[2:]) == (d.ho, d.wo) and buf.shape[0] == d.n and buf.dtype == x.dtype and \
+                0 <= off and off + k <= buf.shape[1] and buf.stride(1) == 1 and buf.stride(3) == buf.shape[1]:
+            try:
+                with _Timed(d, "fwd"):
+                    lib.rtsds_conv2d_fwd_bn_ld(ctypes.byref(d), _P(x), _P(wq), _P(ss), ss.data_ptr() + 4 * k,
+                                               buf.data_ptr() + off * buf.element_size(), buf.shape[1], act | flag,
+                                               _P(ws), ws.numel(), stream())
+                return buf[:, off:off + k]
+            except RuntimeError as e:
+                if "unsupported" not in str(e):
+                    raise
+    y = empty_nhwc(d.n, k, d.ho, d.wo, x.dtype, x.device)
     with _Timed(d, "fwd"):
         lib.rtsds_conv2d_fwd_bn(ctypes.byref(d), _P(x), _P(wq), _P(ss), ss.data_ptr() + 4 * k, _P(residual), _P(y),
                                 act | flag, _P(ws), ws.numel(), stream())
@@ -774,12 +790,16 @@ def concat_resized(x0, xs, size):
     return CatResizeFn.apply((int(size[0]), int(size[1])), x0, *xs)
 
 
-def concat_resized_scaled_eval(x0, parts, size):
+def concat_resized_scaled_eval(x0, parts, size, into=None):
     """Inference only: concat_resized(x0, [channel_scale(...channel_scale(x, s1)..., sk) for
     (x, (s1, ...)) in parts], size) with the (at most two) channel scales applied to the resize's
     taps (rtsds_bilinear_fwd_scaled; bit-identical to the separate ops).  None when a part's
-    geometry is outside the fused kernel (the caller then runs the separate ops)."""
-    x0 = nhwc(x0)
+    geometry is outside the fused kernel (the caller then runs the separate ops).  ``into``: the
+    preallocated output; x0 is not copied when it already is its leading channel slice (the
+    spatial path's conv wrote it there, conv_bn_eval(out=...))."""
+    in_place = into is not None and x0.data_ptr() == into.data_ptr() and x0.stride() == into.stride()
+    if not in_place:
+        x0 = nhwc(x0)
     n, c0, h, w = x0.shape
     ps = []
     for x, scales in parts:
@@ -789,7 +809,10 @@ def concat_resized_scaled_eval(x0, parts, size):
         ss = [(s if s.dtype == x.dtype else cast(s, x.dtype)).contiguous() for s in scales]
         ps.append((x, ss + [None] * (2 - len(ss))))
     ct = c0 + sum(x.shape[1] for x, _ in ps)
-    y = empty_nhwc(n, ct, h, w, x0.dtype, x0.device)
+    if into is not None and tuple(into.shape) == (n, ct, h, w) and into.dtype == x0.dtype:
+        y = into
+    else:
+        y, in_place = empty_nhwc(n, ct, h, w, x0.dtype, x0.device), False
     off = c0
     for x, (s1, s2) in ps:
         _, c, hi, wi = x.shape
@@ -801,7 +824,8 @@ def concat_resized_scaled_eval(x0, parts, size):
                 return None
             raise
         off += c
-    lib.rtsds_copy_channels(_P(x0), c0, 0, _P(y), ct, 0, n * h * w, c0, 0, dcode(x0), stream())
+    if not in_place:
+        lib.rtsds_copy_channels(_P(x0), c0, 0, _P(y), ct, 0, n * h * w, c0, 0, dcode(x0), stream())
     return y
 
 

@@ -28,8 +28,9 @@ class ConvBlock(torch.nn.Module):
         self.bn = BatchNorm2d(out_channels)
         self.relu = ReLU()
 
-    def forward(self, input):
-        return conv_bn(self.conv1, self.bn, input, "relu")
+    def forward(self, input, out=None):
+        """``out``: inference only, a destination channel slice (nn.conv_bn)."""
+        return conv_bn(self.conv1, self.bn, input, "relu", out=out)
 
 
 class Spatial_path(torch.nn.Module):
@@ -41,8 +42,8 @@ class Spatial_path(torch.nn.Module):
         self.convblock2 = ConvBlock(in_channels=64, out_channels=128)
         self.convblock3 = ConvBlock(in_channels=128, out_channels=256)
 
-    def forward(self, input):
-        return self.convblock3(self.convblock2(self.convblock1(input)))
+    def forward(self, input, out=None):
+        return self.convblock3(self.convblock2(self.convblock1(input)), out=out)
 
 
 class AttentionRefinementModule(torch.nn.Module):
@@ -128,6 +129,9 @@ class BiSeNet(torch.nn.Module):
     inference_fusions = True
     # forward() starts with nn.to_input: runtime.GraphedForward may capture from the packed input
     accepts_packed_input = True
+    # inference: the spatial path's last conv writes straight into the fusion module's
+    # concatenated input (no copy of the 256-channel map)
+    spatial_into_concat = True
 
     def __init__(self, num_classes, context_path, with_interpolation=True):
         super().__init__()
@@ -198,7 +202,15 @@ class BiSeNet(torch.nn.Module):
             main.wait_stream(side)
             sx.record_stream(main)
         else:
-            sx = self.saptial_path(x)
+            into = None
+            if self.spatial_into_concat and self.inference_fusions and not self.training and \
+                    not torch.is_grad_enabled() and x.is_cuda:
+                # the fusion module's input, allocated before the spatial path writes its slice
+                h8, w8 = x.shape[-2], x.shape[-1]
+                for _ in range(3):  # three 3x3 stride-2 pad-1 convs
+                    h8, w8 = (h8 - 1) // 2 + 1, (w8 - 1) // 2 + 1
+                into = F.empty_nhwc(x.shape[0], self.feature_fusion_module.in_channels, h8, w8, x.dtype, x.device)
+            sx = self.saptial_path(x, out=None if into is None else (into, 0))
             f3, f4, tail = self.context_path(x, tail_join=j4)
         hw = sx.shape[-2:]
         heads = []
@@ -211,7 +223,7 @@ class BiSeNet(torch.nn.Module):
             # interpolate, interpolate, cat); ARM2's global average pool is the tail itself
             att1 = self.attention_refinement_module1.attention(f3)
             att2 = self.attention_refinement_module2.attention(f4, pooled=tail)
-            cat = F.concat_resized_scaled_eval(sx, ((f3, (att1,)), (f4, (att2, tail))), hw)
+            cat = F.concat_resized_scaled_eval(sx, ((f3, (att1,)), (f4, (att2, tail))), hw, into=into)
         if cat is None:
             cx1 = self.attention_refinement_module1(f3)
             # ARM2's global average pool is the tail itself (same kernel, same f4)

@@ -127,7 +127,7 @@ def _no_grad_needed(conv, bn, x, residual):
     return not any(t is not None and t.requires_grad for t in ts)
 
 
-def conv_bn(conv, bn, x, act=None, residual=None, join=None, res_join=None, in_link=None, out_link=None):
+def conv_bn(conv, bn, x, act=None, residual=None, join=None, res_join=None, in_link=None, out_link=None, out=None):
     """bn(conv(x)) with the BatchNorm's batch statistics produced by the conv epilogue
     (train mode) instead of a separate pass over the conv output.  Eval mode without
     autograd (inference, validation): the BN (+ residual + act) folds into the conv's
@@ -135,12 +135,13 @@ def conv_bn(conv, bn, x, act=None, residual=None, join=None, res_join=None, in_l
     functional.GradJoin shared by the readers of ``x`` / ``residual`` (residual blocks).
     ``in_link``: functional.BnBwdLink of the BatchNorm that produced ``x`` (its backward
     statistics come from this conv's data gradient); ``out_link``: the link this BatchNorm
-    registers with (its output's single reader passes it as ``in_link``)."""
+    registers with (its output's single reader passes it as ``in_link``).  ``out``: inference
+    only, a destination channel slice (functional.conv_bn_eval)."""
     use_batch = bn.training or not bn.track_running_stats
     if not use_batch and bn.momentum is not None and _no_grad_needed(conv, bn, x, residual):
         wq = _shadow(conv.weight, x.dtype)
         return F.conv_bn_eval(x, conv.weight, conv.bias, wq, conv.stride, conv.padding, conv.dilation,
-                              bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.eps, ACT[act], residual)
+                              bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.eps, ACT[act], residual, out=out)
     return bn(conv(x, bn_stats=use_batch, join=join, bn_link=in_link), act=act, residual=residual, res_join=res_join,
               link=out_link)
 

@@ -443,8 +443,8 @@ def test_bisenet_bench_inference_bf16_blockwise(eval_state):
         rec["att1" if self is net.attention_refinement_module1 else "att2"] = ((keep(t), keep(pooled)), keep(o))
         return o
 
-    def cat(x0, parts, size):
-        o = orig["cat"](x0, parts, size)
+    def cat(x0, parts, size, into=None):
+        o = orig["cat"](x0, parts, size, into=into)
         rec["concat"] = ((keep(x0), keep(parts), size), keep(o))
         return o
 

@@ -822,6 +822,32 @@ def test_conv_bn_eval_fold(case, dt):
 
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("geo", [(2, 128, 32, 64, 256, 3, 2, 1, 1024, 0),   # the spatial path's conv3 into the FFM input
+                                 (2, 64, 16, 24, 64, 3, 2, 1, 96, 32),      # 64 x 64 tiles, offset slice
+                                 (1, 32, 9, 13, 32, 3, 2, 1, 40, 8)])       # ragged M tiles
+def test_conv_bn_eval_into_slice(geo, dt):
+    """conv_bn_eval(out=(buf, off)) -- rtsds_conv2d_fwd_bn_ld, the row-pitched epilogue --
+    writes exactly the plain conv_bn_eval result into channels [off, off + k) of the wider
+    tensor and leaves the other channels untouched."""
+    n, c, h, w, k, kh, s, p, ct, off = geo
+    g = torch.Generator().manual_seed(12)
+    x = _dev(torch.randn(n, c, h, w, generator=g), dt)
+    wt = (torch.randn(k, c, kh, kh, generator=g) / (c * kh * kh) ** 0.5).to(DEV).contiguous(memory_format=CL)
+    rm, rv = torch.randn(k, generator=g).to(DEV), (0.5 + torch.rand(k, generator=g)).to(DEV)
+    gam, bet = torch.randn(k, generator=g).to(DEV), torch.randn(k, generator=g).to(DEV)
+    args = (wt, None, _shadow(wt, dt), (s, s), (p, p), (1, 1), gam, bet, rm, rv, 1e-5, 1)
+    with torch.no_grad():
+        ref = F.conv_bn_eval(x, *args)
+        buf = _dev(torch.randn(n, ct, ref.shape[2], ref.shape[3], generator=g), dt)
+        before = buf.clone()
+        got = F.conv_bn_eval(x, *args, out=(buf, off))
+    torch.cuda.synchronize()
+    assert got.data_ptr() == buf.data_ptr() + off * buf.element_size()
+    assert torch.equal(buf[:, off:off + k], ref)
+    assert torch.equal(buf[:, :off], before[:, :off]) and torch.equal(buf[:, off + k:], before[:, off + k:])
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 def test_bisenet_eval_fold_and_graph(dt):
     """BiSeNet eval forward: folded conv+BN path == unfused path (autograd-enabled eval), and a
     hipGraph replay (runtime.GraphedForward) == eager."""
