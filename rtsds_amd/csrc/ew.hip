@@ -913,46 +913,59 @@ __global__ void bilinear_fwd_kernel(const T* __restrict__ x, T* __restrict__ y, 
 // [n][c]): channel scales applied to each tap first, rounded to T after each as the stored
 // rtsds_chscale_fwd outputs would be (BiSeNet's attention refinement, build_bisenet.py:42-53,
 // 157-159, folded into the eval forward's resize: bit-identical to scale, scale, resize).
-template <typename T>
-__global__ void bilinear_fwd_group_vec_kernel(const T* __restrict__ x, T* __restrict__ y, int n, int hi, int wi, int c, int ho,
-                                              int wo, float sh, float sw, int yld, int yoff, const T* __restrict__ s1,
-                                              const T* __restrict__ s2) {
+template <typename T, int U>
+__global__ void __launch_bounds__(256) bilinear_fwd_group_vec_kernel(const T* __restrict__ x, T* __restrict__ y, int n, int hi,
+                                                                     int wi, int c, int ho, int wo, float sh, float sw, int yld,
+                                                                     int yoff, const T* __restrict__ s1, const T* __restrict__ s2) {
   constexpr int V = VecT<T>::N;
   typedef typename VecT<T>::v16 V16;
-  // grid (column-vector blocks, n * hi): the source row and its output rows are block-uniform
-  const int cpp = c / V;
+  // grid (column-vector blocks, n * hi): the source row and its output rows are block-uniform.
+  // A thread takes U column vectors gridDim.x * 256 apart and issues all their tap loads before
+  // any arithmetic (U x 4 loads in flight instead of 4 per thread-lifetime).
+  const int cpp = c / V, nv = wo * cpp;
   const int img = blockIdx.y / hi, h0 = blockIdx.y - img * hi;
   const int oa = bil_first_ge(h0, sh, hi, ho), ob = bil_first_ge(h0 + 1, sh, hi, ho);
   const int h1 = h0 + (h0 < hi - 1 ? 1 : 0);
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  if (oa >= ob || i >= wo * cpp) return;
-  {
+  if (oa >= ob) return;
+  const int i0 = blockIdx.x * 256 + threadIdx.x, step = gridDim.x * 256;
+  const T* xb = x + (long)img * hi * wi * c;
+  V16 a[U], bb[U], cc[U], dd[U], k1[U], k2[U];
+  float lw0[U], lw1[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int i = min(i0 + u * step, nv - 1);  // clamped: unconditional loads
     const int ow = i / cpp, chunk = i - ow * cpp;
     int w0, w1;
-    float lw0, lw1;
-    bil_src(ow, sw, wi, w0, w1, lw0, lw1);
-    const T* b = x + (long)img * hi * wi * c + chunk * V;
-    const V16 a = *(const V16*)(b + ((long)h0 * wi + w0) * c), bb = *(const V16*)(b + ((long)h0 * wi + w1) * c);
-    const V16 cc = *(const V16*)(b + ((long)h1 * wi + w0) * c), dd = *(const V16*)(b + ((long)h1 * wi + w1) * c);
-    V16 k1, k2;
-    if (s1) k1 = *(const V16*)(s1 + (long)img * c + chunk * V);
-    if (s2) k2 = *(const V16*)(s2 + (long)img * c + chunk * V);
+    bil_src(ow, sw, wi, w0, w1, lw0[u], lw1[u]);
+    const T* b = xb + chunk * V;
+    a[u] = *(const V16*)(b + ((long)h0 * wi + w0) * c);
+    bb[u] = *(const V16*)(b + ((long)h0 * wi + w1) * c);
+    cc[u] = *(const V16*)(b + ((long)h1 * wi + w0) * c);
+    dd[u] = *(const V16*)(b + ((long)h1 * wi + w1) * c);
+    if (s1) k1[u] = *(const V16*)(s1 + (long)img * c + chunk * V);
+    if (s2) k2[u] = *(const V16*)(s2 + (long)img * c + chunk * V);
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int i = i0 + u * step;
+    if (i >= nv) break;
+    const int ow = i / cpp, chunk = i - ow * cpp;
     auto tap = [&](T v, int j) {
       float f = to_f(v);
-      if (s1) f = to_f(from_f<T>(f * to_f(k1[j])));
-      if (s2) f = to_f(from_f<T>(f * to_f(k2[j])));
+      if (s1) f = to_f(from_f<T>(f * to_f(k1[u][j])));
+      if (s2) f = to_f(from_f<T>(f * to_f(k2[u][j])));
       return f;
     };
     float t0[V], t1[V];
 #pragma unroll
     for (int j = 0; j < V; ++j) {
-      t0[j] = fmaf(lw1, tap(bb[j], j), lw0 * tap(a[j], j));
-      t1[j] = fmaf(lw1, tap(dd[j], j), lw0 * tap(cc[j], j));
+      t0[j] = fmaf(lw1[u], tap(bb[u][j], j), lw0[u] * tap(a[u][j], j));
+      t1[j] = fmaf(lw1[u], tap(dd[u][j], j), lw0[u] * tap(cc[u][j], j));
     }
     for (int oh = oa; oh < ob; ++oh) {
-      int i0, i1;
+      int i0_, i1_;
       float lh0, lh1;
-      bil_src(oh, sh, hi, i0, i1, lh0, lh1);
+      bil_src(oh, sh, hi, i0_, i1_, lh0, lh1);
       V16 r;
 #pragma unroll
       for (int j = 0; j < V; ++j) r[j] = from_f<T>(fmaf(lh1, t1[j], lh0 * t0[j]));
@@ -1079,6 +1092,7 @@ __global__ void __launch_bounds__(256) bilinear_fwd_rowgroup_kernel(const T* __r
 }
 
 static const bool kBilRowGroup = true;
+static constexpr auto kBilGroupU = 4;  // column vectors per thread of bilinear_fwd_group_vec_kernel (1 / 2 / 4: 48 / 43 / 41 us, profiles/r6f)
 static constexpr auto kBilJ = 2;  // output vectors per thread and column chunk (2, 3, 4, 6 measured: 2 best)
 
 // Backward, separable gather (deterministic, no atomics): input index i along one axis
@@ -1300,8 +1314,8 @@ extern "C" int rtsds_bilinear_fwd(const void* x, void* y, int n, int hi, int wi,
     // grouped taps pay off from ~3 output rows per source row (x2: 24 vs 17 us at 256 ch, x4:
     // 26 vs 28 us, tools/ab_bilinear.sh)
     if (c % V == 0 && y_ld % V == 0 && y_off % V == 0 && ho >= 3 * hi && kBilRowGroup)
-      hipLaunchKernelGGL((bilinear_fwd_group_vec_kernel<T>), dim3(rt_cdiv(wo * (c / V), 256), n * hi), dim3(256), 0, st,
-                         (const T*)x, (T*)y, n, hi, wi, c, ho, wo, scale_h, scale_w, y_ld, y_off, nullptr, nullptr);
+      hipLaunchKernelGGL((bilinear_fwd_group_vec_kernel<T, kBilGroupU>), dim3(rt_cdiv(wo * (c / V), 256 * kBilGroupU), n * hi),
+                         dim3(256), 0, st, (const T*)x, (T*)y, n, hi, wi, c, ho, wo, scale_h, scale_w, y_ld, y_off, nullptr, nullptr);
     else if (c % V == 0 && y_ld % V == 0 && y_off % V == 0)
       hipLaunchKernelGGL((bilinear_fwd_kernel<T, 0>), dim3(ew_blocks(pix * (c / V))), dim3(256), 0, st, (const T*)x, (T*)y, n, hi, wi, c, ho, wo, scale_h, scale_w, y_ld, y_off);
     else if (c >= V && y_ld == c && y_off == 0 && (wo * c) % V == 0 && 2L * wi * c * 4 <= 64 * 1024 && ho >= hi && kBilRowGroup) {
@@ -1332,8 +1346,9 @@ extern "C" int rtsds_bilinear_fwd_scaled(const void* x, const void* s1, const vo
   DISPATCH_T(dtype, {
     constexpr int V = VecT<T>::N;
     if (!(c % V == 0 && y_ld % V == 0 && y_off % V == 0 && ho >= hi)) return RTSDS_ERR_UNSUPPORTED;
-    hipLaunchKernelGGL((bilinear_fwd_group_vec_kernel<T>), dim3(rt_cdiv(wo * (c / V), 256), n * hi), dim3(256), 0, st,
-                       (const T*)x, (T*)y, n, hi, wi, c, ho, wo, scale_h, scale_w, y_ld, y_off, (const T*)s1, (const T*)s2);
+    hipLaunchKernelGGL((bilinear_fwd_group_vec_kernel<T, kBilGroupU>), dim3(rt_cdiv(wo * (c / V), 256 * kBilGroupU), n * hi),
+                       dim3(256), 0, st, (const T*)x, (T*)y, n, hi, wi, c, ho, wo, scale_h, scale_w, y_ld, y_off, (const T*)s1,
+                       (const T*)s2);
   });
   RET_LAUNCH();
 }
