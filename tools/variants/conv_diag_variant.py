@@ -1,5 +1,4 @@
-"""Build diagnostic variants of the implicit-GEMM conv kernels (out of tree; csrc/ keeps no
-diagnostic macros).  Each variant rewrites a temporary copy of csrc/conv_gemm_kernel.h:
+"""Diagnostic variants of the implicit-GEMM conv kernels (out of tree, tools/variants/textvariant.py):
 
   nogather  every LDS-DMA of the buffer-resource paths (FWD / DGRAD tap-aligned tiles, WGRAD
             whole-row tiles) reads the same 8 KB at the start of its operand instead of the
@@ -12,14 +11,10 @@ diagnostic macros).  Each variant rewrites a temporary copy of csrc/conv_gemm_ke
 usage: python3 tools/variants/conv_diag_variant.py NAME [NAME ...]  ->  rtsds_amd/var_diag_NAME.so
 """
 import os
-import shutil
-import subprocess
 import sys
 
-ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-CSRC = os.path.join(ROOT, "rtsds_amd", "csrc")
-HIPCC = "/opt/rocm/bin/hipcc"
-FLAGS = ["-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-Wno-unused-function", "-Wno-unused-variable"]
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from textvariant import build  # noqa: E402
 
 SMALL = "((((i) * (8 * NW) + wave * 8 + (lane >> 3)) & 63) * 128 + (lane & 7) * 16)"
 EDITS = {
@@ -41,42 +36,6 @@ EDITS = {
 }
 EDITS["both"] = EDITS["nogather"] + EDITS["noepi"]
 
-
-def build(name):
-    tmp = os.path.join(CSRC, "build", "diag_" + name)
-    shutil.rmtree(tmp, ignore_errors=True)
-    src = os.path.join(tmp, "x", "src")  # common.h includes ../../include/rtsds_hip.h
-    os.makedirs(src)
-    os.makedirs(os.path.join(tmp, "include"))
-    shutil.copy(os.path.join(ROOT, "include", "rtsds_hip.h"), os.path.join(tmp, "include"))
-    for f in os.listdir(CSRC):
-        if f.endswith((".h", ".hip")):
-            shutil.copy(os.path.join(CSRC, f), os.path.join(src, f))
-    hdr = os.path.join(src, "conv_gemm_kernel.h")
-    text = open(hdr).read()
-    for old, new in EDITS[name]:
-        n = text.count(old)
-        if n != 1:
-            raise SystemExit(f"{name}: pattern found {n} times: {old[:60]}")
-        text = text.replace(old, new)
-    open(hdr, "w").write(text)
-    objs = []
-    procs = []
-    for unit in ("conv_gemm_fwd", "conv_gemm_dgrad", "conv_gemm_wgrad"):
-        o = os.path.join(tmp, unit + ".o")
-        procs.append(subprocess.Popen([HIPCC, *FLAGS, "-c", os.path.join(src, unit + ".hip"), "-o", o]))
-        objs.append(o)
-    for p in procs:
-        if p.wait() != 0:
-            raise SystemExit(f"{name}: compile failed")
-    for f in os.listdir(os.path.join(CSRC, "build")):
-        if f.endswith(".o") and not f.startswith("conv_gemm_"):
-            objs.append(os.path.join(CSRC, "build", f))
-    out = os.path.join(ROOT, "rtsds_amd", f"var_diag_{name}.so")
-    subprocess.check_call([HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", out, *objs])
-    print("built", out)
-
-
 if __name__ == "__main__":
     for n in sys.argv[1:]:
-        build(n)
+        build("diag_" + n, {"conv_gemm_kernel.h": EDITS[n]}, ["conv_gemm_fwd", "conv_gemm_dgrad", "conv_gemm_wgrad"])
