@@ -254,13 +254,15 @@ int rtsds_gap_bwd(const void* dy, void* dx, int n, long hw, int c, int accumulat
  * mode 0: y = x*a[n][c] (build_bisenet.py:52,149); mode 1: y = x*a + x (build_bisenet.py:79-80).
  * Backward: dx (may be NULL), da[n][c] = sum_hw dy*x (may be NULL; needs
  * ws = rtsds_gap_workspace(n, hw, c) bytes).                                              */
-/* Inference tail of FeatureFusionModule + the final 1x1 conv (build_bisenet.py:75-80, 167), one
- * launch: out = conv3(f * a + f) + b3 with a = sigmoid(conv2(relu(conv1(GAP(f)) + b1)) + b2);
+/* Inference tail of FeatureFusionModule + the final 1x1 conv (build_bisenet.py:75-80, 167), two
+ * launches: out = conv3(f * a + f) + b3 with a = sigmoid(conv2(relu(conv1(GAP(f)) + b1)) + b2);
  * f / out NHWC [n][hw][c] (c = 19 -- the class maps -- and hw a multiple of the 16-B vector length,
- * else RTSDS_ERR_UNSUPPORTED); w1..w3 [c][c] in the compute dtype, biases fp32 (NULL = 0).     */
+ * else RTSDS_ERR_UNSUPPORTED); w1..w3 [c][c] in the compute dtype, biases fp32 (NULL = 0).  Needs
+ * ws >= rtsds_ffm_head_eval_workspace(n, hw, c) bytes (the GAP partials).                     */
+size_t rtsds_ffm_head_eval_workspace(int n, long hw, int c);
 int rtsds_ffm_head_eval(const void* f, const void* w1, const float* b1, const void* w2, const float* b2,
-                        const void* w3, const float* b3, void* out, int n, long hw, int c, int dtype,
-                        void* stream);
+                        const void* w3, const float* b3, void* out, int n, long hw, int c, int dtype, void* ws,
+                        size_t ws_bytes, void* stream);
 int rtsds_chscale_fwd(const void* x, const void* a, void* y, int n, long hw, int c, int mode,
                       int dtype, void* stream);
 int rtsds_chscale_bwd(const void* dy, const void* x, const void* a, void* dx, void* da, int n,
@@ -444,7 +446,7 @@ int rtsds_graph_split_destroy(void* handle);
 /* ABI revision of this header (RTSDS_ABI_VERSION): bumped whenever an entry point's signature
  * changes.  The Python loader refuses a library whose revision differs (A/B variant libraries
  * built from older sources would otherwise be called with the wrong argument lists). */
-#define RTSDS_ABI_VERSION 7
+#define RTSDS_ABI_VERSION 8
 int rtsds_abi_version(void);
 
 #ifdef __cplusplus

@@ -13,7 +13,7 @@ import torch  # noqa: F401  (must precede the dlopen below)
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # RTSDS_LIB: alternative in-tree build of the same ABI (kernel-variant A/B measurements)
 DEFAULT_LIB_PATH = os.path.join(_HERE, "librtsds_hip.so")
-ABI_VERSION = 7  # include/rtsds_hip.h RTSDS_ABI_VERSION
+ABI_VERSION = 8  # include/rtsds_hip.h RTSDS_ABI_VERSION
 LIB_PATH = os.environ.get("RTSDS_LIB") or DEFAULT_LIB_PATH
 
 F32, BF16 = 0, 1
@@ -76,7 +76,8 @@ SIGNATURES = {
     "rtsds_nchw_to_nhwc": (c_int, [P, P, c_int, c_int, c_int, c_int, c_int, P]),
     "rtsds_nchw_to_nhwc_pad": (c_int, [P, P, c_int, c_int, c_int, c_int, c_int, c_int, P]),
     "rtsds_cast": (c_int, [P, c_int, P, c_int, c_long, P]),
-    "rtsds_ffm_head_eval": (c_int, [P, P, P, P, P, P, P, P, c_int, c_long, c_int, c_int, P]),
+    "rtsds_ffm_head_eval_workspace": (c_size_t, [c_int, c_long, c_int]),
+    "rtsds_ffm_head_eval": (c_int, [P, P, P, P, P, P, P, P, c_int, c_long, c_int, c_int, P, c_size_t, P]),
     "rtsds_graph_split": (c_int, [P, c_int, P, P, P]),
     "rtsds_graph_split_launch": (c_int, [P, P]),
     "rtsds_graph_lanes": (c_int, [P, c_int]),

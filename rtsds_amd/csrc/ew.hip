@@ -676,25 +676,26 @@ extern "C" int rtsds_chscale_fwd(const void* x, const void* a, void* y, int n, l
 // 167): a = sigmoid(conv2(relu(conv1(GAP(f))))), r = f * a + f, out = conv(r) + bias, for a
 // narrow class map f [N][hw][C] (C <= 32).  Unfused these are 8 launches (two-stage GAP, two
 // pooled 1x1 convs, the channel scale, two channel pads and the padded GEMM: ~54 us at bs 8,
-// all launch-bound).  Grid (chunks, N): every workgroup reduces its image's GAP itself (the
-// image's map is ~0.3 MB, L2-resident) with 16-B loads of V-pixel groups (C vectors whose
-// element -> channel map is static), evaluates the two pooled convs in LDS, then stages its
-// chunk of pixels in LDS (coalesced 16-B loads), maps each pixel in place (one pixel per
-// thread, the C x C head weights in LDS) and writes the chunk back with 16-B stores.  Each
-// intermediate is rounded to T where the unfused chain stores it.
+// all launch-bound).  Two launches here: (1) chan_part_kernel's GAP partials over FFM_CHUNK-pixel
+// slices of each image; (2) grid (slices, N): every workgroup sums its image's partials in slice
+// order, evaluates the two pooled convs in LDS, stages its slice of pixels in LDS (coalesced 16-B
+// loads), maps each pixel in place (one pixel per thread, the C x C head weights in LDS) and writes
+// the slice back with 16-B stores.  (One launch whose 64 workgroups each re-read their whole image
+// for the GAP ran one wave per CU through the 19 x 19 per-pixel maps: 21.7 us.)  Each intermediate
+// is rounded to T where the unfused chain stores it.
+static constexpr int kFfmChunk = 256;  // pixels per slice / workgroup
 template <typename T, int C>
-__global__ void __launch_bounds__(256) ffm_head_eval_kernel(const T* __restrict__ f, const T* __restrict__ w1,
-                                                            const float* __restrict__ b1, const T* __restrict__ w2,
-                                                            const float* __restrict__ b2, const T* __restrict__ w3,
-                                                            const float* __restrict__ b3, T* __restrict__ out, int hw, int chunk) {
+__global__ void __launch_bounds__(256) ffm_head_apply_kernel(const float* __restrict__ part, const T* __restrict__ f,
+                                                             const T* __restrict__ w1, const float* __restrict__ b1,
+                                                             const T* __restrict__ w2, const float* __restrict__ b2,
+                                                             const T* __restrict__ w3, const float* __restrict__ b3,
+                                                             T* __restrict__ out, int hw) {
   typedef typename VecT<T>::v16 V16;
   constexpr int V = VecT<T>::N;
-  __shared__ float red[256][C + 1];
   __shared__ float wl[3][C][C + 1];
   __shared__ float gap[C], hid[C], att[C], bias3[C];
-  extern __shared__ __attribute__((aligned(16))) unsigned char stage_raw[];
-  T* stage = (T*)stage_raw;  // [chunk][C]
-  const int tid = threadIdx.x, img = blockIdx.y;
+  __shared__ __attribute__((aligned(16))) T stage[kFfmChunk * C];
+  const int tid = threadIdx.x, img = blockIdx.y, S = gridDim.x;
   const T* fi = f + (long)img * hw * C;
   for (int e = tid; e < C * C; e += 256) {
     const int o = e / C, i = e - o * C;
@@ -702,27 +703,24 @@ __global__ void __launch_bounds__(256) ffm_head_eval_kernel(const T* __restrict_
     wl[1][o][i] = to_f(w2[e]);
     wl[2][o][i] = to_f(w3[e]);
   }
-  float s[C];
-#pragma unroll
-  for (int ch = 0; ch < C; ++ch) s[ch] = 0.f;
-  const int groups = hw / V;  // hw % V == 0 (host)
-  for (int g = tid; g < groups; g += 256) {
-    const V16* q = (const V16*)(fi + (long)g * V * C);
-    V16 v[C];
-#pragma unroll
-    for (int k = 0; k < C; ++k) v[k] = q[k];
-#pragma unroll
-    for (int k = 0; k < C; ++k)
-#pragma unroll
-      for (int j = 0; j < V; ++j) s[(k * V + j) % C] += to_f(v[k][j]);
-  }
-#pragma unroll
-  for (int ch = 0; ch < C; ++ch) red[tid][ch] = s[ch];
-  __syncthreads();
-  if (tid < C) {  // fixed-order reduction over the 256 thread partials
+  // this slice's pixels, in flight while the attention vector is formed
+  const int p0 = blockIdx.x * kFfmChunk, np = min(kFfmChunk, hw - p0);  // np % V == 0 (host: hw % V == 0)
+  const int nvec = np * C / V;
+  const V16* src = (const V16*)(fi + (long)p0 * C);
+  for (int e = tid; e < nvec; e += 256) ((V16*)stage)[e] = src[e];
+  if (tid < C) {  // GAP: the slices' partials summed in order (chan_final_kernel's order)
+    const float* pp = part + (long)img * S * C + tid;
     float t = 0.f;
-    for (int r = 0; r < 256; ++r) t += red[r][tid];
-    gap[tid] = to_f(from_f<T>(t / (float)hw));
+    int q = 0;
+    for (; q + 8 <= S; q += 8) {
+      float u[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) u[k] = pp[(long)(q + k) * C];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) t += u[k];
+    }
+    for (; q < S; ++q) t += pp[(long)q * C];
+    gap[tid] = to_f(from_f<T>(t * (1.f / (float)hw)));
     bias3[tid] = b3 ? b3[tid] : 0.f;
   }
   __syncthreads();
@@ -737,10 +735,6 @@ __global__ void __launch_bounds__(256) ffm_head_eval_kernel(const T* __restrict_
     for (int i = 0; i < C; ++i) v = fmaf(wl[1][tid][i], hid[i], v);
     att[tid] = to_f(from_f<T>(1.f / (1.f + expf(-v))));
   }
-  const int p0 = blockIdx.x * chunk, np = min(chunk, hw - p0);  // np % V == 0
-  const int nvec = np * C / V;
-  const V16* src = (const V16*)(fi + (long)p0 * C);
-  for (int e = tid; e < nvec; e += 256) ((V16*)stage)[e] = src[e];
   __syncthreads();
   for (int p = tid; p < np; p += 256) {
     T* q = stage + p * C;
@@ -762,18 +756,27 @@ __global__ void __launch_bounds__(256) ffm_head_eval_kernel(const T* __restrict_
   V16* dst = (V16*)(out + ((long)img * hw + p0) * C);
   for (int e = tid; e < nvec; e += 256) dst[e] = ((const V16*)stage)[e];
 }
+extern "C" size_t rtsds_ffm_head_eval_workspace(int n, long hw, int c) {
+  if (n <= 0 || hw <= 0 || c <= 0) return 256;
+  return (size_t)n * ((hw + kFfmChunk - 1) / kFfmChunk) * c * 4 + 256;
+}
 extern "C" int rtsds_ffm_head_eval(const void* f, const void* w1, const float* b1, const void* w2, const float* b2,
-                                   const void* w3, const float* b3, void* out, int n, long hw, int c, int dtype,
-                                   void* stream) {
-  if (n <= 0 || hw <= 0 || hw >= (1L << 31)) return RTSDS_ERR_SHAPE;
+                                   const void* w3, const float* b3, void* out, int n, long hw, int c, int dtype, void* ws,
+                                   size_t ws_bytes, void* stream) {
+  if (n <= 0 || n > 65535 || hw <= 0 || hw >= (1L << 31)) return RTSDS_ERR_SHAPE;
   if (c != 19) return RTSDS_ERR_UNSUPPORTED;  // instantiated for the 19-class maps
   const int V = dtype == RTSDS_BF16 ? 8 : 4;
   if (hw % V) return RTSDS_ERR_UNSUPPORTED;
-  const int chunk = dtype == RTSDS_BF16 ? 1024 : 512;  // 38 KB of staged pixels
-  const int chunks = (int)((hw + chunk - 1) / chunk);
-  const size_t lds = (size_t)chunk * c * (dtype == RTSDS_BF16 ? 2 : 4);
-  DISPATCH_T(dtype, hipLaunchKernelGGL((ffm_head_eval_kernel<T, 19>), dim3(chunks, n), dim3(256), lds, (hipStream_t)stream, (const T*)f,
-                                       (const T*)w1, b1, (const T*)w2, b2, (const T*)w3, b3, (T*)out, (int)hw, chunk));
+  if (ws_bytes < rtsds_ffm_head_eval_workspace(n, hw, c)) return RTSDS_ERR_WORKSPACE;
+  hipStream_t st = (hipStream_t)stream;
+  const int S = (int)((hw + kFfmChunk - 1) / kFfmChunk);
+  float* part = (float*)ws;
+  DISPATCH_T(dtype, {
+    hipLaunchKernelGGL((chan_part_kernel<T, 1, false>), dim3(S, n, 1), dim3(256), 0, st, (const T*)f, (const T*)nullptr, part,
+                       hw, c);
+    hipLaunchKernelGGL((ffm_head_apply_kernel<T, 19>), dim3(S, n), dim3(256), 0, st, (const float*)part, (const T*)f, (const T*)w1,
+                       b1, (const T*)w2, b2, (const T*)w3, b3, (T*)out, (int)hw);
+  });
   RET_LAUNCH();
 }
 extern "C" int rtsds_chscale_bwd(const void* dy, const void* x, const void* a, void* dx, void* da, int n, long hw, int c, int mode,

@@ -838,8 +838,9 @@ def ffm_head_eval(feature, w1, b1, w2, b2, w3, b3):
     out = empty_nhwc(n, c, h, w, f.dtype, f.device)
     ws = [t.reshape(c, c).contiguous() for t in (w1, w2, w3)]
     bs = [None if b is None else b.float().contiguous() for b in (b1, b2, b3)]
+    wk = workspace(lib.rtsds_ffm_head_eval_workspace(n, h * w, c), f.device)
     lib.rtsds_ffm_head_eval(_P(f), _P(ws[0]), _P(bs[0]), _P(ws[1]), _P(bs[1]), _P(ws[2]), _P(bs[2]), _P(out), n, h * w, c,
-                            dcode(f), stream())
+                            dcode(f), _P(wk), wk.numel(), stream())
     return out
 
 

@@ -848,6 +848,31 @@ def test_conv_bn_eval_into_slice(geo, dt):
 
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("geo", [(2, 64, 128), (3, 8, 40), (1, 16, 17)])
+def test_ffm_head_eval(geo, dt):
+    """FeatureFusionModule attention tail + final 1x1 conv (rtsds_ffm_head_eval: GAP partials per
+    256-pixel slice, then one workgroup per slice) vs fp64: conv3(f * a + f) + b3 with
+    a = sigmoid(conv2(relu(conv1(GAP(f)) + b1)) + b2); last slices partial (8 x 40, 16 x 17)."""
+    n, h, w = geo
+    if (h * w) % (8 if dt == torch.bfloat16 else 4):
+        pytest.skip("hw must be a multiple of the vector length")
+    g = torch.Generator().manual_seed(21)
+    c = 19
+    f = torch.randn(n, c, h, w, generator=g, dtype=torch.float64)
+    ws = [torch.randn(c, c, 1, 1, generator=g, dtype=torch.float64) / c ** 0.5 for _ in range(3)]
+    bs = [torch.randn(c, generator=g, dtype=torch.float64) for _ in range(3)]
+    if dt == torch.bfloat16:
+        f = f.bfloat16().double()
+        ws = [t.bfloat16().double() for t in ws]
+    a = torch.sigmoid(TF.conv2d(torch.relu(TF.conv2d(f.mean((2, 3), keepdim=True), ws[0], bs[0])), ws[1], bs[1]))
+    ref = TF.conv2d(f * a + f, ws[2], bs[2])
+    with torch.no_grad():
+        got = F.ffm_head_eval(_dev(f, dt), *[t.to(DEV, dt) for t in ws[:1]], bs[0].float().to(DEV),
+                              ws[1].to(DEV, dt), bs[1].float().to(DEV), ws[2].to(DEV, dt), bs[2].float().to(DEV))
+    _close(got, ref, dt, "out", 1e-4 if dt == torch.float32 else 3e-2)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 def test_bisenet_eval_fold_and_graph(dt):
     """BiSeNet eval forward: folded conv+BN path == unfused path (autograd-enabled eval), and a
     hipGraph replay (runtime.GraphedForward) == eager."""
