@@ -453,6 +453,63 @@ __global__ void __launch_bounds__(256) maxpool_bwd_k3s2(const T* __restrict__ dy
   }
 }
 
+// The same gather for 2 x 2 input pixels per thread (padding 0 or 1): the four pixels of the quad
+// (2m + {0, 1}, 2k + {0, 1}) are covered only by the windows (m - 1 + p + {0, 1}, k - 1 + p + {0, 1}),
+// so one set of four dY vectors + argmax loads serves four outputs (the per-pixel kernel loaded
+// 16 for them).  Each pixel adds its matching windows in the same (oh, ow) order: bit-identical.
+template <typename T>
+__global__ void __launch_bounds__(256) maxpool_bwd_k3s2_quad(const T* __restrict__ dy, const uint8_t* __restrict__ idx,
+                                                            T* __restrict__ dx, int n, int h, int w, int c, int ho, int wo, int p,
+                                                            FastDiv f_cv, FastDiv f_w2, FastDiv f_h2) {
+  typedef typename VecT<T>::v16 V16;
+  constexpr int V = VecT<T>::N;
+  const int cv = c / V, w2 = (w + 1) >> 1, h2 = (h + 1) >> 1;
+  const long total = (long)n * h2 * w2 * cv;  // < 2^31 (host-checked)
+  GRID_STRIDE_XCD(i, total) {
+    const uint32_t ii = (uint32_t)i, q0 = fdiv(ii, f_cv), q1 = fdiv(q0, f_w2), img = fdiv(q1, f_h2);
+    const int ch = (int)(ii - q0 * cv) * V;
+    const int kq = (int)(q0 - q1 * w2), mq = (int)(q1 - img * h2);
+    const int oh0 = mq - 1 + p, ow0 = kq - 1 + p;
+    V16 g[4];
+    unsigned long long ib[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int oh = min(max(oh0 + (t >> 1), 0), ho - 1), ow = min(max(ow0 + (t & 1), 0), wo - 1);
+      const long o = (((long)img * ho + oh) * wo + ow) * c + ch;
+      g[t] = *(const V16*)(dy + o);
+      if constexpr (V == 8) {
+        ib[t] = *(const unsigned long long*)(idx + o);
+      } else {
+        ib[t] = 0;
+#pragma unroll
+        for (int j = 0; j < V; ++j) ib[t] |= (unsigned long long)idx[o + j] << (8 * j);
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int ih = 2 * mq + (e >> 1), iw = 2 * kq + (e & 1);
+      if (ih >= h || iw >= w) continue;
+      float acc[V];
+#pragma unroll
+      for (int j = 0; j < V; ++j) acc[j] = 0.f;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int oh = oh0 + (t >> 1), ow = ow0 + (t & 1);
+        const int a = ih - (oh * 2 - p), b = iw - (ow * 2 - p);
+        if (oh < 0 || ow < 0 || oh >= ho || ow >= wo || a < 0 || a >= 3 || b < 0 || b >= 3) continue;
+        const unsigned want = (unsigned)(a * 3 + b);
+#pragma unroll
+        for (int j = 0; j < V; ++j)
+          if (((ib[t] >> (8 * j)) & 0xff) == want) acc[j] += to_f(g[t][j]);
+      }
+      V16 r;
+#pragma unroll
+      for (int j = 0; j < V; ++j) r[j] = from_f<T>(acc[j]);
+      *(V16*)(dx + (((long)img * h + ih) * w + iw) * c + ch) = r;
+    }
+  }
+}
+
 extern "C" int rtsds_maxpool_fwd(const void* x, void* y, uint8_t* idx, int n, int h, int w, int c, int ho, int wo, int k, int s,
                                  int p, int dtype, void* stream) {
   if (k * k > 255 || n <= 0 || ho <= 0 || wo <= 0) return RTSDS_ERR_SHAPE;
@@ -475,7 +532,12 @@ extern "C" int rtsds_maxpool_bwd(const void* dy, const uint8_t* idx, void* dx, i
   const long total = (long)n * h * w * c;
   if (total <= 0) return RTSDS_ERR_SHAPE;
   DISPATCH_T(dtype, {
-    if (c % VecT<T>::N == 0 && k == 3 && s == 2 && total < (1L << 31))
+    if (c % VecT<T>::N == 0 && k == 3 && s == 2 && (p == 0 || p == 1) && total < (1L << 31)) {
+      const long quads = (long)n * ((h + 1) / 2) * ((w + 1) / 2) * (c / VecT<T>::N);
+      hipLaunchKernelGGL(maxpool_bwd_k3s2_quad<T>, dim3(ew_blocks(quads, 256, 1 << 20)), dim3(256), 0, (hipStream_t)stream, (const T*)dy,
+                         idx, (T*)dx, n, h, w, c, ho, wo, p, fastdiv_make(c / VecT<T>::N), fastdiv_make((w + 1) / 2),
+                         fastdiv_make((h + 1) / 2));
+    } else if (c % VecT<T>::N == 0 && k == 3 && s == 2 && total < (1L << 31))
       hipLaunchKernelGGL(maxpool_bwd_k3s2<T>, dim3(ew_blocks(total / VecT<T>::N, 256, 1 << 20)), dim3(256), 0, (hipStream_t)stream, (const T*)dy, idx, (T*)dx,
                          n, h, w, c, ho, wo, p, fastdiv_make(c / VecT<T>::N), fastdiv_make(w), fastdiv_make(h));
     else if (c % VecT<T>::N == 0)

@@ -342,7 +342,8 @@ def test_batchnorm_module_counter():
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("geo", [(3, 2, 1, False, 17, 23), (3, 2, 1, True, 17, 23), (3, 2, 1, True, 16, 16),
-                                 (3, 2, 1, False, 32, 64, "relu"), (3, 1, 1, False, 9, 12), (2, 2, 0, False, 8, 10)])
+                                 (3, 2, 1, False, 32, 64, "relu"), (3, 1, 1, False, 9, 12), (2, 2, 0, False, 8, 10),
+                                 (3, 2, 0, False, 17, 23), (3, 2, 0, True, 16, 16), (3, 2, 1, False, 1, 5)])
 def test_maxpool(geo, dt):
     """Incl. post-ReLU input (ties at 0: the first maximum in window order wins, as ATen)
     and the generic (non 3x3 / stride-2) kernels."""
