@@ -1273,12 +1273,29 @@ __global__ void bilinear_bwd_h_tab_kernel(const float* __restrict__ tmp, T* __re
     dx[i] = from_f<T>(acc);
   }
 }
+// [first, last] nonzero entry of each table row, packed first | (last + 1) << 16 (the tables
+// carry a one-entry margin either side, so a plain loop over maxw wastes taps)
+RT_DEV void bil_table_span(const float* tab, int* span, int in, int maxw) {
+  for (int i = threadIdx.x; i < in; i += blockDim.x) {
+    int f = maxw, l = -1;
+    for (int j = 0; j < maxw; ++j)
+      if (tab[i * maxw + j] != 0.f) {
+        f = min(f, j);
+        l = j;
+      }
+    span[i] = f | (l + 1) << 16;
+  }
+  __syncthreads();
+}
 // Both passes in one kernel for 16-B channel vectors: a thread owns V channels of one input
 // pixel and forms each output row's W-pass sum t (the W kernel's taps, order and zero skipping,
 // fp32) right before the H-pass FMA that consumes it -- the same two fp32 FMA chains, so dx is
 // bit-identical to the two-pass kernels, without the fp32 [ho][wi] intermediate's write and
 // re-read.  Neighbouring input pixels re-read dY rows through L2 (XCD-aware block order).
-template <typename T>
+// Only each row's nonzero span is visited, and its column taps go four at a time: the four
+// loads issued (clamped into the span) before their FMAs, a zero weight leaving t unchanged
+// exactly as the skipped tap of the two-pass kernel.
+template <typename T, int G>
 __global__ void __launch_bounds__(256) bilinear_bwd_fused_vec_kernel(const T* __restrict__ dy, T* __restrict__ dx, int hi, int wi,
                                                                      int c, int ho, int wo, float sh, float sw, int dyld, int dyoff,
                                                                      int maxh, int maxw, long total, FastDiv f_cv, FastDiv f_wi,
@@ -1288,8 +1305,12 @@ __global__ void __launch_bounds__(256) bilinear_bwd_fused_vec_kernel(const T* __
   int* wlo = (int*)(wtab + wi * maxw);
   float* htab = (float*)(wlo + wi);
   int* hlo = (int*)(htab + hi * maxh);
+  int* wspan = hlo + hi;
+  int* hspan = wspan + wi;
   bil_table_build(wtab, wlo, wi, wo, sw, maxw);
   bil_table_build(htab, hlo, hi, ho, sh, maxh);
+  bil_table_span(wtab, wspan, wi, maxw);
+  bil_table_span(htab, hspan, hi, maxh);
   typedef typename VecT<T>::v16 V16;
   constexpr int V = VecT<T>::N;
   const int cv = c / V;
@@ -1301,22 +1322,31 @@ __global__ void __launch_bounds__(256) bilinear_bwd_fused_vec_kernel(const T* __
     const float* wx = wtab + iw * maxw;
     const float* wy = htab + ih * maxh;
     const T* base = dy + ((long)img * ho + hlo[ih]) * wo * dyld + (long)wlo[iw] * dyld + dyoff + ch;
+    const int jx0 = wspan[iw] & 0xffff, jx1 = wspan[iw] >> 16;
+    const int ky0 = hspan[ih] & 0xffff, ky1 = hspan[ih] >> 16;
     float acc[V];
 #pragma unroll
     for (int e = 0; e < V; ++e) acc[e] = 0.f;
-    for (int k = 0; k < maxh; ++k) {
+    for (int k = ky0; k < ky1; ++k) {
       const float yk = wy[k];
       if (yk == 0.f) continue;
       const T* row = base + (long)k * wo * dyld;
       float t[V];
 #pragma unroll
       for (int e = 0; e < V; ++e) t[e] = 0.f;
-      for (int j = 0; j < maxw; ++j) {
-        const float xj = wx[j];
-        if (xj == 0.f) continue;
-        const V16 v = *(const V16*)(row + (long)j * dyld);
+      for (int j0 = jx0; j0 < jx1; j0 += G) {
+        V16 v[G];
+        float xw[G];
 #pragma unroll
-        for (int e = 0; e < V; ++e) t[e] = fmaf(xj, to_f(v[e]), t[e]);
+        for (int u = 0; u < G; ++u) {
+          const int j = j0 + u;
+          xw[u] = j < jx1 ? wx[j] : 0.f;
+          v[u] = *(const V16*)(row + (long)min(j, jx1 - 1) * dyld);
+        }
+#pragma unroll
+        for (int u = 0; u < G; ++u)
+#pragma unroll
+          for (int e = 0; e < V; ++e) t[e] = xw[u] != 0.f ? fmaf(xw[u], to_f(v[u][e]), t[e]) : t[e];
       }
 #pragma unroll
       for (int e = 0; e < V; ++e) acc[e] = fmaf(yk, t[e], acc[e]);
@@ -1349,11 +1379,13 @@ static void bilinear_bwd_launch(const T* dy, float* tmp, T* dx, int n, int hi, i
   const int mw = bil_maxw(wi, wo, sw), mh = bil_maxw(hi, ho, sh);
   const size_t bw = bil_tab_bytes(wi, mw), bh = bil_tab_bytes(hi, mh);
   constexpr int V = VecT<T>::N;
-  if (c % V == 0 && dyld % V == 0 && dyoff % V == 0 && th < (1L << 31) && bw + bh <= (size_t)kBilTabLds &&
+  if (c % V == 0 && dyld % V == 0 && dyoff % V == 0 && th < (1L << 31) && bw + bh + (wi + hi) * 4 <= (size_t)kBilTabLds &&
       (long)n * ho * wo * dyld < (1L << 40)) {
     const long tv = th / V;
-    hipLaunchKernelGGL(bilinear_bwd_fused_vec_kernel<T>, dim3(ew_blocks(tv)), dim3(256), bw + bh, st, dy, dx, hi, wi, c, ho, wo, sh,
-                       sw, dyld, dyoff, mh, mw, tv, fastdiv_make(c / V), fastdiv_make(wi), fastdiv_make(hi));
+    // taps per load batch: 8 when an input column reaches ~8 output columns (x4), else 4 (x2)
+    auto kern = mw >= 10 ? bilinear_bwd_fused_vec_kernel<T, 8> : bilinear_bwd_fused_vec_kernel<T, 4>;
+    hipLaunchKernelGGL(kern, dim3(ew_blocks(tv)), dim3(256), bw + bh + (wi + hi) * 4, st, dy, dx, hi, wi, c, ho, wo, sh, sw, dyld,
+                       dyoff, mh, mw, tv, fastdiv_make(c / V), fastdiv_make(wi), fastdiv_make(hi));
     return;
   }
   if (tw < (1L << 31) && bw <= (size_t)kBilTabLds)
