@@ -365,11 +365,13 @@ int rtsds_confusion(const int64_t* label, const int64_t* pred, unsigned long lon
  * logits / dlogits: host arrays of nheads device pointers.  scale_h/w: ATen source scales
  * (in/out for size=, 1/scale_factor for scale_factor=; upsampling only, <= 1).
  * Forward writes loss[nheads] (mean over non-ignored pixels; may be NULL) and *loss_sum (their
- * sum in head order; may be NULL), adds the head-0 argmax matches to *correct (may be NULL)
- * and, when want_grad, keeps unscaled low-res gradient partials in ws.  Backward:
+ * sum in head order; may be NULL), adds the head-0 argmax matches to *correct (may be NULL;
+ * overwrites it instead when want_grad carries RTSDS_UPCE_SET_CORRECT, so the caller need not
+ * zero it) and, when want_grad & 1, keeps unscaled low-res gradient partials in ws.  Backward:
  * dlogits[h] = grad_loss[h * grad_stride] * d loss[h] / d logits[h] from those partials (ws
  * must be the forward's; grad_stride 0 = one upstream gradient for loss_sum).  Full-resolution logits are never materialised.  workspace()
  * returns 0 for geometries the fused path does not cover.                                 */
+#define RTSDS_UPCE_SET_CORRECT 2
 size_t rtsds_upce_workspace(int nheads, int n, int hl, int wl, int c, int H, int W, float scale_h,
                             float scale_w);
 int rtsds_upce_fwd(int nheads, const void* const* logits, const int64_t* target, int n, int hl,

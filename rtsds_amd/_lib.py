@@ -21,6 +21,7 @@ ACT_NONE, ACT_RELU, ACT_LEAKY, ACT_SIGMOID = 0, 1, 2, 3
 ACCUMULATE = 0x100
 INPUT_PADDED = 0x400
 WEIGHT_PACKED = 0x800
+UPCE_SET_CORRECT = 2  # rtsds_upce_fwd want_grad flag
 ERRORS = {1: "bad shape", 2: "unsupported configuration", 3: "HIP launch failure", 4: "workspace too small"}
 
 c_int, c_long, c_float, c_size_t, c_void_p = (ctypes.c_int, ctypes.c_long, ctypes.c_float,

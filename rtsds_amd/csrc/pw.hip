@@ -13,7 +13,9 @@
 
 namespace {
 constexpr int kPwMaxK = 32;
-constexpr int kPwTile = 64;         // data gradient: dY pixels staged per tile
+constexpr int kPwTile = 64;         // data gradient: dY pixels staged per tile (large maps)
+constexpr int kPwTileSmall = 16;    // ... for maps that would not give kPwDgradBlocks tiles of kPwTile
+constexpr int kPwRows = 1;          // data gradient: pixel rows per thread pass
 constexpr int kPwDgradBlocks = 1024;
 typedef float f2 __attribute__((ext_vector_type(2)));
 
@@ -37,10 +39,10 @@ bool pw_ok(const rtsds_conv_desc* d) {
 // Thread t: lane t % lanes owns channels [lane*V, lane*V + V), pixel slot t / lanes of the
 // `slots` pixels a block pass covers.  Per tile of kPwTile pixels: stage dY as fp32 [p][KP]
 // (zero beyond k), then each slot walks its pixels.
-template <int KP, int V>
+template <int KP, int V, int TILE, int ROWS>
 __global__ void __launch_bounds__(256) pw_dgrad_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ w,
                                                        bf16* __restrict__ dx, long pixels, int c, int k, int accum) {
-  __shared__ __attribute__((aligned(16))) float gs[kPwTile][KP];
+  __shared__ __attribute__((aligned(16))) float gs[TILE][KP];
   const int lanes = c / V, slots = 256 / lanes;
   const int lane = threadIdx.x % lanes, slot = threadIdx.x / lanes;
   const bool active = slot < slots;
@@ -61,44 +63,58 @@ __global__ void __launch_bounds__(256) pw_dgrad_kernel(const bf16* __restrict__ 
         wr[co][h] = co < k ? v : f2{0.f, 0.f};
       }
     }
-  const long tiles = (pixels + kPwTile - 1) / kPwTile;
+  const long tiles = (pixels + TILE - 1) / TILE;
   for (long tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
-    const long p0 = tile * kPwTile;
-    const int np = (int)min((long)kPwTile, pixels - p0);
+    const long p0 = tile * TILE;
+    const int np = (int)min((long)TILE, pixels - p0);
     __syncthreads();
 #pragma unroll
-    for (int j = 0; j < kPwTile * KP / 256; ++j) {
+    for (int j = 0; j < (TILE * KP + 255) / 256; ++j) {
       const int i = threadIdx.x + j * 256;
+      if (TILE * KP % 256 && i >= TILE * KP) break;
       const int r = i / KP, co = i - r * KP;
       const float v = (float)dy[(p0 + min(r, np - 1)) * k + min(co, k - 1)];
       gs[r][co] = (r < np && co < k) ? v : 0.f;
     }
     __syncthreads();
     if (!active) continue;
-    for (int r = slot; r < np; r += slots) {
-      f2 acc[H];
+    // ROWS pixel rows per pass: their accumulate operands loaded first (all in flight with
+    // the FMAs), their FMA chains interleaved; each row's sum in the same co order
+    for (int r0 = slot; r0 < np; r0 += ROWS * slots) {
+      f2 acc[ROWS][H], prev[ROWS][H];
 #pragma unroll
-      for (int h = 0; h < H; ++h) acc[h] = f2{0.f, 0.f};
+      for (int u = 0; u < ROWS; ++u) {
+        const int r = min(r0 + u * slots, np - 1);
+        const bf16* o = dx + (p0 + r) * c + ci;
 #pragma unroll
-      for (int co = 0; co < KP; ++co) {
-        const float g = gs[r][co];
-#pragma unroll
-        for (int h = 0; h < H; ++h) acc[h] = pk_fma(g, wr[co][h], acc[h]);
-      }
-      bf16* o = dx + (p0 + r) * c + ci;
-      if constexpr (V == 1) {
-        o[0] = (bf16)(accum ? acc[0][0] + (float)o[0] : acc[0][0]);
-      } else {
-        unsigned int out[H];
-        if (accum) {
-#pragma unroll
-          for (int h = 0; h < H; ++h) out[h] = f2_to_bf2(acc[h] + bf2_to_f2(((const unsigned int*)o)[h]));
-        } else {
-#pragma unroll
-          for (int h = 0; h < H; ++h) out[h] = f2_to_bf2(acc[h]);
+        for (int h = 0; h < H; ++h) {
+          acc[u][h] = f2{0.f, 0.f};
+          if (accum) prev[u][h] = V == 1 ? f2{(float)o[0], 0.f} : bf2_to_f2(((const unsigned int*)o)[h]);
         }
-        if constexpr (V == 4) *(uint2*)o = make_uint2(out[0], out[1]);
-        else *(unsigned int*)o = out[0];
+      }
+#pragma unroll
+      for (int co = 0; co < KP; ++co)
+#pragma unroll
+        for (int u = 0; u < ROWS; ++u) {
+          const float g = gs[min(r0 + u * slots, np - 1)][co];
+#pragma unroll
+          for (int h = 0; h < H; ++h) acc[u][h] = pk_fma(g, wr[co][h], acc[u][h]);
+        }
+#pragma unroll
+      for (int u = 0; u < ROWS; ++u) {
+        if (r0 + u * slots >= np) break;
+        bf16* o = dx + (p0 + r0 + u * slots) * c + ci;
+        // accumulate: the contribution rounded to bf16 first, then added -- bit-identical to
+        // storing it and adding the two bf16 gradients (the GEMM epilogue's order)
+        if constexpr (V == 1) {
+          o[0] = (bf16)(accum ? (float)(bf16)acc[u][0][0] + prev[u][0][0] : acc[u][0][0]);
+        } else {
+          unsigned int out[H];
+#pragma unroll
+          for (int h = 0; h < H; ++h) out[h] = f2_to_bf2(accum ? bf2_to_f2(f2_to_bf2(acc[u][h])) + prev[u][h] : acc[u][h]);
+          if constexpr (V == 4) *(uint2*)o = make_uint2(out[0], out[1]);
+          else *(unsigned int*)o = out[0];
+        }
       }
     }
   }
@@ -108,9 +124,14 @@ __global__ void __launch_bounds__(256) pw_dgrad_kernel(const bf16* __restrict__ 
 template <int KP, int V>
 static void pw_dgrad_launch(const rtsds_conv_desc* d, const void* dy, const void* w, void* dx, int accum, hipStream_t st) {
   const long px = (long)d->n * d->h * d->w;
-  const int blocks = (int)std::min<long>(kPwDgradBlocks, (px + kPwTile - 1) / kPwTile);
-  hipLaunchKernelGGL((pw_dgrad_kernel<KP, V>), dim3(blocks), dim3(256), 0, st, (const bf16*)dy, (const bf16*)w, (bf16*)dx, px,
-                     d->c, d->k, accum);
+  if (px >= (long)kPwDgradBlocks * kPwTile) {
+    hipLaunchKernelGGL((pw_dgrad_kernel<KP, V, kPwTile, kPwRows>), dim3(kPwDgradBlocks), dim3(256), 0, st, (const bf16*)dy,
+                       (const bf16*)w, (bf16*)dx, px, d->c, d->k, accum);
+  } else {  // small maps (the supervision heads' 1/16 and 1/32 inputs): more, shorter tiles
+    const int blocks = (int)std::min<long>(kPwDgradBlocks, (px + kPwTileSmall - 1) / kPwTileSmall);
+    hipLaunchKernelGGL((pw_dgrad_kernel<KP, V, kPwTileSmall, kPwRows>), dim3(blocks), dim3(256), 0, st, (const bf16*)dy,
+                       (const bf16*)w, (bf16*)dx, px, d->c, d->k, accum);
+  }
 }
 void pw_dgrad(const rtsds_conv_desc* d, const void* dy, const void* w, void* dx, int accum, hipStream_t st) {
   const int v = pw_dgrad_v(d->k, d->c);

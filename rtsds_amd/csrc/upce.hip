@@ -46,6 +46,7 @@ struct UpceArgs {
   float* gcorr;  // [nblocks][tile_el]: the auxiliary wave's one-hot partials (null: no auxiliary wave)
   float* lpart;  // [heads][nblocks]
   float* cpart;  // [nblocks]
+  float* kpart;  // [nblocks]: head 0's argmax matches per block (exact: <= the block's pixels)
   const int64_t* tgt;
   unsigned long long* correct;
   UpceGeo g;
@@ -429,7 +430,7 @@ __global__ void __launch_bounds__(256, kUpceOcc) upce_fwd_kernel(UpceArgs a) {
   }
   if (a.correct && (aux || (!has_aux && h == 0))) {
     for (int o = 32; o > 0; o >>= 1) corr += __shfl_xor(corr, o, 64);
-    if (lane == 0 && corr) atomicAdd(a.correct, corr);
+    if (lane == 0) a.kpart[blockIdx.x] = (float)corr;
   }
 }
 
@@ -448,8 +449,21 @@ RT_DEV void upce_losses(const float* stat, int nheads, float* loss, float* loss_
 }
 __global__ void __launch_bounds__(256) upce_final_kernel(const float* __restrict__ lpart, const float* __restrict__ cpart, int nblocks,
                                                          int nheads, float* __restrict__ loss, float* __restrict__ loss_sum,
-                                                         float* __restrict__ stat) {
+                                                         float* __restrict__ stat, const float* __restrict__ kpart,
+                                                         unsigned long long* __restrict__ correct, int set_correct) {
   __shared__ float red[4];
+  __shared__ unsigned long long kred[4];
+  if (correct) {  // the argmax matches: integer sums, exact in any order
+    unsigned long long k = 0;
+    for (int b = threadIdx.x; b < nblocks; b += 256) k += (unsigned long long)kpart[b];
+    for (int o = 32; o > 0; o >>= 1) k += __shfl_xor(k, o, 64);
+    if ((threadIdx.x & 63) == 0) kred[threadIdx.x >> 6] = k;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const unsigned long long t = kred[0] + kred[1] + kred[2] + kred[3];
+      *correct = set_correct ? t : *correct + t;
+    }
+  }
   // every array's partials of a thread loaded in one batch (8 rows in flight per array), then
   // summed in the original per-thread order b = tid, tid + 256, ...
   float acc[1 + kUpceMaxHeads];
@@ -567,11 +581,14 @@ static size_t upce_lds(const UpceGeo& g, int nheads) {
 static size_t upce_tile_el(const UpceGeo& g) { return (size_t)(g.th + 1) * (g.tw + 1) * g.c; }
 // ws: stat[64] (count, per-head loss sums; offset 0, see the header) | [heads][nblocks][tile_el]
 //     gradient partials | [heads][nblocks] loss partials | [nblocks] counts | (auxiliary wave)
-//     [nblocks][tile_el] one-hot partials
+//     [nblocks][tile_el] one-hot partials | [nblocks] argmax matches
 static const size_t kUpceStat = 64;
 static size_t upce_ws_floats(const UpceGeo& g, int heads) {
   return kUpceStat + (size_t)(heads + (upce_aux(heads) ? 1 : 0)) * g.nblocks * upce_tile_el(g) + (size_t)heads * g.nblocks +
-         g.nblocks;
+         2 * (size_t)g.nblocks;
+}
+static float* upce_kpart(float* f, const UpceGeo& g, int heads) {
+  return f + (size_t)(heads + (upce_aux(heads) ? 1 : 0)) * g.nblocks * upce_tile_el(g) + (size_t)heads * g.nblocks + g.nblocks;
 }
 static float* upce_gcorr(float* f, const UpceGeo& g, int heads) {
   return upce_aux(heads) ? f + (size_t)heads * g.nblocks * (upce_tile_el(g) + 1) + g.nblocks : nullptr;
@@ -603,12 +620,13 @@ extern "C" int rtsds_upce_fwd(int nheads, const void* const* logits, const int64
   a.lpart = f + (size_t)nheads * g.nblocks * te;
   a.cpart = a.lpart + (size_t)nheads * g.nblocks;
   a.gcorr = upce_gcorr(f, g, nheads);
+  a.kpart = upce_kpart(f, g, nheads);
   a.tgt = target;
   a.correct = correct;
   a.g = g;
   a.nheads = nheads;
   a.ignore = ignore_index;
-  a.want_grad = want_grad;
+  a.want_grad = want_grad & 1;
   hipStream_t st = (hipStream_t)stream;
   const size_t lds = upce_lds(g, nheads);
   const dim3 blk(64 * (nheads + (upce_aux(nheads) ? 1 : 0)));
@@ -625,7 +643,8 @@ extern "C" int rtsds_upce_fwd(int nheads, const void* const* logits, const int64
 #undef UPCE_CASE
     default: return RTSDS_ERR_UNSUPPORTED;
   }
-  hipLaunchKernelGGL(upce_final_kernel, dim3(1), dim3(256), 0, st, a.lpart, a.cpart, g.nblocks, nheads, loss, loss_sum, stat);
+  hipLaunchKernelGGL(upce_final_kernel, dim3(1), dim3(256), 0, st, a.lpart, a.cpart, g.nblocks, nheads, loss, loss_sum, stat,
+                     a.kpart, correct, (want_grad & RTSDS_UPCE_SET_CORRECT) ? 1 : 0);
   return hipGetLastError() == hipSuccess ? RTSDS_OK : RTSDS_ERR_LAUNCH;
 }
 

@@ -10,7 +10,7 @@ import ctypes
 import numpy as np
 import torch
 
-from ._lib import ACT_RELU, ACT_SIGMOID, INPUT_PADDED, WEIGHT_PACKED, ConvDesc, SplitReduceDesc, lib
+from ._lib import ACT_RELU, ACT_SIGMOID, INPUT_PADDED, UPCE_SET_CORRECT, WEIGHT_PACKED, ConvDesc, SplitReduceDesc, lib
 from .runtime import (CL, bump_params_epoch, collective, dcode, dp_world, empty_nhwc, nhwc, params_epoch,
                       register_fold, require_hip, side_enabled, side_fork, stream, workspace)
 
@@ -154,16 +154,27 @@ class GradJoin:
     activation.  Instead the first contribution's buffer is kept here and handed to the next
     producer, whose kernel accumulates into it (conv dgrad ``accumulate`` flag); the first
     ``n - 1`` backward calls return None for the tensor and the last returns the sum, so the
-    engine sees one gradient.  Order-independent: whichever producer runs last returns."""
+    engine sees one gradient.  Order-independent: whichever producer runs last returns.
 
-    __slots__ = ("left", "buf")
+    ``first_returns``: for a tensor whose readers need not all be reached by the backward (a
+    model output the caller may leave out of the loss): the first contribution returns its
+    buffer and later ones accumulate into it in place and return None -- the engine runs the
+    tensor's producer only after every reached reader, so it sees the full sum either way."""
 
-    def __init__(self, n):
+    __slots__ = ("left", "buf", "first")
+
+    def __init__(self, n, first_returns=False):
         self.left = n
         self.buf = None
+        self.first = first_returns
 
     def put(self, g):
         """Record this producer's finished contribution (``g`` already includes ``buf``)."""
+        if self.first:
+            if self.buf is None:
+                self.buf = g
+                return g
+            return None  # accumulated into the returned buffer
         self.buf = g
         self.left -= 1
         return g if self.left == 0 else None
@@ -174,6 +185,9 @@ def _join_add(join, g):
     if join is None:
         return g
     if join.buf is not None:  # not reached in the residual blocks (the BN runs first)
+        if join.first:
+            join.buf.add_(g)
+            return join.put(join.buf)
         g.add_(join.buf)
     return join.put(g)
 
@@ -741,10 +755,11 @@ class CatResizeFn(torch.autograd.Function):
     output (rtsds_bilinear_fwd's output pitch / offset) and, backward, each resize's gradient
     read straight from its slice of dy (rtsds_bilinear_bwd's input pitch / offset): neither the
     resized maps nor their gradients exist on their own; x0 (already at ``size``) is the one
-    copy each way."""
+    copy each way.  ``joins[k]``: GradJoin of xs[k]'s readers (BiSeNet's cx1 / cx2 also feed the
+    supervision convs, whose data gradients then accumulate into the resize adjoint's buffer)."""
 
     @staticmethod
-    def forward(ctx, size, x0, *xs):
+    def forward(ctx, size, joins, x0, *xs):
         x0 = nhwc(x0)
         n, c0, h, w = x0.shape
         if (h, w) != (int(size[0]), int(size[1])):
@@ -761,33 +776,35 @@ class CatResizeFn(torch.autograd.Function):
             geos.append((off, c, hi, wi, ho, wo, sh, sw))
             off += c
         ctx.meta = (n, c0, h, w, ct, geos)
+        ctx.joins = joins
         return y
 
     @staticmethod
     def backward(ctx, dy):
         n, c0, h, w, ct, geos = ctx.meta
         dy = nhwc(dy)
-        grads = [None, None]
-        if ctx.needs_input_grad[1]:
+        grads = [None, None, None]
+        if ctx.needs_input_grad[2]:
             g0 = empty_nhwc(n, c0, h, w, dy.dtype, dy.device)
             lib.rtsds_copy_channels(_P(dy), ct, 0, _P(g0), c0, 0, n * h * w, c0, 0, dcode(dy), stream())
-            grads[1] = g0
+            grads[2] = g0
         for k, (off, c, hi, wi, ho, wo, sh, sw) in enumerate(geos):
-            if not ctx.needs_input_grad[2 + k]:
+            if not ctx.needs_input_grad[3 + k]:
                 grads.append(None)
                 continue
             dx = empty_nhwc(n, c, hi, wi, dy.dtype, dy.device)
             ws = workspace(lib.rtsds_bilinear_bwd_workspace(n, hi, wi, c, ho, wo), dy.device)
             lib.rtsds_bilinear_bwd(_P(dy), _P(dx), n, hi, wi, c, ho, wo, sh, sw, ct, off, dcode(dy), _P(ws),
                                    ws.numel(), stream())
-            grads.append(dx)
+            # first contribution: the other reader accumulates into dx (otherwise one add)
+            grads.append(_join_add(ctx.joins[k], dx) if ctx.joins else dx)
         return tuple(grads)
 
 
-def concat_resized(x0, xs, size):
+def concat_resized(x0, xs, size, joins=None):
     """cat([x0] + [interpolate_bilinear(x, size) for x in xs], dim=1) without materialising the
-    resized maps (CatResizeFn)."""
-    return CatResizeFn.apply((int(size[0]), int(size[1])), x0, *xs)
+    resized maps (CatResizeFn).  ``joins``: per-xs GradJoin (or None) for inputs with other readers."""
+    return CatResizeFn.apply((int(size[0]), int(size[1])), tuple(joins) if joins else None, x0, *xs)
 
 
 def concat_resized_scaled_eval(x0, parts, size, into=None):
@@ -1247,7 +1264,7 @@ class UpsampleCrossEntropyFn(torch.autograd.Function):
     Also adds head 0's argmax==target pixel count into ``correct`` when given."""
 
     @staticmethod
-    def forward(ctx, target, geo, ignore_index, correct, *heads):
+    def forward(ctx, target, geo, ignore_index, correct, set_correct, *heads):
         n, c, hl, wl, H, W, sh, sw = geo
         xs = [nhwc(h) for h in heads]
         k = len(xs)
@@ -1257,9 +1274,10 @@ class UpsampleCrossEntropyFn(torch.autograd.Function):
         ptrs = (ctypes.c_void_p * k)(*[x.data_ptr() for x in xs])
         per_head = torch.empty(k, dtype=torch.float32, device=xs[0].device)
         total = torch.empty((), dtype=torch.float32, device=xs[0].device)
-        want = any(ctx.needs_input_grad[4:])
+        want = any(ctx.needs_input_grad[5:])
+        flags = int(want) | (UPCE_SET_CORRECT if set_correct else 0)
         lib.rtsds_upce_fwd(k, ptrs, _P(target), n, hl, wl, c, H, W, sh, sw, ignore_index, _P(per_head),
-                           _P(total), _P(correct), int(want), dt, _P(ws), ws.numel(), stream())
+                           _P(total), _P(correct), flags, dt, _P(ws), ws.numel(), stream())
         if dp_world() > 1:
             # global-batch mean: this rank's loss sums over the all-reduced valid-pixel count
             # (its contribution; the ranks' losses and gradients then SUM to the single-device
@@ -1283,7 +1301,7 @@ class UpsampleCrossEntropyFn(torch.autograd.Function):
         lib.rtsds_upce_bwd(ctx.k, _P(g), 0, ptrs, n, hl, wl, c, H, W, sh, sw, ctx.dt, _P(ws), ws.numel(),
                            stream())
         ctx.ws = None
-        return (None, None, None, None, *dxs)
+        return (None, None, None, None, None, *dxs)
 
 
 def interpolate_geometry(x, geo):
@@ -1312,10 +1330,11 @@ def upsample_cross_entropy_supported(heads, geo, ignore_index):
     return lib.rtsds_upce_workspace(len(heads), n, hl, wl, c, ho, wo, sh, sw) > 0
 
 
-def upsample_cross_entropy(heads, target, geo, ignore_index=-100, correct=None):
+def upsample_cross_entropy(heads, target, geo, ignore_index=-100, correct=None, set_correct=False):
     """Sum over heads (in order) of cross_entropy(interpolate_bilinear(head, ...), target),
     fused; ``geo`` from upsample_geometry().  ``correct``: optional int64 device counter that
-    receives head 0's pixel-accuracy matches.  Returns (total_loss, per_head_losses)."""
+    receives head 0's pixel-accuracy matches (added; ``set_correct``: overwritten, so the
+    caller need not zero it).  Returns the total loss."""
     require_hip(target, *heads)
     t = target.squeeze(1) if target.dim() == 4 else target
     t = t.contiguous()
@@ -1329,7 +1348,7 @@ def upsample_cross_entropy(heads, target, geo, ignore_index=-100, correct=None):
         raise RuntimeError("rtsds_amd: fused upsample+CE does not cover this geometry")
     full = (n, c, hl, wl, ho, wo, sh, sw)
     fn = UpsampleCrossEntropyFn
-    total = fn.apply(t, full, int(ignore_index), correct, *heads)
+    total = fn.apply(t, full, int(ignore_index), correct, bool(set_correct), *heads)
     return total
 
 

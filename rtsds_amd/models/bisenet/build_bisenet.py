@@ -132,6 +132,9 @@ class BiSeNet(torch.nn.Module):
     # inference: the spatial path's last conv writes straight into the fusion module's
     # concatenated input (no copy of the 256-channel map)
     spatial_into_concat = True
+    # training: cx1 / cx2's two readers (supervision conv, fusion-module resize) share one
+    # gradient buffer (functional.GradJoin first_returns) instead of autograd's add
+    supervision_joins = True
 
     def __init__(self, num_classes, context_path, with_interpolation=True):
         super().__init__()
@@ -247,20 +250,28 @@ class BiSeNet(torch.nn.Module):
                 return [(main, F.upsample_geometry(main, scale_factor=8))]
             return [(result, None)]
         aux_on = self.training and not main_only
+        j1 = j2 = None
         if aux_on:
             # reference: supervision_i(interpolate(cx_i)) (build_bisenet.py:151-152, 156-157).  The
             # 1x1 conv commutes with the bilinear resize (as the main head's, below), so each
             # supervision conv runs on the un-resized map -- 1/4 (cx1) and 1/16 (cx2) of the
             # pixels, without reading the resized 256 / 512-channel maps -- and its 19-channel
             # output is resized instead; the loss then resizes it to full resolution as before.
+            # cx1 / cx2 also feed the fusion module's resizes: one gradient buffer each, the
+            # supervision conv's data gradient accumulating into the resize adjoint's (or the
+            # reverse), instead of autograd's add of two full gradients; first_returns: correct
+            # also when a caller leaves the supervision outputs out of its loss
+            if torch.is_grad_enabled() and self.supervision_joins:
+                j1 = F.GradJoin(2, first_returns=True) if cx1.requires_grad else None
+                j2 = F.GradJoin(2, first_returns=True) if cx2.requires_grad else None
             full = input.shape[-2:]
-            s1 = F.interpolate_bilinear(self.supervision1(cx1), size=hw)
-            s2 = F.interpolate_bilinear(self.supervision2(cx2), size=hw)
+            s1 = F.interpolate_bilinear(self.supervision1(cx1, join=j1), size=hw)
+            s2 = F.interpolate_bilinear(self.supervision2(cx2, join=j2), size=hw)
             aux = [(s1, F.upsample_geometry(s1, size=full)), (s2, F.upsample_geometry(s2, size=full))]
         # the two resizes write straight into the fusion module's concatenated input and read
         # their gradients straight from its gradient (functional.CatResizeFn; the reference:
         # interpolate, interpolate, cat)
-        result = self.feature_fusion_module(F.concat_resized(sx, (cx1, cx2), hw))
+        result = self.feature_fusion_module(F.concat_resized(sx, (cx1, cx2), hw, joins=(j1, j2)))
         if self.with_interpolation:
             # reference: conv(up8(result)) (build_bisenet.py:165-167).  A 1x1 conv mixes channels
             # per pixel and bilinear resize mixes pixels per channel with weights summing to 1,

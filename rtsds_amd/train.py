@@ -58,6 +58,19 @@ def _fused_heads(model, criterion, inputs):
     return ts, geo
 
 
+_ONES = {}
+
+
+def _one(t):
+    """The unit seed of ``t.backward()`` as a cached tensor: autograd's own ones_like is a fill
+    launch per backward (a node of every replay of a captured step)."""
+    key = (t.device, t.dtype, tuple(t.shape))
+    one = _ONES.get(key)
+    if one is None:
+        one = _ONES[key] = torch.ones_like(t)
+    return one
+
+
 def _backward(loss, optimizer, cuts, since=None):
     """loss.backward(); with cuts (runtime.grad_cut under data parallelism, recorded in forward
     order): phase 1 down to the last cut's leaf, then, cut by cut from the last, the all-reduce
@@ -66,7 +79,7 @@ def _backward(loss, optimizer, cuts, since=None):
     while the next phase computes.  Same gradients (a cut leaf accumulates exactly what its
     tensor would have received).  ``since``: the gradient-arrival generation of this backward
     (optim.begin_grad_phase) when an earlier backward already touched the parameters."""
-    loss.backward()
+    loss.backward(_one(loss))
     for x, xd in reversed(cuts or []):
         optimizer.start_grad_allreduce(partial=True, since=since)
         if xd.grad is not None:
@@ -89,8 +102,8 @@ def seg_step(model, criterion, optimizer, inputs, targets):
         if fused is None:
             outs = _unpack(model(inputs))
     if fused is not None and fused[1] is not None:
-        correct = torch.zeros(1, dtype=torch.int64, device=fused[0][0].device)
-        loss = F.upsample_cross_entropy(fused[0], targets, fused[1], criterion.ignore_index, correct)
+        correct = torch.empty(1, dtype=torch.int64, device=fused[0][0].device)  # (overwritten)
+        loss = F.upsample_cross_entropy(fused[0], targets, fused[1], criterion.ignore_index, correct, set_correct=True)
         _backward(loss, optimizer, cuts)
         optimizer.step()
         return loss.detach(), correct
@@ -210,7 +223,7 @@ def da_step(generator, discriminator, generator_optimizer, discriminator_optimiz
         return _da_step_fused(generator, discriminator, generator_optimizer, discriminator_optimizer,
                               discriminator_loss, main, geo, target_image, lambda_, iterations, loss_seg,
                               correct)
-    loss_seg.backward()
+    loss_seg.backward(_one(loss_seg))
     with torch.no_grad():
         source_features = _full(main.detach(), geo)
 
@@ -231,10 +244,10 @@ def da_step(generator, discriminator, generator_optimizer, discriminator_optimiz
     target_feature = target_feature.detach()
     pred_s = discriminator(F.softmax(source_features, dim=1))
     loss_dsrc = discriminator_loss(pred_s, torch.ones(pred_s.size(), device=pred_s.device)) / iterations
-    loss_dsrc.backward()
+    loss_dsrc.backward(_one(loss_dsrc))
     pred_t2 = discriminator(F.softmax(target_feature, dim=1))
     loss_dtgt = discriminator_loss(pred_t2, torch.zeros(pred_t2.size(), device=pred_t2.device)) / iterations
-    loss_dtgt.backward()
+    loss_dtgt.backward(_one(loss_dtgt))
     _start_allreduce(discriminator_optimizer)  # overlaps G's optimizer step
 
     generator_optimizer.step()
@@ -264,7 +277,7 @@ def _da_step_fused(generator, discriminator, generator_optimizer, discriminator_
         target_image.record_stream(side)
         ctx = torch.cuda.stream(side)
     else:
-        loss_seg.backward()
+        loss_seg.backward(_one(loss_seg))
         ctx = contextlib.nullcontext()
     split = dp_world() > 1 and hasattr(generator_optimizer, "start_grad_allreduce")
     with ctx, (branches_serial() if overlap else contextlib.nullcontext()), collect_cuts(split) as cuts:
@@ -274,7 +287,7 @@ def _da_step_fused(generator, discriminator, generator_optimizer, discriminator_
         ones = torch.ones(pred_t.size(), device=pred_t.device)
         loss_adv = lambda_ * discriminator_loss(pred_t, ones) / iterations
     if overlap:
-        loss_seg.backward()
+        loss_seg.backward(_one(loss_seg))
         amb.wait_stream(side)
         for t in (target_probs, loss_adv):
             t.record_stream(amb)
@@ -296,14 +309,14 @@ def _da_step_fused(generator, discriminator, generator_optimizer, discriminator_
     with torch.cuda.stream(side2) if overlap else contextlib.nullcontext():
         pred_s = discriminator(source_probs)
         loss_dsrc = discriminator_loss(pred_s, torch.ones(pred_s.size(), device=pred_s.device)) / iterations
-        loss_dsrc.backward()
+        loss_dsrc.backward(_one(loss_dsrc))
     if overlap:
         amb.wait_stream(side)  # the adversarial backward ran on the target ops' streams
         amb.wait_stream(side2)
         loss_dsrc.record_stream(amb)
     pred_t2 = discriminator(F.detach_padded(target_probs))
     loss_dtgt = discriminator_loss(pred_t2, torch.zeros(pred_t2.size(), device=pred_t2.device)) / iterations
-    loss_dtgt.backward()
+    loss_dtgt.backward(_one(loss_dtgt))
     _start_allreduce(discriminator_optimizer)
 
     generator_optimizer.step()
@@ -336,7 +349,7 @@ def da2_step(generator, discriminator, generator_optimizer, discriminator_optimi
     d_real_output = discriminator(F.softmax(real_seg, dim=1))
     loss_adv = discriminator_loss(d_real_output, fake_labels)
     g_loss = g_loss_seg + lambda_adv * loss_adv
-    g_loss.backward()
+    g_loss.backward(_one(g_loss))
     generator_optimizer.step()
     for p in discriminator.parameters():
         p.requires_grad = True
@@ -350,7 +363,7 @@ def da2_step(generator, discriminator, generator_optimizer, discriminator_optimi
     d_real_loss = discriminator_loss(d_real_output, real_labels)
     d_fake_loss = discriminator_loss(d_fake_output, fake_labels)
     d_loss = d_real_loss + d_fake_loss
-    d_loss.backward()
+    d_loss.backward(_one(d_loss))
     discriminator_optimizer.step()
     return (g_loss_seg.detach(), loss_adv.detach(), g_loss.detach(), d_real_loss.detach(),
             d_fake_loss.detach(), d_loss.detach(), correct)

@@ -786,6 +786,67 @@ def test_bisenet_branch_streams_bit_identical(graphed):
 
 
 @pytest.mark.parametrize("graphed", [False, True])
+def test_bisenet_supervision_joins_bit_identical(graphed):
+    """BiSeNet.supervision_joins (cx1 / cx2's gradient accumulated in place by the supervision
+    conv's data gradient instead of autograd's add of the two bf16 gradients) leaves losses,
+    the accuracy count (overwritten by the fused CE, never zeroed), parameters and optimizer
+    state bit-identical, eagerly and as hipGraph replays."""
+    from rtsds_amd.runtime import GraphedStep
+    g = torch.Generator().manual_seed(9)
+    x = torch.randn(2, 3, 128, 256, generator=g).to(DEV)
+    y = torch.randint(0, 20, (2, 128, 256), generator=g).to(DEV)
+    ce = losses.CrossEntropyLoss(ignore_index=19)
+    runs = []
+    with rtsds_amd.precision(torch.bfloat16):
+        for joins in (False, True):
+            BiSeNet.supervision_joins = joins
+            try:
+                torch.manual_seed(3)
+                net = BiSeNet(19, "resnet18").to(DEV).train()
+                opt = optim.Adam(net.parameters(), lr=1e-3)
+                core = lambda: rtrain.seg_step(net, ce, opt, x, y)  # noqa: E731
+                step = GraphedStep(core, [opt], warmup=1) if graphed else core
+                ls = [[float(v) for v in step()] for _ in range(3)]
+                torch.cuda.synchronize()
+                st = {k: v.detach().float().cpu().clone() for k, v in net.state_dict().items()}
+                st.update({f"m{i}": a.m.cpu() for i, a in enumerate(opt.arenas())})
+                runs.append((ls, st))
+            finally:
+                BiSeNet.supervision_joins = True
+    (l0, s0), (l1, s1) = runs
+    assert l0 == l1
+    assert all(c > 0 for _, c in l1)
+    for k in s0:
+        assert torch.equal(s0[k], s1[k]), k
+
+
+def test_bisenet_supervision_joins_main_head_only():
+    """A caller that leaves the supervision outputs out of its loss: with the joins (first
+    contribution returned, GradJoin first_returns) cx1 / cx2 still receive the resize
+    adjoint's gradient -- every parameter gradient equal to the unjoined model's."""
+    g = torch.Generator().manual_seed(10)
+    x = torch.randn(2, 3, 128, 256, generator=g).to(DEV)
+    grads = []
+    with rtsds_amd.precision(torch.bfloat16):
+        for joins in (False, True):
+            BiSeNet.supervision_joins = joins
+            try:
+                torch.manual_seed(4)
+                net = BiSeNet(19, "resnet18").to(DEV).train()
+                out, _, _ = net(x)
+                out.float().square().mean().backward()
+                torch.cuda.synchronize()
+                grads.append({k: p.grad.detach().float().cpu().clone() for k, p in net.named_parameters()
+                              if p.grad is not None})
+            finally:
+                BiSeNet.supervision_joins = True
+    assert grads[0].keys() == grads[1].keys()
+    assert any(k.startswith("attention_refinement_module1") for k in grads[1])
+    for k in grads[0]:
+        assert torch.equal(grads[0][k], grads[1][k]), k
+
+
+@pytest.mark.parametrize("graphed", [False, True])
 def test_da_step_overlap_bit_identical(graphed):
     """train.DA_OVERLAP (target forward on a second stream during the source backward) leaves
     the four losses, G/D parameters, optimizer state and BN buffers bit-identical to the

@@ -185,19 +185,22 @@ def test_fwd_split_k_accumulate():
     _close(y, y0.double() + fresh.double(), torch.bfloat16, "y accum", tol=1e-2)
 
 
+@pytest.mark.parametrize("hw", [(32, 64), (33, 63)])
 @pytest.mark.parametrize("c", [512, 256, 19])
-def test_pw_backward_accumulate(c):
+def test_pw_backward_accumulate(c, hw):
     """Narrow 1x1 backward with the accumulate flag (pw.hip dgrad, split-K GEMM wgrad): dx +=
     dgrad, dw/db += wgrad (the flat-arena gradient sink and ConvSum paths), checked against the
-    non-accumulating call plus the prior contents; the weight gradient against fp64, and for the
-    19-channel input also from the 32-channel padded image (RTSDS_INPUT_PADDED)."""
+    non-accumulating call plus the prior contents (dx: bit-identical to adding the two bf16
+    gradients, as autograd would; 33 x 63 leaves a partial pixel tile); the weight gradient
+    against fp64, and for the 19-channel input also from the 32-channel padded image
+    (RTSDS_INPUT_PADDED)."""
     import ctypes
     from rtsds_amd._lib import lib
     from rtsds_amd.functional import _conv_desc, _P
     from rtsds_amd.runtime import stream, workspace
 
     g = torch.Generator().manual_seed(c)
-    n, h, w, k = 2, 32, 64, 19
+    n, (h, w), k = 2, hw, 19
     x = _dev(torch.randn(n, c, h, w, generator=g), torch.bfloat16)
     dy = _dev(torch.randn(n, k, h, w, generator=g), torch.bfloat16)
     wq = _dev(torch.randn(k, c, 1, 1, generator=g) / c ** 0.5, torch.bfloat16)
@@ -217,7 +220,9 @@ def test_pw_backward_accumulate(c):
         assert lib.rtsds_conv2d_wgrad(ctypes.byref(d), _P(x), _P(dy), _P(out_w), _P(out_b), acc, _P(ws), ws.numel(),
                                       stream()) == 0
     torch.cuda.synchronize()
-    _close(dx, dx0.double() + dx_fresh.double(), torch.bfloat16, "dx accum", tol=1e-2)
+    assert torch.equal(dx, dx0 + dx_fresh)
+    ref_dx = torch.einsum("nkhw,kc->nchw", dy.double(), wq.double().reshape(k, c))
+    _close(dx_fresh, ref_dx, torch.bfloat16, "dx", tol=1e-2)
     _close(dw, dw0.double() + dw_f.double(), torch.float32, "dw accum", tol=1e-5)
     _close(db, db0.double() + db_f.double(), torch.float32, "db accum", tol=1e-5)
     ref_w = torch.einsum("nkhw,nchw->kc", dy.double(), x.double())
