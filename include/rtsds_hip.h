@@ -169,6 +169,14 @@ int rtsds_bn_fwd(const void* x, const void* res, void* y, long rows, int c, cons
                  float* save_invstd, float momentum, float eps, int training, int act,
                  const float* stats_part, int stats_nrb, int dtype, void* ws, size_t ws_bytes,
                  void* stream);
+/* rtsds_bn_fwd with y's row pitch ldy >= c (ldy == c: rtsds_bn_fwd): y is a channel slice of a
+ * wider NHWC tensor -- the spatial path's output written into the fusion module's concatenated
+ * input (build_bisenet.py:153,72).  ldy != c: bf16, c % 8 == 0, ldy % 8 == 0.              */
+int rtsds_bn_fwd_ld(const void* x, const void* res, void* y, long ldy, long rows, int c,
+                    const float* gamma, const float* beta, float* running_mean, float* running_var,
+                    long long* num_batches_tracked, float* save_mean, float* save_invstd,
+                    float momentum, float eps, int training, int act, const float* stats_part,
+                    int stats_nrb, int dtype, void* ws, size_t ws_bytes, void* stream);
 /* Eval-mode fold of BatchNorm2d(running stats) into the preceding conv (+ its bias, may be
  * NULL): scale = gamma / sqrt(running_var + eps), shift = beta + (bias - running_mean) * scale
  * (fp32 [c]; gamma / beta may be NULL = 1 / 0).                                            */
@@ -184,6 +192,12 @@ int rtsds_bn_bwd(const void* dy, const void* x, const void* y, void* dx, void* d
                  float* dgamma, float* dbeta, long rows, int c, const float* gamma,
                  const float* beta, const float* save_mean, const float* save_invstd, int training, int act,
                  int accumulate_params, int dtype, void* ws, size_t ws_bytes, void* stream);
+/* rtsds_bn_bwd reading dy with row pitch ldy >= c (a channel slice of the concatenated
+ * input's gradient; ldy != c: bf16, c % 8 == 0, ldy % 8 == 0).                              */
+int rtsds_bn_bwd_ld(const void* dy, long ldy, const void* x, const void* y, void* dx, void* dres,
+                    float* dgamma, float* dbeta, long rows, int c, const float* gamma,
+                    const float* beta, const float* save_mean, const float* save_invstd, int training,
+                    int act, int accumulate_params, int dtype, void* ws, size_t ws_bytes, void* stream);
 /* rtsds_bn_bwd without its statistics pass: part / nrb = the channel-major (sum g,
  * sum g (x - mean)) partials of rtsds_conv2d_dgrad_bnstats (bf16, c % 8 == 0, no residual).  */
 int rtsds_bn_bwd_part(const void* dy, const void* x, void* dx, float* dgamma, float* dbeta, long rows, int c,
@@ -448,7 +462,7 @@ int rtsds_graph_split_destroy(void* handle);
 /* ABI revision of this header (RTSDS_ABI_VERSION): bumped whenever an entry point's signature
  * changes.  The Python loader refuses a library whose revision differs (A/B variant libraries
  * built from older sources would otherwise be called with the wrong argument lists). */
-#define RTSDS_ABI_VERSION 8
+#define RTSDS_ABI_VERSION 9
 int rtsds_abi_version(void);
 
 #ifdef __cplusplus

@@ -234,7 +234,7 @@ RT_DEV void load_coef(const float* __restrict__ p, int ch0, int c, float* v) {
 template <typename T, int VEC, int ACT>
 __global__ void __launch_bounds__(256) bn_apply_kernel(const T* __restrict__ x, const T* __restrict__ res, T* __restrict__ y,
                                                         const float* __restrict__ scale, const float* __restrict__ shift,
-                                                        long rows, int c, int act_rt) {
+                                                        long rows, int c, int act_rt, long ldy) {
   const int act = ACT >= 0 ? ACT : act_rt;
   const int cbase = blockIdx.y * 256 * VEC;
   const int cl = min(c - cbase, 256 * VEC);
@@ -262,8 +262,8 @@ __global__ void __launch_bounds__(256) bn_apply_kernel(const T* __restrict__ x, 
       v0[j] = act_f(a, act);
       v1[j] = act_f(b, act);
     }
-    store_vec<T, VEC>(y + r * c + ch0, v0, cvalid);
-    store_vec<T, VEC>(y + (r + step) * c + ch0, v1, cvalid);
+    store_vec<T, VEC>(y + r * ldy + ch0, v0, cvalid);
+    store_vec<T, VEC>(y + (r + step) * ldy + ch0, v1, cvalid);
   }
   if (r < rows) {
     float v0[VEC], r0[VEC];
@@ -275,7 +275,7 @@ __global__ void __launch_bounds__(256) bn_apply_kernel(const T* __restrict__ x, 
       if (res) a += r0[j];
       v0[j] = act_f(a, act);
     }
-    store_vec<T, VEC>(y + r * c + ch0, v0, cvalid);
+    store_vec<T, VEC>(y + r * ldy + ch0, v0, cvalid);
   }
 }
 
@@ -685,7 +685,7 @@ extern "C" size_t rtsds_bn_workspace(long rows, int c) {
 template <typename T, int VEC>
 static void bn_fwd_launch(const void* x, const void* res, void* y, long rows, int c, const float* gamma, const float* beta,
                           float* rm, float* rv, float* sm, float* si, float mom, float eps, int training, int act,
-                          const float* pre, int pre_nrb, long long* nbt, const BnWs& w, hipStream_t st) {
+                          const float* pre, int pre_nrb, long long* nbt, const BnWs& w, hipStream_t st, long ldy) {
   float* scale = w.coef;
   float* shift = w.coef + c;
   if (training) {
@@ -703,16 +703,16 @@ static void bn_fwd_launch(const void* x, const void* res, void* y, long rows, in
   }
   with_act(act, [&](auto a) {
     hipLaunchKernelGGL((bn_apply_kernel<T, VEC, decltype(a)::value>), dim3(bn_apply_rb(rows, c, VEC), rt_cdiv(c, 256 * VEC)),
-                       dim3(256), 0, st, (const T*)x, (const T*)res, (T*)y, scale, shift, rows, c, act);
+                       dim3(256), 0, st, (const T*)x, (const T*)res, (T*)y, scale, shift, rows, c, act, ldy);
   });
 }
 
-extern "C" int rtsds_bn_fwd(const void* x, const void* res, void* y, long rows, int c, const float* gamma, const float* beta,
-                            float* running_mean, float* running_var, long long* num_batches_tracked, float* save_mean,
-                            float* save_invstd, float momentum,
-                            float eps, int training, int act, const float* stats_part, int stats_nrb, int dtype, void* ws,
-                            size_t ws_bytes, void* stream) {
-  if (rows <= 0 || c <= 0) return RTSDS_ERR_SHAPE;
+extern "C" int rtsds_bn_fwd_ld(const void* x, const void* res, void* y, long ldy, long rows, int c, const float* gamma,
+                               const float* beta, float* running_mean, float* running_var, long long* num_batches_tracked,
+                               float* save_mean, float* save_invstd, float momentum, float eps, int training, int act,
+                               const float* stats_part, int stats_nrb, int dtype, void* ws, size_t ws_bytes, void* stream) {
+  if (rows <= 0 || c <= 0 || ldy < c) return RTSDS_ERR_SHAPE;
+  if (ldy != c && !(dtype == RTSDS_BF16 && c % 8 == 0 && ldy % 8 == 0)) return RTSDS_ERR_UNSUPPORTED;
   if (ws_bytes < rtsds_bn_workspace(rows, c)) return RTSDS_ERR_WORKSPACE;
   if (!training && (!running_mean || !running_var)) return RTSDS_ERR_UNSUPPORTED;
   if (training && (!save_mean || !save_invstd)) return RTSDS_ERR_UNSUPPORTED;
@@ -721,13 +721,22 @@ extern "C" int rtsds_bn_fwd(const void* x, const void* res, void* y, long rows, 
   const BnWs w = bn_ws(ws, rows, c);
   long long* nbt = training ? num_batches_tracked : nullptr;
   if (dtype == RTSDS_BF16) {
-    if (c % 8 == 0) bn_fwd_launch<bf16, 8>(x, res, y, rows, c, gamma, beta, running_mean, running_var, save_mean, save_invstd, momentum, eps, training, act, stats_part, stats_nrb, nbt, w, st);
-    else bn_fwd_launch<bf16, 1>(x, res, y, rows, c, gamma, beta, running_mean, running_var, save_mean, save_invstd, momentum, eps, training, act, stats_part, stats_nrb, nbt, w, st);
+    if (c % 8 == 0) bn_fwd_launch<bf16, 8>(x, res, y, rows, c, gamma, beta, running_mean, running_var, save_mean, save_invstd, momentum, eps, training, act, stats_part, stats_nrb, nbt, w, st, ldy);
+    else bn_fwd_launch<bf16, 1>(x, res, y, rows, c, gamma, beta, running_mean, running_var, save_mean, save_invstd, momentum, eps, training, act, stats_part, stats_nrb, nbt, w, st, ldy);
   } else if (dtype == RTSDS_F32) {
-    if (c % 4 == 0) bn_fwd_launch<float, 4>(x, res, y, rows, c, gamma, beta, running_mean, running_var, save_mean, save_invstd, momentum, eps, training, act, stats_part, stats_nrb, nbt, w, st);
-    else bn_fwd_launch<float, 1>(x, res, y, rows, c, gamma, beta, running_mean, running_var, save_mean, save_invstd, momentum, eps, training, act, stats_part, stats_nrb, nbt, w, st);
+    if (c % 4 == 0) bn_fwd_launch<float, 4>(x, res, y, rows, c, gamma, beta, running_mean, running_var, save_mean, save_invstd, momentum, eps, training, act, stats_part, stats_nrb, nbt, w, st, ldy);
+    else bn_fwd_launch<float, 1>(x, res, y, rows, c, gamma, beta, running_mean, running_var, save_mean, save_invstd, momentum, eps, training, act, stats_part, stats_nrb, nbt, w, st, ldy);
   } else return RTSDS_ERR_UNSUPPORTED;
   return hipGetLastError() == hipSuccess ? RTSDS_OK : RTSDS_ERR_LAUNCH;
+}
+
+extern "C" int rtsds_bn_fwd(const void* x, const void* res, void* y, long rows, int c, const float* gamma, const float* beta,
+                            float* running_mean, float* running_var, long long* num_batches_tracked, float* save_mean,
+                            float* save_invstd, float momentum,
+                            float eps, int training, int act, const float* stats_part, int stats_nrb, int dtype, void* ws,
+                            size_t ws_bytes, void* stream) {
+  return rtsds_bn_fwd_ld(x, res, y, c, rows, c, gamma, beta, running_mean, running_var, num_batches_tracked, save_mean,
+                         save_invstd, momentum, eps, training, act, stats_part, stats_nrb, dtype, ws, ws_bytes, stream);
 }
 
 static constexpr auto kBnBwdRBMax = 512;
@@ -786,8 +795,9 @@ static void bn_bwd_launch(const GS& gs, const void* x, const void* y, void* dx, 
 template <typename T, int VEC>
 static void bn_bwd_launch(const void* dy, const void* x, const void* y, void* dx, void* dres, float* dgamma, float* dbeta,
                           long rows, int c, const float* gamma, const float* beta, const float* smean, const float* sinv, int training,
-                          int act, int accumulate, const BnWs& w, hipStream_t st, const float* pre = nullptr, int pre_nrb = 0) {
-  const GradDirect<T> gs{(const T*)dy, c};
+                          int act, int accumulate, const BnWs& w, hipStream_t st, const float* pre = nullptr, int pre_nrb = 0,
+                          long ldy = 0) {
+  const GradDirect<T> gs{(const T*)dy, (int)(ldy ? ldy : c)};
   bn_bwd_launch<T, VEC, GradDirect<T>>(gs, x, y, dx, dres, dgamma, dbeta, rows, c, gamma, beta, smean, sinv, training, act,
                                        accumulate, w, st, pre, pre_nrb);
 }
@@ -805,24 +815,32 @@ extern "C" int rtsds_bn_bwd_part(const void* dy, const void* x, void* dx, float*
   return hipGetLastError() == hipSuccess ? RTSDS_OK : RTSDS_ERR_LAUNCH;
 }
 
-extern "C" int rtsds_bn_bwd(const void* dy, const void* x, const void* y, void* dx, void* dres, float* dgamma, float* dbeta,
-                            long rows, int c, const float* gamma, const float* beta, const float* save_mean,
-                            const float* save_invstd, int training, int act, int accumulate_params, int dtype, void* ws,
-                            size_t ws_bytes, void* stream) {
-  if (rows <= 0 || c <= 0) return RTSDS_ERR_SHAPE;
+extern "C" int rtsds_bn_bwd_ld(const void* dy, long ldy, const void* x, const void* y, void* dx, void* dres, float* dgamma,
+                               float* dbeta, long rows, int c, const float* gamma, const float* beta, const float* save_mean,
+                               const float* save_invstd, int training, int act, int accumulate_params, int dtype, void* ws,
+                               size_t ws_bytes, void* stream) {
+  if (rows <= 0 || c <= 0 || ldy < c || ldy > (1L << 30)) return RTSDS_ERR_SHAPE;
+  if (ldy != c && !(dtype == RTSDS_BF16 && c % 8 == 0 && ldy % 8 == 0)) return RTSDS_ERR_UNSUPPORTED;
   if (ws_bytes < rtsds_bn_workspace(rows, c)) return RTSDS_ERR_WORKSPACE;
   if (!y && !(act == RTSDS_ACT_NONE || act == RTSDS_ACT_RELU || act == RTSDS_ACT_LEAKY)) return RTSDS_ERR_UNSUPPORTED;
   if (!y && act && dres) return RTSDS_ERR_UNSUPPORTED;  // residual: the mask needs y
   hipStream_t st = (hipStream_t)stream;
   const BnWs w = bn_ws(ws, rows, c);
   if (dtype == RTSDS_BF16) {
-    if (c % 8 == 0) bn_bwd_launch<bf16, 8>(dy, x, y, dx, dres, dgamma, dbeta, rows, c, gamma, beta, save_mean, save_invstd, training, act, accumulate_params, w, st);
-    else bn_bwd_launch<bf16, 1>(dy, x, y, dx, dres, dgamma, dbeta, rows, c, gamma, beta, save_mean, save_invstd, training, act, accumulate_params, w, st);
+    if (c % 8 == 0) bn_bwd_launch<bf16, 8>(dy, x, y, dx, dres, dgamma, dbeta, rows, c, gamma, beta, save_mean, save_invstd, training, act, accumulate_params, w, st, nullptr, 0, ldy);
+    else bn_bwd_launch<bf16, 1>(dy, x, y, dx, dres, dgamma, dbeta, rows, c, gamma, beta, save_mean, save_invstd, training, act, accumulate_params, w, st, nullptr, 0, ldy);
   } else if (dtype == RTSDS_F32) {
-    if (c % 4 == 0) bn_bwd_launch<float, 4>(dy, x, y, dx, dres, dgamma, dbeta, rows, c, gamma, beta, save_mean, save_invstd, training, act, accumulate_params, w, st);
-    else bn_bwd_launch<float, 1>(dy, x, y, dx, dres, dgamma, dbeta, rows, c, gamma, beta, save_mean, save_invstd, training, act, accumulate_params, w, st);
+    if (c % 4 == 0) bn_bwd_launch<float, 4>(dy, x, y, dx, dres, dgamma, dbeta, rows, c, gamma, beta, save_mean, save_invstd, training, act, accumulate_params, w, st, nullptr, 0, ldy);
+    else bn_bwd_launch<float, 1>(dy, x, y, dx, dres, dgamma, dbeta, rows, c, gamma, beta, save_mean, save_invstd, training, act, accumulate_params, w, st, nullptr, 0, ldy);
   } else return RTSDS_ERR_UNSUPPORTED;
   return hipGetLastError() == hipSuccess ? RTSDS_OK : RTSDS_ERR_LAUNCH;
+}
+extern "C" int rtsds_bn_bwd(const void* dy, const void* x, const void* y, void* dx, void* dres, float* dgamma, float* dbeta,
+                            long rows, int c, const float* gamma, const float* beta, const float* save_mean,
+                            const float* save_invstd, int training, int act, int accumulate_params, int dtype, void* ws,
+                            size_t ws_bytes, void* stream) {
+  return rtsds_bn_bwd_ld(dy, c, x, y, dx, dres, dgamma, dbeta, rows, c, gamma, beta, save_mean, save_invstd, training, act,
+                         accumulate_params, dtype, ws, ws_bytes, stream);
 }
 
 // ---- BatchNorm + ReLU + MaxPool2d(3, 2, p) (the ResNet stem: bn1 -> relu -> maxpool,

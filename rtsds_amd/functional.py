@@ -562,27 +562,34 @@ class BatchNormFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, gamma, beta, res, running_mean, running_var, training, momentum, eps, act,
-                stats, stats_nrb, nbt, res_join=None, link=None):
+                stats, stats_nrb, nbt, res_join=None, link=None, out=None):
         require_hip(x)
         x = nhwc(x)
         if res is not None:
             res = nhwc(res)
         n, c, h, w = x.shape
         rows = n * h * w
-        y = torch.empty_like(x, memory_format=CL)
+        keep_y = res is not None or act == ACT_SIGMOID
+        ld = c
+        if out is not None and not keep_y and x.dtype == torch.bfloat16 and c % 8 == 0 and out[0].shape[1] % 8 == 0:
+            # y written straight into channels [off, off + c) of out's NHWC buffer (a view)
+            buf, off = out
+            ld = buf.shape[1]
+            y = buf[:, off:off + c]
+        else:
+            y = torch.empty_like(x, memory_format=CL)
         sm = torch.empty(c, dtype=torch.float32, device=x.device)
         si = torch.empty(c, dtype=torch.float32, device=x.device)
         ws = workspace(lib.rtsds_bn_workspace(rows, c), x.device)
-        lib.rtsds_bn_fwd(_P(x), _P(res), _P(y), rows, c, _P(gamma), _P(beta), _P(running_mean),
-                         _P(running_var), _P(nbt), _P(sm), _P(si), float(momentum), float(eps), int(training),
-                         act, _P(stats) if training else None, int(stats_nrb or 0), dcode(x), _P(ws),
-                         ws.numel(), stream())
+        lib.rtsds_bn_fwd_ld(_P(x), _P(res), _P(y), ld, rows, c, _P(gamma), _P(beta), _P(running_mean),
+                            _P(running_var), _P(nbt), _P(sm), _P(si), float(momentum), float(eps), int(training),
+                            act, _P(stats) if training else None, int(stats_nrb or 0), dcode(x), _P(ws),
+                            ws.numel(), stream())
         ctx.meta = (rows, c, int(training), act, res is not None)
         ctx.gamma, ctx.beta = gamma, beta
         ctx.res_join = res_join
         # Without a residual the ReLU/LeakyReLU mask is recomputed from x in the backward
         # (bit-identical pre-activation), so y is neither kept nor re-read.
-        keep_y = res is not None or act == ACT_SIGMOID
         ctx.save_for_backward(x, y if keep_y else None, gamma, beta, sm, si)
         ctx.link = None
         if link is not None and BN_BWD_LINK and training and res is None and act in (0, 1, 2) \
@@ -595,7 +602,10 @@ class BatchNormFn(torch.autograd.Function):
     def backward(ctx, dy):
         x, y, gamma, beta, sm, si = ctx.saved_tensors
         rows, c, training, act, has_res = ctx.meta
-        dy = nhwc(dy)
+        ldy = _channel_slice_pitch(dy) if ctx.link is None else 0
+        if not ldy:
+            dy = nhwc(dy)
+            ldy = c
         need_dx, need_g, need_b, need_r = (ctx.needs_input_grad[0], ctx.needs_input_grad[1],
                                            ctx.needs_input_grad[2], ctx.needs_input_grad[3])
         dx = torch.empty_like(x, memory_format=CL) if need_dx else None
@@ -615,28 +625,42 @@ class BatchNormFn(torch.autograd.Function):
                                   _P(si), training, act, acc, _P(link.part), link.nrb, dcode(x), _P(ws), ws.numel(),
                                   stream())
         else:
-            lib.rtsds_bn_bwd(_P(dy), _P(x), _P(y), _P(dx), _P(dres), _P(dg), _P(db), rows, c,
-                             _P(gamma), _P(beta), _P(sm), _P(si), training, act, acc, dcode(x), _P(ws), ws.numel(),
-                             stream())
+            lib.rtsds_bn_bwd_ld(_P(dy), ldy, _P(x), _P(y), _P(dx), _P(dres), _P(dg), _P(db), rows, c,
+                                _P(gamma), _P(beta), _P(sm), _P(si), training, act, acc, dcode(x), _P(ws), ws.numel(),
+                                stream())
         if link is not None:
             link.src = link.part = None
         if acc:
             dg = db = None
         if dres is not None:
             dres = _join_add(ctx.res_join, dres)
-        return dx, dg, db, dres, None, None, None, None, None, None, None, None, None, None, None
+        return dx, dg, db, dres, None, None, None, None, None, None, None, None, None, None, None, None
+
+
+def _channel_slice_pitch(t):
+    """Row pitch of a bf16 [N, C, H, W] view that is a channel slice of a wider NHWC buffer
+    (C % 8 == 0, pitch % 8 == 0, pitch > C), else 0."""
+    if t.dim() != 4 or t.dtype != torch.bfloat16:
+        return 0
+    n, c, h, w = t.shape
+    ld = t.stride(3)
+    if c % 8 or ld % 8 or ld <= c or t.stride(1) != 1 or t.stride(2) != w * ld or (n > 1 and t.stride(0) != h * w * ld) \
+            or t.data_ptr() % 16:
+        return 0
+    return ld
 
 
 def batch_norm(x, gamma, beta, running_mean, running_var, training, momentum, eps, act=0,
-               residual=None, num_batches_tracked=None, res_join=None, link=None):
+               residual=None, num_batches_tracked=None, res_join=None, link=None, out=None):
     """``num_batches_tracked`` (int64, optional) is incremented by the finalize kernel.
-    ``res_join``: GradJoin shared with the other readers of ``residual``."""
+    ``res_join``: GradJoin shared with the other readers of ``residual``.  ``out``: (NHWC
+    buffer, channel offset) to write y into (a view of it is returned; bf16 without residual)."""
     st = getattr(x, "_rt_bn_stats", None) if training else None
     stats, nrb = st if st is not None else (None, None)
     if training and running_mean is not None:
         bump_params_epoch()  # running statistics change (raw-pointer write)
     return BatchNormFn.apply(x, gamma, beta, residual, running_mean, running_var, training,
-                             momentum, eps, act, stats, nrb, num_batches_tracked, res_join, link)
+                             momentum, eps, act, stats, nrb, num_batches_tracked, res_join, link, out)
 
 
 # ----------------------------------------------------------------------------- layout / dtype
@@ -759,15 +783,20 @@ class CatResizeFn(torch.autograd.Function):
     supervision convs, whose data gradients then accumulate into the resize adjoint's buffer)."""
 
     @staticmethod
-    def forward(ctx, size, joins, x0, *xs):
-        x0 = nhwc(x0)
+    def forward(ctx, size, joins, into, x0, *xs):
+        xs = [nhwc(x) for x in xs]
+        ct = x0.shape[1] + sum(x.shape[1] for x in xs)
+        # x0 already written as channels [0, c0) of ``into`` (its producer's pitched store): no copy
+        ctx.x0_in_place = into is not None and tuple(into.shape[1:]) == (ct,) + tuple(x0.shape[2:]) and \
+            x0.data_ptr() == into.data_ptr() and _channel_slice_pitch(x0) == ct
+        if not ctx.x0_in_place:
+            x0 = nhwc(x0)
         n, c0, h, w = x0.shape
         if (h, w) != (int(size[0]), int(size[1])):
             raise RuntimeError("rtsds_amd.concat_resized: x0 must have the target size")
-        xs = [nhwc(x) for x in xs]
-        ct = c0 + sum(x.shape[1] for x in xs)
-        y = empty_nhwc(n, ct, h, w, x0.dtype, x0.device)
-        lib.rtsds_copy_channels(_P(x0), c0, 0, _P(y), ct, 0, n * h * w, c0, 0, dcode(x0), stream())
+        y = into if ctx.x0_in_place else empty_nhwc(n, ct, h, w, x0.dtype, x0.device)
+        if not ctx.x0_in_place:
+            lib.rtsds_copy_channels(_P(x0), c0, 0, _P(y), ct, 0, n * h * w, c0, 0, dcode(x0), stream())
         off, geos = c0, []
         for x in xs:
             _, c, hi, wi = x.shape
@@ -783,13 +812,16 @@ class CatResizeFn(torch.autograd.Function):
     def backward(ctx, dy):
         n, c0, h, w, ct, geos = ctx.meta
         dy = nhwc(dy)
-        grads = [None, None, None]
-        if ctx.needs_input_grad[2]:
-            g0 = empty_nhwc(n, c0, h, w, dy.dtype, dy.device)
-            lib.rtsds_copy_channels(_P(dy), ct, 0, _P(g0), c0, 0, n * h * w, c0, 0, dcode(dy), stream())
-            grads[2] = g0
+        grads = [None, None, None, None]
+        if ctx.needs_input_grad[3]:
+            if ctx.x0_in_place:  # x0's producer reads its gradient from the slice in place
+                grads[3] = dy[:, :c0]
+            else:
+                g0 = empty_nhwc(n, c0, h, w, dy.dtype, dy.device)
+                lib.rtsds_copy_channels(_P(dy), ct, 0, _P(g0), c0, 0, n * h * w, c0, 0, dcode(dy), stream())
+                grads[3] = g0
         for k, (off, c, hi, wi, ho, wo, sh, sw) in enumerate(geos):
-            if not ctx.needs_input_grad[3 + k]:
+            if not ctx.needs_input_grad[4 + k]:
                 grads.append(None)
                 continue
             dx = empty_nhwc(n, c, hi, wi, dy.dtype, dy.device)
@@ -801,10 +833,12 @@ class CatResizeFn(torch.autograd.Function):
         return tuple(grads)
 
 
-def concat_resized(x0, xs, size, joins=None):
+def concat_resized(x0, xs, size, joins=None, into=None):
     """cat([x0] + [interpolate_bilinear(x, size) for x in xs], dim=1) without materialising the
-    resized maps (CatResizeFn).  ``joins``: per-xs GradJoin (or None) for inputs with other readers."""
-    return CatResizeFn.apply((int(size[0]), int(size[1])), tuple(joins) if joins else None, x0, *xs)
+    resized maps (CatResizeFn).  ``joins``: per-xs GradJoin (or None) for inputs with other readers.
+    ``into``: the preallocated NHWC output; when x0 already is its leading channel slice (e.g.
+    written there by nn.conv_bn(out=...)), x0 is neither copied in nor its gradient copied out."""
+    return CatResizeFn.apply((int(size[0]), int(size[1])), tuple(joins) if joins else None, into, x0, *xs)
 
 
 def concat_resized_scaled_eval(x0, parts, size, into=None):

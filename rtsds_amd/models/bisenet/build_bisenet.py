@@ -129,8 +129,9 @@ class BiSeNet(torch.nn.Module):
     inference_fusions = True
     # forward() starts with nn.to_input: runtime.GraphedForward may capture from the packed input
     accepts_packed_input = True
-    # inference: the spatial path's last conv writes straight into the fusion module's
-    # concatenated input (no copy of the 256-channel map)
+    # the spatial path's last ConvBlock writes straight into the fusion module's concatenated
+    # input and, in training, its BatchNorm backward reads its gradient slice in place (no copy
+    # of the 256-channel map or its gradient)
     spatial_into_concat = True
     # training: cx1 / cx2's two readers (supervision conv, fusion-module resize) share one
     # gradient buffer (functional.GradJoin first_returns) instead of autograd's add
@@ -173,6 +174,15 @@ class BiSeNet(torch.nn.Module):
         heads (build_bisenet.py:151-166).  main_only: skip the supervision heads (1x1 convs
         with no state; for callers that discard them, e.g. the DA target branch)."""
         x = to_input(input)
+        # the fusion module's concatenated input, allocated up front: the spatial path's last
+        # ConvBlock writes its channel slice in place (nn.conv_bn out=; inference: the folded conv
+        # epilogue, training: the BatchNorm apply), the context resizes the rest
+        into = None
+        if self.spatial_into_concat and x.is_cuda:
+            h8, w8 = x.shape[-2], x.shape[-1]
+            for _ in range(3):  # three 3x3 stride-2 pad-1 convs
+                h8, w8 = (h8 - 1) // 2 + 1, (w8 - 1) // 2 + 1
+            into = F.empty_nhwc(x.shape[0], self.feature_fusion_module.in_channels, h8, w8, x.dtype, x.device)
         # the 1/32 features have two readers, the context path's GAP (the tail) and ARM2's scale:
         # one gradient buffer (functional.GradJoin).  Only when ARM2 runs with autograd below.
         j4 = F.GradJoin(2) if self.training and torch.is_grad_enabled() else None
@@ -186,8 +196,10 @@ class BiSeNet(torch.nn.Module):
 
             def run_spatial():
                 x.record_stream(side)  # read (and saved for backward) on the branch stream
+                if into is not None:
+                    into.record_stream(side)
                 with torch.cuda.stream(side):
-                    box.append(BranchOut.apply(self.saptial_path(x), main, side))
+                    box.append(BranchOut.apply(self.saptial_path(x, out=None if into is None else (into, 0)), main, side))
 
             def fork():  # after the context path's layer1 (_ContextPath.fork_after): beside its later layers
                 if self.spatial_enqueued_last:
@@ -205,14 +217,6 @@ class BiSeNet(torch.nn.Module):
             main.wait_stream(side)
             sx.record_stream(main)
         else:
-            into = None
-            if self.spatial_into_concat and self.inference_fusions and not self.training and \
-                    not torch.is_grad_enabled() and x.is_cuda:
-                # the fusion module's input, allocated before the spatial path writes its slice
-                h8, w8 = x.shape[-2], x.shape[-1]
-                for _ in range(3):  # three 3x3 stride-2 pad-1 convs
-                    h8, w8 = (h8 - 1) // 2 + 1, (w8 - 1) // 2 + 1
-                into = F.empty_nhwc(x.shape[0], self.feature_fusion_module.in_channels, h8, w8, x.dtype, x.device)
             sx = self.saptial_path(x, out=None if into is None else (into, 0))
             f3, f4, tail = self.context_path(x, tail_join=j4)
         hw = sx.shape[-2:]
@@ -271,7 +275,7 @@ class BiSeNet(torch.nn.Module):
         # the two resizes write straight into the fusion module's concatenated input and read
         # their gradients straight from its gradient (functional.CatResizeFn; the reference:
         # interpolate, interpolate, cat)
-        result = self.feature_fusion_module(F.concat_resized(sx, (cx1, cx2), hw, joins=(j1, j2)))
+        result = self.feature_fusion_module(F.concat_resized(sx, (cx1, cx2), hw, joins=(j1, j2), into=into))
         if self.with_interpolation:
             # reference: conv(up8(result)) (build_bisenet.py:165-167).  A 1x1 conv mixes channels
             # per pixel and bilinear resize mixes pixels per channel with weights summing to 1,

@@ -59,7 +59,7 @@ class Conv2d(nn.Conv2d):
 
 
 class BatchNorm2d(nn.BatchNorm2d):
-    def forward(self, x, act=None, residual=None, res_join=None, link=None):
+    def forward(self, x, act=None, residual=None, res_join=None, link=None, out=None):
         training = self.training or not self.track_running_stats
         if training and x.shape[0] * x.shape[2] * x.shape[3] == 1:
             raise ValueError(f"Expected more than 1 value per channel when training, got input size {tuple(x.shape)}")
@@ -70,7 +70,7 @@ class BatchNorm2d(nn.BatchNorm2d):
         # num_batches_tracked.add_(1) happens inside the statistics-finalize kernel
         nbt = self.num_batches_tracked if (self.training and self.track_running_stats) else None
         return F.batch_norm(x, self.weight, self.bias, rm, rv, training, self.momentum, self.eps,
-                            ACT[act], residual, nbt, res_join, link)
+                            ACT[act], residual, nbt, res_join, link, out)
 
 
 class ReLU(nn.Module):
@@ -135,15 +135,16 @@ def conv_bn(conv, bn, x, act=None, residual=None, join=None, res_join=None, in_l
     functional.GradJoin shared by the readers of ``x`` / ``residual`` (residual blocks).
     ``in_link``: functional.BnBwdLink of the BatchNorm that produced ``x`` (its backward
     statistics come from this conv's data gradient); ``out_link``: the link this BatchNorm
-    registers with (its output's single reader passes it as ``in_link``).  ``out``: inference
-    only, a destination channel slice (functional.conv_bn_eval)."""
+    registers with (its output's single reader passes it as ``in_link``).  ``out``: (NHWC buffer,
+    channel offset) the result is written into (functional.conv_bn_eval at inference,
+    functional.batch_norm in training; a view of the slice is returned)."""
     use_batch = bn.training or not bn.track_running_stats
     if not use_batch and bn.momentum is not None and _no_grad_needed(conv, bn, x, residual):
         wq = _shadow(conv.weight, x.dtype)
         return F.conv_bn_eval(x, conv.weight, conv.bias, wq, conv.stride, conv.padding, conv.dilation,
                               bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.eps, ACT[act], residual, out=out)
     return bn(conv(x, bn_stats=use_batch, join=join, bn_link=in_link), act=act, residual=residual, res_join=res_join,
-              link=out_link)
+              link=out_link, out=out)
 
 
 def conv_bn_relu_maxpool(conv, bn, pool, x):

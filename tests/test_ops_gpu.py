@@ -313,6 +313,38 @@ def test_batchnorm_train(shape, act, res, dt):
     _close(rvd, rv, torch.float32, "running_var", 1e-3)
 
 
+@pytest.mark.parametrize("shape,ld,off", [((2, 64, 9, 13), 96, 16), ((4, 256, 8, 16), 1024, 0), ((1, 8, 3, 5), 24, 8)])
+def test_batchnorm_channel_slice_bit_identical(shape, ld, off):
+    """Train-mode BatchNorm + ReLU writing y into a channel slice of a wider NHWC buffer
+    (batch_norm out=, rtsds_bn_fwd_ld) and reading its gradient from such a slice in place
+    (rtsds_bn_bwd_ld): y, dx, dgamma, dbeta and the running statistics bit-identical to the
+    dense call; the rest of the buffer untouched."""
+    g = torch.Generator().manual_seed(sum(shape) + ld)
+    n, c, h, w = shape
+    x = _dev(torch.randn(shape, generator=g) * 2 + 3, torch.bfloat16)
+    gy = torch.randn(n, ld, h, w, generator=g).to(DEV).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    gam = (1 + 0.1 * torch.randn(c, generator=g)).to(DEV)
+    bet = (0.1 * torch.randn(c, generator=g)).to(DEV)
+    outs = []
+    for sliced in (False, True):
+        xd = x.clone().requires_grad_()
+        gp, bp = gam.clone().requires_grad_(), bet.clone().requires_grad_()
+        rm, rv = torch.zeros(c, device=DEV), torch.ones(c, device=DEV)
+        buf = None
+        if sliced:
+            buf = torch.full((n, ld, h, w), 7.0, device=DEV, dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        y = F.batch_norm(xd, gp, bp, rm, rv, True, 0.1, 1e-5, 1, None, out=None if buf is None else (buf, off))
+        if sliced:
+            assert y.data_ptr() == buf.data_ptr() + 2 * off and y.stride(3) == ld
+            assert torch.equal(buf[:, :off].float(), torch.full_like(buf[:, :off].float(), 7.0))
+            assert torch.equal(buf[:, off + c:].float(), torch.full_like(buf[:, off + c:].float(), 7.0))
+        y.backward(gy[:, off:off + c] if sliced else gy[:, off:off + c].contiguous(memory_format=torch.channels_last))
+        torch.cuda.synchronize()
+        outs.append([t.detach().float().cpu() for t in (y, xd.grad, gp.grad, bp.grad, rm, rv)])
+    for a, b_, what in zip(outs[0], outs[1], ("y", "dx", "dgamma", "dbeta", "running_mean", "running_var")):
+        assert torch.equal(a, b_), what
+
+
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 def test_batchnorm_eval(dt):
     g = torch.Generator().manual_seed(5)
