@@ -315,7 +315,7 @@ __global__ void __launch_bounds__(256) pooled_dgrad_kernel(const T* __restrict__
   for (int m = 0; m < MR; ++m)
     if (m < m_n) {
       const long o = (long)m * c + ci;
-      dx[o] = from_f<T>(accum ? acc[m] + to_f(dx[o]) : acc[m]);
+      dx[o] = from_f<T>(accum ? to_f(from_f<T>(acc[m])) + to_f(dx[o]) : acc[m]);
     }
 }
 
@@ -436,7 +436,8 @@ __global__ void __launch_bounds__(256) pooled_dgrad_vec_kernel(const bf16* __res
   const int m = lane >> 3;
   if (m < m_n) {
     const long off = (long)m * c + ci0 + (lane & 7);
-    dx[off] = (bf16)(accum ? v[0] + (float)dx[off] : v[0]);
+    // accumulate: rounded first, then added (= storing it and adding the two bf16 gradients)
+    dx[off] = (bf16)(accum ? (float)(bf16)v[0] + (float)dx[off] : v[0]);
   }
 }
 

@@ -1098,10 +1098,10 @@ def global_avg_pool(x, join=None):
 
 class ChScaleFn(torch.autograd.Function):
     """x * a[N,C,1,1] (mode 0) or x * a + x (mode 1).  ``join``: GradJoin shared with x's
-    other reader (GapFn)."""
+    other reader (GapFn); ``join_a``: the same for a's other reader."""
 
     @staticmethod
-    def forward(ctx, x, a, mode, join=None):
+    def forward(ctx, x, a, mode, join=None, join_a=None):
         require_hip(x, a)
         x = nhwc(x)
         a = a.contiguous()
@@ -1111,7 +1111,7 @@ class ChScaleFn(torch.autograd.Function):
         y = torch.empty_like(x, memory_format=CL)
         lib.rtsds_chscale_fwd(_P(x), _P(a), _P(y), n, h * w, c, mode, dcode(x), stream())
         ctx.mode = mode
-        ctx.join = join
+        ctx.join, ctx.join_a = join, join_a
         ctx.save_for_backward(x, a)
         return y
 
@@ -1127,12 +1127,14 @@ class ChScaleFn(torch.autograd.Function):
                               dcode(x), _P(ws), ws.numel(), stream())
         if dx is not None and ctx.join is not None:
             dx = _join_add(ctx.join, dx)
-        return dx, da, None, None
+        if da is not None and ctx.join_a is not None:
+            da = _join_add(ctx.join_a, da)
+        return dx, da, None, None, None
 
 
-def channel_scale(x, a, residual=False, join=None):
-    """``join``: GradJoin shared with x's other reader (see GapFn)."""
-    return ChScaleFn.apply(x, a, 1 if residual else 0, join)
+def channel_scale(x, a, residual=False, join=None, join_a=None):
+    """``join`` / ``join_a``: GradJoin shared with x's / a's other reader (see GapFn)."""
+    return ChScaleFn.apply(x, a, 1 if residual else 0, join, join_a)
 
 
 # ----------------------------------------------------------------------------- bilinear

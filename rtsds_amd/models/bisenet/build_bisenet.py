@@ -58,24 +58,27 @@ class AttentionRefinementModule(torch.nn.Module):
         self.in_channels = in_channels
         self.avgpool = AdaptiveAvgPool2d(output_size=(1, 1))
 
-    def attention(self, input, pooled=None, join=None):
+    def attention(self, input, pooled=None, join=None, pooled_join=None):
         """sigmoid(BN(conv(GAP(input)))) [N, C, 1, 1]; ``pooled``: GAP(input) when the caller
         already has it (BiSeNet's ARM2 reads the context path's tail, the same kernel on the
-        same tensor); ``join``: GradJoin of input's two readers (the pool and the scale)."""
+        same tensor); ``join``: GradJoin of input's two readers (the pool and the scale);
+        ``pooled_join``: GradJoin of the caller's pooled tensor's readers."""
         if pooled is None:
             pooled = F.global_avg_pool(input, join)
         assert self.in_channels == pooled.size(1), \
             "in_channels and out_channels should all be {}".format(pooled.size(1))
-        return conv_bn(self.conv, self.bn, pooled, "sigmoid")
+        return conv_bn(self.conv, self.bn, pooled, "sigmoid", join=pooled_join)
 
-    def forward(self, input, pooled=None, join=None):
-        """``join``: with ``pooled``, the caller's GradJoin of input's readers (the pool that made
-        ``pooled`` and this scale)."""
+    def forward(self, input, pooled=None, join=None, pooled_join=None):
+        """``join``: the caller's GradJoin of input's readers (with ``pooled``: the pool that
+        made it and this scale; without: this module's pool and scale plus the caller's other
+        readers).  ``pooled_join``: see attention()."""
         # input's two readers (the pool and the scale) share one gradient buffer: the pool's
         # backward adds into the scale's (no autograd sum of two full-size gradients)
-        if pooled is None:
+        if pooled is None and join is None:
             join = F.GradJoin(2) if torch.is_grad_enabled() and input.requires_grad else None
-        return F.channel_scale(input, self.attention(input, pooled, join if pooled is None else None), join=join)
+        att = self.attention(input, pooled, join if pooled is None else None, pooled_join)
+        return F.channel_scale(input, att, join=join)
 
 
 class FeatureFusionModule(torch.nn.Module):
@@ -133,9 +136,10 @@ class BiSeNet(torch.nn.Module):
     # input and, in training, its BatchNorm backward reads its gradient slice in place (no copy
     # of the 256-channel map or its gradient)
     spatial_into_concat = True
-    # training: cx1 / cx2's two readers (supervision conv, fusion-module resize) share one
-    # gradient buffer (functional.GradJoin first_returns) instead of autograd's add
-    supervision_joins = True
+    # training: the tensors read by two modules share one gradient buffer (functional.GradJoin
+    # first_returns) instead of autograd's add: cx1 / cx2 (supervision conv, fusion-module
+    # resize) and the tail (ARM2's attention conv, cx2's scale)
+    feature_joins = True
 
     def __init__(self, num_classes, context_path, with_interpolation=True):
         super().__init__()
@@ -186,6 +190,10 @@ class BiSeNet(torch.nn.Module):
         # the 1/32 features have two readers, the context path's GAP (the tail) and ARM2's scale:
         # one gradient buffer (functional.GradJoin).  Only when ARM2 runs with autograd below.
         j4 = F.GradJoin(2) if self.training and torch.is_grad_enabled() else None
+        # the tail's readers (ARM2's attention conv, cx2's scale); not the 1/16 features' two
+        # (layer4, ARM1): joining those would regroup the bf16 roundings of four contributions
+        fj = self.training and torch.is_grad_enabled() and self.feature_joins
+        jt = F.GradJoin(0, first_returns=True) if fj else None
         if self.branch_parallel and self.training and x.is_cuda and F.CONV_PROFILE is None and branches_enabled():
             # (not while bench.py event-times each conv: concurrent branches would inflate them)
             # spatial path on the branch stream, concurrently with the context path (forward and,
@@ -234,7 +242,8 @@ class BiSeNet(torch.nn.Module):
         if cat is None:
             cx1 = self.attention_refinement_module1(f3)
             # ARM2's global average pool is the tail itself (same kernel, same f4)
-            cx2 = F.channel_scale(self.attention_refinement_module2(f4, pooled=tail, join=j4), tail)
+            cx2 = F.channel_scale(self.attention_refinement_module2(f4, pooled=tail, join=j4, pooled_join=jt), tail,
+                                  join_a=jt)
         if infer:
             if cat is None:  # a geometry outside the fused resize
                 cat = F.concat_resized(sx, (cx1, cx2), hw)
@@ -265,7 +274,7 @@ class BiSeNet(torch.nn.Module):
             # supervision conv's data gradient accumulating into the resize adjoint's (or the
             # reverse), instead of autograd's add of two full gradients; first_returns: correct
             # also when a caller leaves the supervision outputs out of its loss
-            if torch.is_grad_enabled() and self.supervision_joins:
+            if torch.is_grad_enabled() and self.feature_joins:
                 j1 = F.GradJoin(2, first_returns=True) if cx1.requires_grad else None
                 j2 = F.GradJoin(2, first_returns=True) if cx2.requires_grad else None
             full = input.shape[-2:]

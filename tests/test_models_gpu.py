@@ -786,9 +786,10 @@ def test_bisenet_branch_streams_bit_identical(graphed):
 
 
 @pytest.mark.parametrize("graphed", [False, True])
-def test_bisenet_supervision_joins_bit_identical(graphed):
-    """BiSeNet.supervision_joins (cx1 / cx2's gradient accumulated in place by the supervision
-    conv's data gradient instead of autograd's add of the two bf16 gradients) leaves losses,
+def test_bisenet_feature_joins_bit_identical(graphed):
+    """BiSeNet.feature_joins (cx1 / cx2 and the tail: the gradient of a tensor with two
+    reading modules accumulated in place by the second instead of autograd's
+    add of the two bf16 gradients) leaves losses,
     the accuracy count (overwritten by the fused CE, never zeroed), parameters and optimizer
     state bit-identical, eagerly and as hipGraph replays."""
     from rtsds_amd.runtime import GraphedStep
@@ -799,7 +800,7 @@ def test_bisenet_supervision_joins_bit_identical(graphed):
     runs = []
     with rtsds_amd.precision(torch.bfloat16):
         for joins in (False, True):
-            BiSeNet.supervision_joins = joins
+            BiSeNet.feature_joins = joins
             try:
                 torch.manual_seed(3)
                 net = BiSeNet(19, "resnet18").to(DEV).train()
@@ -812,7 +813,7 @@ def test_bisenet_supervision_joins_bit_identical(graphed):
                 st.update({f"m{i}": a.m.cpu() for i, a in enumerate(opt.arenas())})
                 runs.append((ls, st))
             finally:
-                BiSeNet.supervision_joins = True
+                BiSeNet.feature_joins = True
     (l0, s0), (l1, s1) = runs
     assert l0 == l1
     assert all(c > 0 for _, c in l1)
@@ -854,7 +855,7 @@ def test_bisenet_spatial_into_concat_train_bit_identical(graphed):
         assert torch.equal(s0[k], s1[k]), k
 
 
-def test_bisenet_supervision_joins_main_head_only():
+def test_bisenet_feature_joins_main_head_only():
     """A caller that leaves the supervision outputs out of its loss: with the joins (first
     contribution returned, GradJoin first_returns) cx1 / cx2 still receive the resize
     adjoint's gradient -- every parameter gradient equal to the unjoined model's."""
@@ -863,7 +864,7 @@ def test_bisenet_supervision_joins_main_head_only():
     grads = []
     with rtsds_amd.precision(torch.bfloat16):
         for joins in (False, True):
-            BiSeNet.supervision_joins = joins
+            BiSeNet.feature_joins = joins
             try:
                 torch.manual_seed(4)
                 net = BiSeNet(19, "resnet18").to(DEV).train()
@@ -873,7 +874,7 @@ def test_bisenet_supervision_joins_main_head_only():
                 grads.append({k: p.grad.detach().float().cpu().clone() for k, p in net.named_parameters()
                               if p.grad is not None})
             finally:
-                BiSeNet.supervision_joins = True
+                BiSeNet.feature_joins = True
     assert grads[0].keys() == grads[1].keys()
     assert any(k.startswith("attention_refinement_module1") for k in grads[1])
     for k in grads[0]:
