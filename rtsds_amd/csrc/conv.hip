@@ -140,16 +140,30 @@ __global__ void __launch_bounds__(256) colsum_part_kernel(const T* __restrict__ 
   float acc[VEC];
 #pragma unroll
   for (int j = 0; j < VEC; ++j) acc[j] = 0.f;
-  if (rg < rpi)
-    for (long r = (long)blockIdx.x * rpi + rg; r < rows; r += (long)gridDim.x * rpi) {
-      if (VEC > 1) {
-        typename VecT<T>::v16 v = *(const typename VecT<T>::v16*)(dy + r * c + ch0);
+  if (rg < rpi) {
+    // 4 rows' loads in flight (clamped, unconditional), then the adds in row order
+    const long step = (long)gridDim.x * rpi;
+    for (long r = (long)blockIdx.x * rpi + rg; r < rows; r += 4 * step) {
+      typename VecT<T>::v16 v[4];
+      T sv[4];
 #pragma unroll
-        for (int j = 0; j < VEC; ++j) acc[j] += to_f(v[j]);
-      } else {
-        acc[0] += to_f(dy[r * c + ch0]);
+      for (int u = 0; u < 4; ++u) {
+        const long rr = min(r + u * step, rows - 1);
+        if (VEC > 1) v[u] = *(const typename VecT<T>::v16*)(dy + rr * c + ch0);
+        else sv[u] = dy[rr * c + ch0];
       }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (r + u * step < rows) {
+          if (VEC > 1) {
+#pragma unroll
+            for (int j = 0; j < VEC; ++j) acc[j] += to_f(v[u][j]);
+          } else {
+            acc[0] += to_f(sv[u]);
+          }
+        }
     }
+  }
 #pragma unroll
   for (int j = 0; j < VEC; ++j) red[tid * VEC + j] = acc[j];
   __syncthreads();
@@ -165,7 +179,14 @@ __global__ void __launch_bounds__(256) colsum_part_kernel(const T* __restrict__ 
 __global__ void colsum_final_kernel(const float* __restrict__ part, float* __restrict__ out, int rb, int c, int accumulate) {
   const int cc = blockIdx.x, lane = threadIdx.x;
   float s = 0.f;
-  for (int i = lane; i < rb; i += 64) s += part[(long)i * c + cc];
+  for (int i0 = lane; i0 < rb; i0 += 64 * 8) {  // 8 partials in flight (clamped), added in order
+    float t[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) t[u] = part[(long)min(i0 + 64 * u, rb - 1) * c + cc];
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (i0 + 64 * u < rb) s += t[u];
+  }
   s = wave_sum(s);
   if (lane == 0) out[cc] = accumulate ? out[cc] + s : s;
 }
@@ -327,10 +348,20 @@ __global__ void __launch_bounds__(256) pooled_wgrad_kernel(const T* __restrict__
   if (i >= k_n * c) return;
   const int k = i / c, ci = i - k * c;
   float acc = 0.f, bsum = 0.f;
-  for (int m = 0; m < m_n; ++m) {
-    const float g = to_f(dy[(long)m * k_n + k]);
-    acc = fmaf(g, to_f(x[(long)m * c + ci]), acc);
-    bsum += g;
+  for (int m0 = 0; m0 < m_n; m0 += 8) {  // 8 rows' loads in flight (clamped), then the FMAs in order
+    float g[8], xv[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int m = min(m0 + u, m_n - 1);
+      g[u] = to_f(dy[(long)m * k_n + k]);
+      xv[u] = to_f(x[(long)m * c + ci]);
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (m0 + u < m_n) {
+        acc = fmaf(g[u], xv[u], acc);
+        bsum += g[u];
+      }
   }
   dw[i] = accum ? dw[i] + acc : acc;
   if (dbias && ci == 0) dbias[k] = accum ? dbias[k] + bsum : bsum;
