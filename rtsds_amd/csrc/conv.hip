@@ -1282,6 +1282,94 @@ static int dgrad_impl(const rtsds_conv_desc* d0, const void* dy, const void* w, 
 // WGRAD split-K: enough (M/BM)*(N/BN)*splits workgroups to fill 256 CUs ~2x, each split at
 // least 8 K-tiles; fp32 partial slabs summed (and channel-unpadded) by split_reduce_kernel --
 // deterministic, no atomics.
+// ---- narrow pointwise weight + bias gradient (1x1, stride 1, Cin and Cout <= 32: BiSeNet's final
+// 19 -> 19 conv, build_bisenet.py:117).  As a GEMM it needed dY and x padded to 32 channels, a
+// split-K launch, its reduce and the bias column sums' two launches -- six launches for 0.05 GFLOP.
+// Here: pass 1, one workgroup per run of kPwnRows pixels stages 64-pixel tiles of dY and x in LDS
+// and accumulates every (co, ci) product and the dY column sums -> part[block][k*c dW | k db];
+// pass 2 (one wave per output) sums the blocks in a fixed order.
+static constexpr int kPwnRows = 128;
+static bool pwn_wgrad_ok(const rtsds_conv_desc* d) {
+  // (k <= 28: 9 threads per output row in a 256-thread workgroup)
+  return d->kh == 1 && d->kw == 1 && d->sh == 1 && d->sw == 1 && d->ph == 0 && d->pw == 0 && d->k <= 28 && d->c <= 32;
+}
+static int pwn_blocks(const rtsds_conv_desc* d) {
+  return (int)std::min<long>(4096, ((long)d->n * d->h * d->w + kPwnRows - 1) / kPwnRows);
+}
+template <typename T>
+__global__ void __launch_bounds__(256) pwn_wgrad_part_kernel(const T* __restrict__ dy, const T* __restrict__ x, float* __restrict__ part,
+                                                             long P, int k, int c, int ldx, int per) {
+  // thread t: output row co = t / 9, column group g = t % 9 -- dW[co][4g .. 4g + 3] for g < 8, the
+  // bias sum (x's ones column 32) for g = 8; one dY read and one 16-B x read per pixel, 4 FMAs
+  __shared__ float sdy[64][33];
+  __shared__ __attribute__((aligned(16))) float sx[64][36];
+  const long p0 = (long)blockIdx.x * per, p1 = min(P, p0 + per);
+  const int co = threadIdx.x / 9, g = threadIdx.x - co * 9;
+  const bool active = co < k && (g == 8 || 4 * g < c);
+  const int coc = min(co, 31);
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (long pb = p0; pb < p1; pb += 64) {
+    const int np = (int)min(64L, p1 - pb);
+    __syncthreads();
+    // 64 x 32 elements of each tensor, 8 per thread: clamped unconditional loads, then the
+    // zero fill past the pixels / channels selected
+    float vd[8], vx[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int e = threadIdx.x + 256 * u, r = e >> 5, ch = e & 31;
+      const long pr = pb + min(r, np - 1);
+      vd[u] = to_f(dy[pr * k + min(ch, k - 1)]);
+      vx[u] = to_f(x[pr * ldx + min(ch, c - 1)]);
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int e = threadIdx.x + 256 * u, r = e >> 5, ch = e & 31;
+      sdy[r][ch] = (r < np && ch < k) ? vd[u] : 0.f;
+      sx[r][ch] = (r < np && ch < c) ? vx[u] : 0.f;
+    }
+    if (threadIdx.x < 64) *(f32x4*)&sx[threadIdx.x][32] = f32x4{threadIdx.x < np ? 1.f : 0.f, 0.f, 0.f, 0.f};
+    __syncthreads();
+    if (active) {
+#pragma unroll 8
+      for (int r = 0; r < 64; ++r) {
+        const float d = sdy[r][coc];
+        const f32x4 v = *(const f32x4*)&sx[r][4 * g];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[j] = fmaf(d, v[j], acc[j]);
+      }
+    }
+  }
+  if (!active) return;
+  const int no = k * c + k;
+  float* out = part + (long)blockIdx.x * no;
+  if (g == 8) {
+    out[k * c + co] = acc[0];
+  } else {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (4 * g + j < c) out[co * c + 4 * g + j] = acc[j];
+  }
+}
+// one wave per output: lane l sums the partials of blocks l, l + 64, ... (8 in flight, in
+// order), then the wave's fixed shuffle tree
+__global__ void __launch_bounds__(64) pwn_wgrad_final_kernel(const float* __restrict__ part, float* __restrict__ dw,
+                                                             float* __restrict__ dbias, int nb, int k, int c, int accum) {
+  const int no = k * c + k, o = blockIdx.x, lane = threadIdx.x;
+  float s = 0.f;
+  for (int b0 = lane; b0 < nb; b0 += 64 * 8) {
+    float t[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) t[u] = part[(long)min(b0 + 64 * u, nb - 1) * no + o];
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (b0 + 64 * u < nb) s += t[u];
+  }
+  s = wave_sum(s);
+  if (lane != 0) return;
+  if (o < k * c) dw[o] = accum ? dw[o] + s : s;
+  else if (dbias) dbias[o - k * c] = accum ? dbias[o - k * c] + s : s;
+}
+
 struct WgradPlan {
   int kp, cp, bm, bn, splits, tps;
   size_t slab_bytes, dyp_bytes, xp_bytes, colsum_bytes;
@@ -1344,7 +1432,8 @@ extern "C" size_t rtsds_conv2d_wgrad_workspace(const rtsds_conv_desc* d) {
     return w.slab_bytes + w.colsum_bytes + sp_x4_bytes(d) + al256((size_t)v.k * v.kh * v.kw * 8 * 4);
   }
   const WgradPlan w = wgrad_plan(d);
-  return w.slab_bytes + w.dyp_bytes + w.xp_bytes + w.colsum_bytes;
+  const size_t pwn = pwn_wgrad_ok(d) ? al256((size_t)pwn_blocks(d) * (d->k * d->c + d->k) * 4) : 0;
+  return std::max(w.slab_bytes + w.dyp_bytes + w.xp_bytes + w.colsum_bytes, pwn);
 }
 
 
@@ -1440,6 +1529,21 @@ static int wgrad_impl(const rtsds_conv_desc* d0, const void* x, const void* dy, 
   if (pooled_1x1(d0)) {
     if (d0->dtype == RTSDS_BF16) pooled_wgrad_launch<bf16>(d0, x, dy, dw, dbias, accumulate ? 1 : 0, st);
     else pooled_wgrad_launch<float>(d0, x, dy, dw, dbias, accumulate ? 1 : 0, st);
+    return hipGetLastError() == hipSuccess ? RTSDS_OK : RTSDS_ERR_LAUNCH;
+  }
+  if (pwn_wgrad_ok(d0)) {
+    const long P = (long)d0->n * d0->h * d0->w;
+    const int nb = pwn_blocks(d0), per = (int)((P + nb - 1) / nb), no = d0->k * d0->c + d0->k;
+    const int ldx = x_padded ? pad_c(d0->c, d0->dtype) : d0->c;
+    float* part = (float*)ws;
+    if (d0->dtype == RTSDS_BF16)
+      hipLaunchKernelGGL(pwn_wgrad_part_kernel<bf16>, dim3(nb), dim3(256), 0, st, (const bf16*)dy, (const bf16*)x, part, P, d0->k,
+                         d0->c, ldx, per);
+    else
+      hipLaunchKernelGGL(pwn_wgrad_part_kernel<float>, dim3(nb), dim3(256), 0, st, (const float*)dy, (const float*)x, part, P,
+                         d0->k, d0->c, ldx, per);
+    hipLaunchKernelGGL(pwn_wgrad_final_kernel, dim3(no), dim3(64), 0, st, (const float*)part, dw, dbias, nb, d0->k, d0->c,
+                       accumulate ? 1 : 0);
     return hipGetLastError() == hipSuccess ? RTSDS_OK : RTSDS_ERR_LAUNCH;
   }
   const bool sp = sp_path(d0);
