@@ -459,10 +459,20 @@ int rtsds_capture_nodes(void* stream);
 int rtsds_graph_split_launch(void* handle, void* stream);
 int rtsds_graph_split_destroy(void* handle);
 
+/* Backward of the FFM attention on pooled vectors (build_bisenet.py:67-70): h = relu(conv1(p)),
+ * a = sigmoid(conv2(h)), 1x1 convs on [n][c] rows (n <= 8, channels <= 64).  From da = dL/da:
+ * dw2 / db2, dw1 / db1 (fp32 [cout][cin] / [cout]; overwritten, or added to when accumulate),
+ * dp = dL/dp (stored).  w1 [c1][c0], w2 [c2][c1] in the compute dtype.  One launch; the
+ * results equal the unfused chain's (act backward, pooled data / weight gradients) bit for bit
+ * for channel counts that are not vector multiples (c % 8 bf16, c % 4 fp32).               */
+int rtsds_pooled_mlp_bwd(const void* da, const void* a, const void* h, const void* p, const void* w1,
+                         const void* w2, float* dw1, float* db1, float* dw2, float* db2, void* dp,
+                         int n, int c0, int c1, int c2, int accumulate, int dtype, void* stream);
+
 /* ABI revision of this header (RTSDS_ABI_VERSION): bumped whenever an entry point's signature
  * changes.  The Python loader refuses a library whose revision differs (A/B variant libraries
  * built from older sources would otherwise be called with the wrong argument lists). */
-#define RTSDS_ABI_VERSION 9
+#define RTSDS_ABI_VERSION 10
 int rtsds_abi_version(void);
 
 #ifdef __cplusplus

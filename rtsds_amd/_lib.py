@@ -13,7 +13,7 @@ import torch  # noqa: F401  (must precede the dlopen below)
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # RTSDS_LIB: alternative in-tree build of the same ABI (kernel-variant A/B measurements)
 DEFAULT_LIB_PATH = os.path.join(_HERE, "librtsds_hip.so")
-ABI_VERSION = 9  # include/rtsds_hip.h RTSDS_ABI_VERSION
+ABI_VERSION = 10  # include/rtsds_hip.h RTSDS_ABI_VERSION
 LIB_PATH = os.environ.get("RTSDS_LIB") or DEFAULT_LIB_PATH
 
 F32, BF16 = 0, 1
@@ -68,6 +68,7 @@ SIGNATURES = {
     "rtsds_bn_fwd_ld": (c_int, [P, P, P, c_long, c_long, c_int, P, P, P, P, P, P, P, c_float, c_float, c_int,
                                 c_int, P, c_int, c_int, P, c_size_t, P]),
     "rtsds_bn_fold": (c_int, [P, P, P, P, P, c_float, c_int, P, P, P]),
+    "rtsds_pooled_mlp_bwd": (c_int, [P, P, P, P, P, P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, P]),
     "rtsds_bn_bwd_part": (c_int, [P, P, P, P, P, c_long, c_int, P, P, P, P, c_int, c_int, c_int, P, c_int, c_int, P,
                                   c_size_t, P]),
     "rtsds_bn_bwd": (c_int, [P, P, P, P, P, P, P, c_long, c_int, P, P, P, P, c_int, c_int, c_int, c_int,

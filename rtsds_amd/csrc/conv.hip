@@ -367,6 +367,139 @@ __global__ void __launch_bounds__(256) pooled_wgrad_kernel(const T* __restrict__
   if (dbias && ci == 0) dbias[k] = accum ? dbias[k] + bsum : bsum;
 }
 
+// ---- the FFM attention's backward in one launch (build_bisenet.py:67-70: conv1 + ReLU, conv2 +
+// sigmoid on the pooled [N, C] vectors).  The unfused chain was six launches of a few hundred
+// values each (sigmoid backward, conv2 data / weight gradient, ReLU backward, conv1 data /
+// weight gradient).  One workgroup runs the same arithmetic in the same order -- the activation
+// gradients rounded to the storage type as act_bwd_kernel stores them, the data gradients as
+// pooled_dgrad_kernel forms them (a wave per input channel, lanes over output channels, the
+// wave's shuffle sum), the weight gradients as pooled_wgrad_kernel (sums over rows in order) --
+// so every result is bit-identical to the chain.
+static constexpr int kMlpMaxC = 64, kMlpMaxN = 8, kMlpThreads = 1024;  // 16 waves: a wave per input channel or two
+template <typename T>
+__global__ void __launch_bounds__(kMlpThreads) pooled_mlp_bwd_kernel(const T* __restrict__ da, const T* __restrict__ a, const T* __restrict__ h,
+                                                             const T* __restrict__ p, const T* __restrict__ w1, const T* __restrict__ w2,
+                                                             float* __restrict__ dw1, float* __restrict__ db1, float* __restrict__ dw2,
+                                                             float* __restrict__ db2, T* __restrict__ dp, int n, int c0, int c1, int c2,
+                                                             int accum) {
+  __shared__ float sg2[kMlpMaxN][kMlpMaxC], sg1[kMlpMaxN][kMlpMaxC], sh[kMlpMaxN][kMlpMaxC], sp[kMlpMaxN][kMlpMaxC];
+  __shared__ float sw1[kMlpMaxC * kMlpMaxC], sw2[kMlpMaxC * kMlpMaxC];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // every operand staged in LDS up front, each thread's loads clamped and unconditional (one
+  // memory round trip for the launch; a load per loop iteration serialised them)
+  {
+    constexpr int NW = kMlpMaxC * kMlpMaxC / kMlpThreads, NV = (kMlpMaxN * kMlpMaxC + kMlpThreads - 1) / kMlpThreads;
+    const int n1 = c1 * c0, n2 = c2 * c1;
+    float v1[NW], v2[NW], vd[NV], va[NV], vh[NV], vp[NV];
+#pragma unroll
+    for (int u = 0; u < NW; ++u) {
+      const int e = tid + kMlpThreads * u;
+      v1[u] = to_f(w1[min(e, n1 - 1)]);
+      v2[u] = to_f(w2[min(e, n2 - 1)]);
+    }
+    // (m, ch) = (e / 64, e % 64) of the [kMlpMaxN][kMlpMaxC] arrays, zero outside [n][c]
+#pragma unroll
+    for (int u = 0; u < NV; ++u) {
+      const int e = tid + kMlpThreads * u, m = min(e >> 6, n - 1), ch = e & 63;
+      vd[u] = to_f(da[m * c2 + min(ch, c2 - 1)]);
+      va[u] = to_f(a[m * c2 + min(ch, c2 - 1)]);
+      vh[u] = to_f(h[m * c1 + min(ch, c1 - 1)]);
+      vp[u] = to_f(p[m * c0 + min(ch, c0 - 1)]);
+    }
+#pragma unroll
+    for (int u = 0; u < NW; ++u) {
+      const int e = tid + kMlpThreads * u;
+      if (e < n1) sw1[e] = v1[u];
+      if (e < n2) sw2[e] = v2[u];
+    }
+#pragma unroll
+    for (int u = 0; u < NV; ++u) {
+      const int e = tid + kMlpThreads * u, m = e >> 6, ch = e & 63;
+      if (m >= kMlpMaxN) break;
+      // sigmoid backward (act_bwd_kernel, act 3): g * s * (1 - s), stored rounded
+      sg2[m][ch] = m < n && ch < c2 ? to_f(from_f<T>(vd[u] * va[u] * (1.f - va[u]))) : 0.f;
+      sh[m][ch] = m < n && ch < c1 ? vh[u] : 0.f;
+      sp[m][ch] = m < n && ch < c0 ? vp[u] : 0.f;
+      sg1[m][ch] = 0.f;
+    }
+  }
+  __syncthreads();
+  // conv2 weight / bias gradient (pooled_wgrad_kernel): dw2[k][ci] over the rows in order
+  for (int i = tid; i < c2 * c1; i += kMlpThreads) {
+    const int k = i / c1, ci = i - k * c1;
+    float acc = 0.f, bsum = 0.f;
+    for (int m = 0; m < n; ++m) {
+      acc = fmaf(sg2[m][k], sh[m][ci], acc);
+      bsum += sg2[m][k];
+    }
+    dw2[i] = accum ? dw2[i] + acc : acc;
+    if (db2 && ci == 0) db2[k] = accum ? db2[k] + bsum : bsum;
+  }
+  // conv2 data gradient (pooled_dgrad_kernel), then the ReLU backward (act_bwd_kernel, act 1)
+  for (int ci = wave; ci < c1; ci += kMlpThreads / 64) {
+    float acc[kMlpMaxN];
+#pragma unroll
+    for (int m = 0; m < kMlpMaxN; ++m) acc[m] = 0.f;
+    for (int k = lane; k < c2; k += 64) {
+      const float wv = sw2[k * c1 + ci];
+#pragma unroll
+      for (int m = 0; m < kMlpMaxN; ++m) acc[m] = fmaf(sg2[m][k], wv, acc[m]);  // (rows past n: zero)
+    }
+#pragma unroll
+    for (int m = 0; m < kMlpMaxN; ++m) acc[m] = wave_sum(acc[m]);
+    if (lane == 0)
+#pragma unroll
+      for (int m = 0; m < kMlpMaxN; ++m)
+        if (m < n) sg1[m][ci] = sh[m][ci] > 0.f ? to_f(from_f<T>(acc[m])) : 0.f;
+  }
+  __syncthreads();
+  // conv1 weight / bias gradient, data gradient into dp (stored, not accumulated)
+  for (int i = tid; i < c1 * c0; i += kMlpThreads) {
+    const int k = i / c0, ci = i - k * c0;
+    float acc = 0.f, bsum = 0.f;
+    for (int m = 0; m < n; ++m) {
+      acc = fmaf(sg1[m][k], sp[m][ci], acc);
+      bsum += sg1[m][k];
+    }
+    dw1[i] = accum ? dw1[i] + acc : acc;
+    if (db1 && ci == 0) db1[k] = accum ? db1[k] + bsum : bsum;
+  }
+  for (int ci = wave; ci < c0; ci += kMlpThreads / 64) {
+    float acc[kMlpMaxN];
+#pragma unroll
+    for (int m = 0; m < kMlpMaxN; ++m) acc[m] = 0.f;
+    for (int k = lane; k < c1; k += 64) {
+      const float wv = sw1[k * c0 + ci];
+#pragma unroll
+      for (int m = 0; m < kMlpMaxN; ++m) acc[m] = fmaf(sg1[m][k], wv, acc[m]);
+    }
+#pragma unroll
+    for (int m = 0; m < kMlpMaxN; ++m) acc[m] = wave_sum(acc[m]);
+    if (lane == 0)
+#pragma unroll
+      for (int m = 0; m < kMlpMaxN; ++m)
+        if (m < n) dp[(long)m * c0 + ci] = from_f<T>(acc[m]);
+  }
+}
+extern "C" int rtsds_pooled_mlp_bwd(const void* da, const void* a, const void* h, const void* p, const void* w1, const void* w2,
+                                    float* dw1, float* db1, float* dw2, float* db2, void* dp, int n, int c0, int c1, int c2,
+                                    int accumulate, int dtype, void* stream) {
+  if (n <= 0 || n > kMlpMaxN || c0 <= 0 || c1 <= 0 || c2 <= 0 || c0 > kMlpMaxC || c1 > kMlpMaxC || c2 > kMlpMaxC)
+    return RTSDS_ERR_UNSUPPORTED;
+  if (!da || !a || !h || !p || !w1 || !w2 || !dw1 || !dw2 || !dp) return RTSDS_ERR_SHAPE;
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == RTSDS_BF16)
+    hipLaunchKernelGGL(pooled_mlp_bwd_kernel<bf16>, dim3(1), dim3(kMlpThreads), 0, st, (const bf16*)da, (const bf16*)a, (const bf16*)h,
+                       (const bf16*)p, (const bf16*)w1, (const bf16*)w2, dw1, db1, dw2, db2, (bf16*)dp, n, c0, c1, c2,
+                       accumulate ? 1 : 0);
+  else if (dtype == RTSDS_F32)
+    hipLaunchKernelGGL(pooled_mlp_bwd_kernel<float>, dim3(1), dim3(kMlpThreads), 0, st, (const float*)da, (const float*)a, (const float*)h,
+                       (const float*)p, (const float*)w1, (const float*)w2, dw1, db1, dw2, db2, (float*)dp, n, c0, c1, c2,
+                       accumulate ? 1 : 0);
+  else return RTSDS_ERR_UNSUPPORTED;
+  return hipGetLastError() == hipSuccess ? RTSDS_OK : RTSDS_ERR_LAUNCH;
+}
+
 // Vector forms (C % V == 0): every lane loads whole 16-B chunks, all loads of a lane issued
 // before its FMAs -- one memory round trip per wave instead of one per 64 channels (the scalar
 // kernels above walked C in 2-B steps: ~14 us for a 512 x 512 GEMV).

@@ -1063,6 +1063,69 @@ def bn_relu_maxpool(x, gamma, beta, running_mean, running_var, training, momentu
                                  num_batches_tracked, p, ceil_mode)
 
 
+class PooledMlpFn(torch.autograd.Function):
+    """sigmoid(conv2(relu(conv1(p)))) on pooled [N, C, 1, 1] vectors -- the FFM attention
+    (build_bisenet.py:67-70) -- forward as the two pooled conv launches, backward as one launch
+    (rtsds_pooled_mlp_bwd) bit-identical to the six of the per-conv chain."""
+
+    @staticmethod
+    def forward(ctx, p, w1, b1, wq1, w2, b2, wq2):
+        p = nhwc(p)
+        n, c0 = p.shape[0], p.shape[1]
+        c1, c2 = w1.shape[0], w2.shape[0]
+        outs = []
+        for x, wq, b, k, act in ((p, wq1, b1, c1, 1), (None, wq2, b2, c2, 3)):
+            x = outs[-1] if x is None else x
+            d = _conv_desc(x, k, 1, 1, (1, 1), (0, 0), (1, 1))
+            y = empty_nhwc(n, k, 1, 1, p.dtype, p.device)
+            ws = workspace(lib.rtsds_conv2d_fwd_workspace(ctypes.byref(d)), p.device)
+            lib.rtsds_conv2d_fwd(ctypes.byref(d), _P(x), _P(wq), _P(b), _P(y), act, None, _P(ws), ws.numel(), stream())
+            outs.append(y)
+        h, a = outs
+        ctx.params = (w1, b1, w2, b2)
+        ctx.dims = (n, c0, c1, c2)
+        ctx.save_for_backward(p, h, a, wq1, wq2)
+        return a
+
+    @staticmethod
+    def backward(ctx, da):
+        p, h, a, wq1, wq2 = ctx.saved_tensors
+        w1, b1, w2, b2 = ctx.params
+        n, c0, c1, c2 = ctx.dims
+        da = nhwc(da)
+        if da.dtype != a.dtype:
+            da = cast(da, a.dtype)
+        sinks = _sinks(w1, b1, w2, b2)
+        if sinks is not None:
+            dw1, db1, dw2, db2 = sinks
+            acc = 1
+        else:
+            dw1 = torch.empty(c1, c0, 1, 1, dtype=torch.float32, device=p.device)
+            dw2 = torch.empty(c2, c1, 1, 1, dtype=torch.float32, device=p.device)
+            db1 = torch.empty(c1, dtype=torch.float32, device=p.device) if b1 is not None else None
+            db2 = torch.empty(c2, dtype=torch.float32, device=p.device) if b2 is not None else None
+            acc = 0
+        dp = empty_nhwc(n, c0, 1, 1, p.dtype, p.device)
+        lib.rtsds_pooled_mlp_bwd(_P(da), _P(a), _P(h), _P(p), _P(wq1), _P(wq2), _P(dw1), _P(db1), _P(dw2), _P(db2),
+                                 _P(dp), n, c0, c1, c2, acc, dcode(p), stream())
+        if acc:
+            dw1 = db1 = dw2 = db2 = None
+        return dp, dw1, db1, None, dw2, db2, None
+
+
+def pooled_mlp_ok(p, c1, c2):
+    """Shapes rtsds_pooled_mlp_bwd reproduces bit for bit: N <= 8 pooled rows, <= 64 channels,
+    channel counts off the vector kernels' multiples."""
+    n, c0 = p.shape[0], p.shape[1]
+    v = 8 if p.dtype == torch.bfloat16 else 4
+    return p.dim() == 4 and p.shape[2] == p.shape[3] == 1 and n <= 8 and max(c0, c1, c2) <= 64 and \
+        all(c % v for c in (c0, c1, c2)) and p.dtype in (torch.bfloat16, torch.float32)
+
+
+def pooled_mlp(p, w1, b1, wq1, w2, b2, wq2):
+    return PooledMlpFn.apply(p, w1, b1, wq1, w2, b2, wq2)
+
+
 class GapFn(torch.autograd.Function):
     """Mean over H, W keeping dims -> [N, C, 1, 1].  ``join``: GradJoin shared with the other
     reader of x (the attention modules' channel scale): the backward adds its broadcast into

@@ -84,6 +84,10 @@ class AttentionRefinementModule(torch.nn.Module):
 class FeatureFusionModule(torch.nn.Module):
     """build_bisenet.py:56-81: cat -> ConvBlock(s1) -> GAP -> 1x1+ReLU -> 1x1+sigmoid -> f*a + f."""
 
+    # with autograd: the attention (two pooled 1x1 convs) as functional.PooledMlpFn, whose
+    # backward is one launch instead of six (False: the per-conv chain, for A/B tests)
+    fused_attention = True
+
     def __init__(self, num_classes, in_channels):
         super().__init__()
         self.in_channels = in_channels
@@ -108,7 +112,14 @@ class FeatureFusionModule(torch.nn.Module):
             "in_channels of ConvBlock should be {}".format(x.size(1))
         feature = self.convblock(x)
         join = F.GradJoin(2) if torch.is_grad_enabled() and feature.requires_grad else None  # see ARM.forward
-        att = self.conv2(self.conv1(F.global_avg_pool(feature, join), act="relu"), act="sigmoid")
+        pooled = F.global_avg_pool(feature, join)
+        if self.fused_attention and torch.is_grad_enabled() and pooled.is_cuda and \
+                F.pooled_mlp_ok(pooled, self.conv1.out_channels, self.conv2.out_channels):
+            # the attention's backward in one launch (functional.PooledMlpFn)
+            att = F.pooled_mlp(pooled, self.conv1.weight, self.conv1.bias, _shadow(self.conv1.weight, pooled.dtype),
+                               self.conv2.weight, self.conv2.bias, _shadow(self.conv2.weight, pooled.dtype))
+        else:
+            att = self.conv2(self.conv1(pooled, act="relu"), act="sigmoid")
         return F.channel_scale(feature, att, residual=True, join=join)
 
 

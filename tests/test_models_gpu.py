@@ -855,6 +855,41 @@ def test_bisenet_spatial_into_concat_train_bit_identical(graphed):
         assert torch.equal(s0[k], s1[k]), k
 
 
+@pytest.mark.parametrize("graphed", [False, True])
+def test_bisenet_fused_attention_bit_identical(graphed):
+    """FeatureFusionModule.fused_attention (the attention's two pooled convs as
+    functional.PooledMlpFn: backward in one launch) leaves losses, parameters and optimizer
+    state bit-identical to the per-conv chain (sigmoid / ReLU backward, pooled data and weight
+    gradients), eagerly and as hipGraph replays."""
+    from rtsds_amd.models.bisenet.build_bisenet import FeatureFusionModule
+    from rtsds_amd.runtime import GraphedStep
+    g = torch.Generator().manual_seed(13)
+    x = torch.randn(2, 3, 128, 256, generator=g).to(DEV)
+    y = torch.randint(0, 20, (2, 128, 256), generator=g).to(DEV)
+    ce = losses.CrossEntropyLoss(ignore_index=19)
+    runs = []
+    with rtsds_amd.precision(torch.bfloat16):
+        for fused in (False, True):
+            FeatureFusionModule.fused_attention = fused
+            try:
+                torch.manual_seed(7)
+                net = BiSeNet(19, "resnet18").to(DEV).train()
+                opt = optim.Adam(net.parameters(), lr=1e-3)
+                core = lambda: rtrain.seg_step(net, ce, opt, x, y)  # noqa: E731
+                step = GraphedStep(core, [opt], warmup=1) if graphed else core
+                ls = [[float(v) for v in step()] for _ in range(3)]
+                torch.cuda.synchronize()
+                st = {k: v.detach().float().cpu().clone() for k, v in net.state_dict().items()}
+                st.update({f"m{i}": a.m.cpu() for i, a in enumerate(opt.arenas())})
+                runs.append((ls, st))
+            finally:
+                FeatureFusionModule.fused_attention = True
+    (l0, s0), (l1, s1) = runs
+    assert l0 == l1
+    for k in s0:
+        assert torch.equal(s0[k], s1[k]), k
+
+
 def test_bisenet_feature_joins_main_head_only():
     """A caller that leaves the supervision outputs out of its loss: with the joins (first
     contribution returned, GradJoin first_returns) cx1 / cx2 still receive the resize
