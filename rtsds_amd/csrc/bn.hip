@@ -11,6 +11,7 @@
 #include <algorithm>
 
 static const int kBnMaxRB = 2048;  // row blocks of the partial-statistics pass
+static const int kBnTinyRows = 64;  // up to this many rows: one block per channel finalizes and applies
 
 // Threads of a 256-block are laid out [row group][channel vector]; TPR = threads per row.
 template <int VEC> struct BnLayout {
@@ -135,10 +136,10 @@ RT_DEV void chan_merge_shfl(float& n, float& m, float& M) {
 }
 // 4 waves per channel: wave w merges partials b = w*64 + lane (+ 256 k), then the four wave
 // results are merged in wave order -- up to kBnMaxRB partials without a pre-merge launch.
-__global__ void __launch_bounds__(256) bn_finalize_kernel(const float* __restrict__ part, int nrb, int c, long rows, const float* gamma,
-                                   const float* beta, float* rmean, float* rvar, float* smean, float* sinv,
-                                   float* scale, float* shift, float momentum, float eps, long long* nbt) {
-  __shared__ float wr[4][3];
+// (returns true in thread 0, which then holds the channel's scale / shift in sc_out / sh_out)
+RT_DEV bool bn_finalize_body(const float* __restrict__ part, int nrb, int c, long rows, const float* gamma, const float* beta,
+                             float* rmean, float* rvar, float* smean, float* sinv, float* scale, float* shift, float momentum,
+                             float eps, long long* nbt, float (*wr)[3], float& sc_out, float& sh_out) {
   const int ch = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   if (nbt && ch == 0 && threadIdx.x == 0) *nbt += 1;  // num_batches_tracked.add_(1)
   // the per-channel operands of the tail, loaded up front (in flight with the partials: the
@@ -169,7 +170,7 @@ __global__ void __launch_bounds__(256) bn_finalize_kernel(const float* __restric
   chan_merge_shfl(n, m, M);
   if (lane == 0) { wr[wave][0] = n; wr[wave][1] = m; wr[wave][2] = M; }
   __syncthreads();
-  if (threadIdx.x != 0) return;
+  if (threadIdx.x != 0) return false;
   n = wr[0][0]; m = wr[0][1]; M = wr[0][2];
   for (int w = 1; w < 4; ++w) chan_merge(n, m, M, wr[w][0], wr[w][1], wr[w][2]);
   const float var = M / (float)rows;
@@ -181,9 +182,18 @@ __global__ void __launch_bounds__(256) bn_finalize_kernel(const float* __restric
     const float unb = rows > 1 ? M / (float)(rows - 1) : var;
     rvar[ch] = (1.f - momentum) * rv0 + momentum * unb;
   }
-  bn_coef(g0, b0, m, inv, scale[ch], shift[ch]);
+  bn_coef(g0, b0, m, inv, sc_out, sh_out);
+  scale[ch] = sc_out;
+  shift[ch] = sh_out;
+  return true;
 }
-
+__global__ void __launch_bounds__(256) bn_finalize_kernel(const float* __restrict__ part, int nrb, int c, long rows, const float* gamma,
+                                   const float* beta, float* rmean, float* rvar, float* smean, float* sinv,
+                                   float* scale, float* shift, float momentum, float eps, long long* nbt) {
+  __shared__ float wr[4][3];
+  float sc, sh;
+  bn_finalize_body(part, nrb, c, rows, gamma, beta, rmean, rvar, smean, sinv, scale, shift, momentum, eps, nbt, wr, sc, sh);
+}
 __global__ void bn_eval_coef_kernel(int c, const float* gamma, const float* beta, const float* rmean, const float* rvar,
                                     float* scale, float* shift, float* smean, float* sinv, float eps) {
   const int ch = blockIdx.x * blockDim.x + threadIdx.x;
@@ -222,6 +232,31 @@ RT_DEV void load_coef(const float* __restrict__ p, int ch0, int c, float* v) {
   } else {
 #pragma unroll
     for (int j = 0; j < VEC; ++j) v[j] = p[min(ch0 + j, c - 1)];
+  }
+}
+
+// Few rows (the attention modules' BatchNorms on [N, C] pooled rows): the finalize's block also
+// applies y = act(x * scale + shift [+ res]) to its channel's rows (bn_apply_kernel's expression)
+// -- one launch instead of two, bit-identical.
+template <typename T>
+__global__ void __launch_bounds__(256) bn_finalize_apply_kernel(const float* __restrict__ part, int nrb, int c, long rows,
+                                                                 const float* gamma, const float* beta, float* rmean, float* rvar,
+                                                                 float* smean, float* sinv, float* scale, float* shift,
+                                                                 float momentum, float eps, long long* nbt, const T* __restrict__ x,
+                                                                 const T* __restrict__ res, T* __restrict__ y, long ldy, int act) {
+  __shared__ float wr[4][3];
+  __shared__ float cs[2];
+  float sc, sh;
+  if (bn_finalize_body(part, nrb, c, rows, gamma, beta, rmean, rvar, smean, sinv, scale, shift, momentum, eps, nbt, wr, sc, sh)) {
+    cs[0] = sc;
+    cs[1] = sh;
+  }
+  __syncthreads();
+  const int ch = blockIdx.x;
+  for (long r = threadIdx.x; r < rows; r += 256) {
+    float a = fmaf(to_f(x[r * c + ch]), cs[0], cs[1]);
+    if (res) a += to_f(res[r * c + ch]);
+    y[r * ldy + ch] = from_f<T>(act_f(a, act));
   }
 }
 
@@ -468,6 +503,175 @@ __global__ void __launch_bounds__(256) bn_bwd_stats_kernel(const GS gs, const T*
   }
 }
 
+// All three backward passes in one launch when the statistics pass has a single row block
+// (bn_bwd_rb == 1: the attention modules' BatchNorms on [N, C] pooled rows): the same statistics
+// loop and reduction as bn_bwd_stats_kernel (grid (1, channel blocks)), the finalize of a single
+// partial (bn_bwd_finalize_rb_kernel's 0 + p), the apply of bn_bwd_apply_kernel -- so the results
+// are bit-identical to the three launches.
+template <typename T, int VEC, bool HAS_Y, class GS, int ACT>
+__global__ void __launch_bounds__(256) bn_bwd_tiny_kernel(const GS gs, const T* __restrict__ x, const T* __restrict__ y,
+                                                           const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                           const float* __restrict__ mean, const float* __restrict__ sinv,
+                                                           float* __restrict__ dgamma, float* __restrict__ dbeta, T* __restrict__ dx,
+                                                           T* __restrict__ dres, long rows, int c, int act_rt, int training,
+                                                           int accumulate) {
+  const int act = ACT >= 0 ? ACT : act_rt;
+  __shared__ float red[2][256][VEC];
+  __shared__ float cf[3][256 * VEC];
+  const int cbase = blockIdx.y * 256 * VEC;
+  const int cl = min(c - cbase, 256 * VEC);
+  const BnLayout<VEC> L(cl);
+  const int tid = threadIdx.x, cv = tid % L.tpr, rg = tid / L.tpr;
+  const int ch0 = cbase + cv * VEC;
+  const bool active = rg < L.rpi && cv * VEC < cl;
+  float sg[VEC], sgx[VEC], mu[VEC], sc[VEC], sh[VEC];
+  constexpr int U = 2;
+  // rows <= U * rpi: the statistics loop runs once and its (masked) g and x stay in registers
+  // for the apply -- one memory round trip fewer
+  const bool one_pass = rows <= U * (long)L.rpi;
+  float g[U][VEC], xv[U][VEC];
+  // the accumulated parameter gradients and the finalize's operands, loaded up front
+  float dg0[VEC], db0[VEC], inv0[VEC], gm0[VEC];
+#pragma unroll
+  for (int j = 0; j < VEC; ++j) {
+    sg[j] = 0.f;
+    sgx[j] = 0.f;
+    const int ch = min(ch0 + j, c - 1);
+    inv0[j] = sinv[ch];
+    gm0[j] = gamma ? gamma[ch] : 1.f;
+    dg0[j] = accumulate && dgamma ? dgamma[ch] : 0.f;
+    db0[j] = accumulate && dbeta ? dbeta[ch] : 0.f;
+  }
+  if (active) {
+    bn_bwd_coef<VEC>(ch0, c, gamma, beta, mean, sinv, mu, sc, sh);
+    const long step = L.rpi;  // (one row block)
+    for (long r = rg; r < rows; r += U * step) {
+      float yv[HAS_Y ? U : 1][VEC];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const long rr = min(r + u * step, rows - 1);
+        gs.template load<VEC>(rr, ch0, g[u], c - ch0);
+        load_vec<T, VEC>(x + rr * c + ch0, xv[u], c - ch0);
+        if constexpr (HAS_Y) load_vec<T, VEC>(y + rr * c + ch0, yv[u], c - ch0);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (r + u * step >= rows) {
+#pragma unroll
+          for (int j = 0; j < VEC; ++j) g[u][j] = 0.f;
+        }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (act) {
+#pragma unroll
+          for (int j = 0; j < VEC; ++j)
+            g[u][j] *= HAS_Y ? act_grad(yv[HAS_Y ? u : 0][j], act)
+                             : (fmaf(xv[u][j], sc[j], sh[j]) > 0.f ? 1.f : (act == RTSDS_ACT_LEAKY ? 0.2f : 0.f));
+        }
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) {
+          sg[j] += g[u][j];
+          sgx[j] = fmaf(g[u][j], xv[u][j] - mu[j], sgx[j]);
+        }
+      }
+    }
+  }
+  // the block sums (bn_bwd_stats_kernel's two reduction forms), then the single partial's finalize
+  float tg[VEC], tgx[VEC];
+  bool have = false;
+  if ((L.tpr & (L.tpr - 1)) == 0 && L.tpr <= 64) {
+    const int lane = tid & 63, wave = tid >> 6;
+    for (int o = L.tpr; o < 64; o <<= 1) {
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) {
+        sg[j] += __shfl_xor(sg[j], o, 64);
+        sgx[j] += __shfl_xor(sgx[j], o, 64);
+      }
+    }
+    if (lane < L.tpr) {
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) { red[0][wave * 64 + lane][j] = sg[j]; red[1][wave * 64 + lane][j] = sgx[j]; }
+    }
+    __syncthreads();
+    if (tid < L.tpr && tid * VEC < cl) {
+      have = true;
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) {
+        tg[j] = (red[0][tid][j] + red[0][64 + tid][j]) + (red[0][128 + tid][j] + red[0][192 + tid][j]);
+        tgx[j] = (red[1][tid][j] + red[1][64 + tid][j]) + (red[1][128 + tid][j] + red[1][192 + tid][j]);
+      }
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) { red[0][tid][j] = sg[j]; red[1][tid][j] = sgx[j]; }
+    __syncthreads();
+    if (rg == 0 && cv * VEC < cl) {
+      have = true;
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) {
+        float a = red[0][tid][j], b = red[1][tid][j];
+        for (int gi = 1; gi < L.rpi; ++gi) {
+          a += red[0][gi * L.tpr + cv][j];
+          b += red[1][gi * L.tpr + cv][j];
+        }
+        tg[j] = a;
+        tgx[j] = b;
+      }
+    }
+  }
+  if (have) {  // (tid == cv here: the first row group holds the channel vector)
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) {
+      const int ch = ch0 + j;
+      if (ch >= c) continue;
+      const float sgv = 0.f + tg[j], sgxv = 0.f + tgx[j];  // bn_bwd_finalize_rb_kernel: one partial
+      const float inv = inv0[j], gm = gm0[j];
+      if (dgamma) dgamma[ch] = accumulate ? dg0[j] + sgxv * inv : sgxv * inv;
+      if (dbeta) dbeta[ch] = accumulate ? db0[j] + sgv : sgv;
+      const float a = gm * inv;
+      const float invn = 1.f / (float)rows;
+      cf[0][cv * VEC + j] = a;
+      cf[1][cv * VEC + j] = training ? -a * inv * inv * sgxv * invn : 0.f;
+      cf[2][cv * VEC + j] = training ? -a * sgv * invn : 0.f;
+    }
+  }
+  __syncthreads();
+  if (!active || (!dx && !dres)) return;
+  const int cvalid = c - ch0;
+  float ca[VEC], cb[VEC], ck[VEC];
+#pragma unroll
+  for (int j = 0; j < VEC; ++j) {
+    ca[j] = cf[0][cv * VEC + j];
+    cb[j] = cf[1][cv * VEC + j];
+    ck[j] = cf[2][cv * VEC + j];
+  }
+  if (one_pass) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long r = rg + u * (long)L.rpi;
+      if (r >= rows) break;
+      const long off = r * c + ch0;
+      float o[VEC];
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) o[j] = fmaf(ca[j], g[u][j], fmaf(cb[j], xv[u][j] - mu[j], ck[j]));
+      if (dx) store_vec<T, VEC>(dx + off, o, cvalid);
+      if (dres) store_vec<T, VEC>(dres + off, g[u], cvalid);
+    }
+    return;
+  }
+  for (long r = rg; r < rows; r += L.rpi) {
+    const long off = r * c + ch0;
+    float gr[VEC], xr[VEC];
+    gs.template load<VEC>(r, ch0, gr, cvalid);
+    load_vec<T, VEC>(x + off, xr, cvalid);
+    bn_act_grad<T, VEC>(gr, HAS_Y ? y + off : nullptr, xr, sc, sh, act, cvalid);
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) xr[j] = fmaf(ca[j], gr[j], fmaf(cb[j], xr[j] - mu[j], ck[j]));
+    if (dx) store_vec<T, VEC>(dx + off, xr, cvalid);
+    if (dres) store_vec<T, VEC>(dres + off, gr, cvalid);
+  }
+}
+
 // Backward pass 2: coefficients  dx = A*g + B*(x-mean) + C  per channel (one wave each).
 // coef = [A | B | C | mean | scale | shift] x c  (the last three for the mask recompute).
 __global__ void __launch_bounds__(256) bn_bwd_finalize_kernel(const float* __restrict__ part, int nrb, int c, long rows, const float* gamma,
@@ -696,6 +900,11 @@ static void bn_fwd_launch(const void* x, const void* res, void* y, long rows, in
       hipLaunchKernelGGL((bn_stats_kernel<T, VEC>), dim3(rb, rt_cdiv(c, 256 * VEC)), dim3(256), 0, st, (const T*)x, w.part, rows, c);
       part = w.part;
     }
+    if (rows <= kBnTinyRows) {  // finalize + apply in one launch
+      hipLaunchKernelGGL(bn_finalize_apply_kernel<T>, dim3(c), dim3(256), 0, st, part, rb, c, rows, gamma, beta, rm, rv, sm, si,
+                         scale, shift, mom, eps, nbt, (const T*)x, (const T*)res, (T*)y, ldy, act);
+      return;
+    }
     hipLaunchKernelGGL(bn_finalize_kernel, dim3(c), dim3(256), 0, st, part, rb, c, rows, gamma, beta, rm, rv,
                        sm, si, scale, shift, mom, eps, nbt);
   } else {
@@ -761,6 +970,22 @@ static void bn_bwd_launch(const GS& gs, const void* x, const void* y, void* dx, 
   // g = dy * relu'(y) as dres, and the apply pass reads g and x (not dy, y) -- one full read
   // less; g is exactly dy or 0, so the arithmetic is unchanged
   const bool g_out = !pre && y && act == RTSDS_ACT_RELU && dres && dx && GS::kDirect;
+  if (!pre && rb == 1 && GS::kDirect && !g_out) {  // one row block: the three passes in one launch
+    const dim3 grid(1, rt_cdiv(c, 256 * VEC));
+    if (y && act)
+      with_act(act, [&](auto a) {
+        hipLaunchKernelGGL((bn_bwd_tiny_kernel<T, VEC, true, GS, decltype(a)::value>), grid, dim3(256), 0, st, gs, (const T*)x,
+                           (const T*)y, gamma, beta, smean, sinv, dgamma, dbeta, (T*)dx, (T*)dres, rows, c, act, training,
+                           accumulate);
+      });
+    else
+      with_act(act, [&](auto a) {
+        hipLaunchKernelGGL((bn_bwd_tiny_kernel<T, VEC, false, GS, decltype(a)::value>), grid, dim3(256), 0, st, gs, (const T*)x,
+                           (const T*)y, gamma, beta, smean, sinv, dgamma, dbeta, (T*)dx, (T*)dres, rows, c, act, training,
+                           accumulate);
+      });
+    return;
+  }
   if (pre) {  // statistics already produced by the consumer conv's data-gradient epilogue
     part = pre;
     rb = pre_nrb;
