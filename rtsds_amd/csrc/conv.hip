@@ -176,6 +176,41 @@ __global__ void __launch_bounds__(256) colsum_part_kernel(const T* __restrict__ 
       if (ch0 + j < c) part[(long)blockIdx.x * c + ch0 + j] = acc[j];
   }
 }
+// colsum_part_kernel<T, 1> (the same layout, loop and reduction: bit-identical partials) that
+// also writes the gradient's channel-padded copy [rows][cp] the weight-gradient GEMM reads
+// (pad_channels_kernel's job) -- one launch and one read of dY for both (c <= 256).
+template <typename T>
+__global__ void __launch_bounds__(256) pad_colsum_kernel(const T* __restrict__ dy, T* __restrict__ dyp, float* __restrict__ part,
+                                                         long rows, int c, int cp) {
+  __shared__ float red[256];
+  const int tpr = c, rpi = 256 / tpr;
+  const int tid = threadIdx.x, cv = tid % tpr, rg = tid / tpr;
+  float acc = 0.f;
+  if (rg < rpi) {
+    const long step = (long)gridDim.x * rpi;
+    for (long r = (long)blockIdx.x * rpi + rg; r < rows; r += 4 * step) {
+      T sv[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) sv[u] = dy[min(r + u * step, rows - 1) * c + cv];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const long rr = r + u * step;
+        if (rr < rows) {
+          acc += to_f(sv[u]);
+          T* o = dyp + rr * cp;
+          o[cv] = sv[u];
+          for (int pc = c + cv; pc < cp; pc += tpr) o[pc] = from_f<T>(0.f);
+        }
+      }
+    }
+  }
+  red[tid] = acc;
+  __syncthreads();
+  if (rg == 0) {
+    for (int g = 1; g < rpi; ++g) acc += red[g * tpr + cv];
+    part[(long)blockIdx.x * c + cv] = acc;
+  }
+}
 __global__ void colsum_final_kernel(const float* __restrict__ part, float* __restrict__ out, int rb, int c, int accumulate) {
   const int cc = blockIdx.x, lane = threadIdx.x;
   float s = 0.f;
@@ -1698,8 +1733,15 @@ static int wgrad_impl(const rtsds_conv_desc* d0, const void* x, const void* dy, 
       x = x4;
     }
   }
+  // bf16 bias gradient of a narrow (k % 8, k <= 256) padded dY: the padded copy and the bias
+  // column-sum partials in one pass (pad_colsum_kernel)
+  const int crb = (int)std::max<long>(1, std::min<long>(kColsumRB, R / 64));
+  const bool fused_colsum = dbias && pl.kp != d.k && d0->dtype == RTSDS_BF16 && d0->k % 8 != 0 && d0->k <= 256;
   if (pl.kp != d.k) {
-    pad_any(d.dtype, dy, dyp, R, d.k, pl.kp, st);
+    if (fused_colsum)
+      hipLaunchKernelGGL(pad_colsum_kernel<bf16>, dim3(crb), dim3(256), 0, st, (const bf16*)dy, (bf16*)dyp, part, R, d.k, pl.kp);
+    else
+      pad_any(d.dtype, dy, dyp, R, d.k, pl.kp, st);
     dyk = dyp;
     d.k = pl.kp;
   }
@@ -1753,9 +1795,11 @@ static int wgrad_impl(const rtsds_conv_desc* d0, const void* x, const void* dy, 
   }
   if (dbias) {
     const int k = d0->k;
-    const int rb = (int)std::max<long>(1, std::min<long>(kColsumRB, R / 64));
+    const int rb = crb;
     const bool b16 = d0->dtype == RTSDS_BF16;
-    if (b16 && k % 8 == 0)
+    if (fused_colsum)
+      ;  // partials already written by pad_colsum_kernel
+    else if (b16 && k % 8 == 0)
       hipLaunchKernelGGL((colsum_part_kernel<bf16, 8>), dim3(rb, rt_cdiv(k, 2048)), dim3(256), 0, st, (const bf16*)dy, part, R, k);
     else if (b16)
       hipLaunchKernelGGL((colsum_part_kernel<bf16, 1>), dim3(rb, rt_cdiv(k, 256)), dim3(256), 0, st, (const bf16*)dy, part, R, k);
