@@ -469,6 +469,12 @@ int rtsds_pooled_mlp_bwd(const void* da, const void* a, const void* h, const voi
                          const void* w2, float* dw1, float* db1, float* dw2, float* db2, void* dp,
                          int n, int c0, int c1, int c2, int accumulate, int dtype, void* stream);
 
+/* Its forward in one launch: h = relu(conv1(p) + b1), a = sigmoid(conv2(h) + b2) (b1 / b2 may
+ * be NULL), h and a stored [n][c1] / [n][c2]; equal bit for bit to the two pooled 1x1 conv
+ * launches of rtsds_conv2d_fwd for the same shapes (same limits as rtsds_pooled_mlp_bwd).     */
+int rtsds_pooled_mlp_fwd(const void* p, const void* w1, const float* b1, const void* w2, const float* b2, void* h,
+                         void* a, int n, int c0, int c1, int c2, int dtype, void* stream);
+
 /* ABI revision of this header (RTSDS_ABI_VERSION): bumped whenever an entry point's signature
  * changes.  The Python loader refuses a library whose revision differs (A/B variant libraries
  * built from older sources would otherwise be called with the wrong argument lists). */

@@ -68,6 +68,7 @@ SIGNATURES = {
     "rtsds_bn_fwd_ld": (c_int, [P, P, P, c_long, c_long, c_int, P, P, P, P, P, P, P, c_float, c_float, c_int,
                                 c_int, P, c_int, c_int, P, c_size_t, P]),
     "rtsds_bn_fold": (c_int, [P, P, P, P, P, c_float, c_int, P, P, P]),
+    "rtsds_pooled_mlp_fwd": (c_int, [P, P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, P]),
     "rtsds_pooled_mlp_bwd": (c_int, [P, P, P, P, P, P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, P]),
     "rtsds_bn_bwd_part": (c_int, [P, P, P, P, P, c_long, c_int, P, P, P, P, c_int, c_int, c_int, P, c_int, c_int, P,
                                   c_size_t, P]),

@@ -516,6 +516,74 @@ __global__ void __launch_bounds__(kMlpThreads) pooled_mlp_bwd_kernel(const T* __
         if (m < n) dp[(long)m * c0 + ci] = from_f<T>(acc[m]);
   }
 }
+// Its forward in one launch: h = relu(conv1(p) + b1), a = sigmoid(conv2(h) + b2) with
+// pooled_fwd_kernel's arithmetic per output channel (a wave per channel, lanes over the input
+// channels in order, the wave's shuffle sum, then the bias and activation) -- bit-identical to
+// its two launches; h is staged (rounded) in LDS between the two layers.
+template <typename T>
+__global__ void __launch_bounds__(kMlpThreads) pooled_mlp_fwd_kernel(const T* __restrict__ p, const T* __restrict__ w1,
+                                                                     const float* __restrict__ b1, const T* __restrict__ w2,
+                                                                     const float* __restrict__ b2, T* __restrict__ h, T* __restrict__ a,
+                                                                     int n, int c0, int c1, int c2) {
+  __shared__ float sx[kMlpMaxN][kMlpMaxC];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  for (int e = tid; e < kMlpMaxN * kMlpMaxC; e += kMlpThreads) {
+    const int m = e >> 6, ch = e & 63;
+    sx[m][ch] = m < n && ch < c0 ? to_f(p[m * c0 + ch]) : 0.f;
+  }
+  __syncthreads();
+  auto layer = [&](const T* __restrict__ w, const float* __restrict__ b, T* __restrict__ y, int c, int k_n, int act,
+                   float (*keep)[kMlpMaxC]) {
+    for (int k = wave; k < k_n; k += kMlpThreads / 64) {
+      float acc[kMlpMaxN];
+#pragma unroll
+      for (int m = 0; m < kMlpMaxN; ++m) acc[m] = 0.f;
+      for (int ci = lane; ci < c; ci += 64) {
+        const float wv = to_f(w[(long)k * c + ci]);
+#pragma unroll
+        for (int m = 0; m < kMlpMaxN; ++m) acc[m] = fmaf(sx[m][ci], wv, acc[m]);  // (rows past n: zero)
+      }
+#pragma unroll
+      for (int m = 0; m < kMlpMaxN; ++m) acc[m] = wave_sum(acc[m]);
+      if (lane == 0) {
+        const float bv = b ? b[k] : 0.f;
+#pragma unroll
+        for (int m = 0; m < kMlpMaxN; ++m)
+          if (m < n) {
+            float v = fmaf(acc[m], 1.f, bv);
+            if (act == RTSDS_ACT_RELU) v = fmaxf(v, 0.f);
+            else v = 1.f / (1.f + expf(-v));
+            const T o = from_f<T>(v);
+            y[(long)m * k_n + k] = o;
+            if (keep) keep[m][k] = to_f(o);
+          }
+      }
+    }
+  };
+  __shared__ float sh[kMlpMaxN][kMlpMaxC];
+  for (int e = tid; e < kMlpMaxN * kMlpMaxC; e += kMlpThreads) sh[e >> 6][e & 63] = 0.f;
+  __syncthreads();
+  layer(w1, b1, h, c0, c1, RTSDS_ACT_RELU, sh);
+  __syncthreads();
+  for (int e = tid; e < kMlpMaxN * kMlpMaxC; e += kMlpThreads) sx[e >> 6][e & 63] = sh[e >> 6][e & 63];
+  __syncthreads();
+  layer(w2, b2, a, c1, c2, RTSDS_ACT_SIGMOID, nullptr);
+}
+extern "C" int rtsds_pooled_mlp_fwd(const void* p, const void* w1, const float* b1, const void* w2, const float* b2, void* h,
+                                    void* a, int n, int c0, int c1, int c2, int dtype, void* stream) {
+  if (n <= 0 || n > kMlpMaxN || c0 <= 0 || c1 <= 0 || c2 <= 0 || c0 > kMlpMaxC || c1 > kMlpMaxC || c2 > kMlpMaxC)
+    return RTSDS_ERR_UNSUPPORTED;
+  if (!p || !w1 || !w2 || !h || !a) return RTSDS_ERR_SHAPE;
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == RTSDS_BF16)
+    hipLaunchKernelGGL(pooled_mlp_fwd_kernel<bf16>, dim3(1), dim3(kMlpThreads), 0, st, (const bf16*)p, (const bf16*)w1, b1,
+                       (const bf16*)w2, b2, (bf16*)h, (bf16*)a, n, c0, c1, c2);
+  else if (dtype == RTSDS_F32)
+    hipLaunchKernelGGL(pooled_mlp_fwd_kernel<float>, dim3(1), dim3(kMlpThreads), 0, st, (const float*)p, (const float*)w1, b1,
+                       (const float*)w2, b2, (float*)h, (float*)a, n, c0, c1, c2);
+  else return RTSDS_ERR_UNSUPPORTED;
+  return hipGetLastError() == hipSuccess ? RTSDS_OK : RTSDS_ERR_LAUNCH;
+}
 extern "C" int rtsds_pooled_mlp_bwd(const void* da, const void* a, const void* h, const void* p, const void* w1, const void* w2,
                                     float* dw1, float* db1, float* dw2, float* db2, void* dp, int n, int c0, int c1, int c2,
                                     int accumulate, int dtype, void* stream) {

@@ -1065,23 +1065,18 @@ def bn_relu_maxpool(x, gamma, beta, running_mean, running_var, training, momentu
 
 class PooledMlpFn(torch.autograd.Function):
     """sigmoid(conv2(relu(conv1(p)))) on pooled [N, C, 1, 1] vectors -- the FFM attention
-    (build_bisenet.py:67-70) -- forward as the two pooled conv launches, backward as one launch
-    (rtsds_pooled_mlp_bwd) bit-identical to the six of the per-conv chain."""
+    (build_bisenet.py:67-70) -- forward as one launch (rtsds_pooled_mlp_fwd) bit-identical to the
+    two pooled conv launches, backward as one launch (rtsds_pooled_mlp_bwd) bit-identical to the
+    six of the per-conv chain."""
 
     @staticmethod
     def forward(ctx, p, w1, b1, wq1, w2, b2, wq2):
         p = nhwc(p)
         n, c0 = p.shape[0], p.shape[1]
         c1, c2 = w1.shape[0], w2.shape[0]
-        outs = []
-        for x, wq, b, k, act in ((p, wq1, b1, c1, 1), (None, wq2, b2, c2, 3)):
-            x = outs[-1] if x is None else x
-            d = _conv_desc(x, k, 1, 1, (1, 1), (0, 0), (1, 1))
-            y = empty_nhwc(n, k, 1, 1, p.dtype, p.device)
-            ws = workspace(lib.rtsds_conv2d_fwd_workspace(ctypes.byref(d)), p.device)
-            lib.rtsds_conv2d_fwd(ctypes.byref(d), _P(x), _P(wq), _P(b), _P(y), act, None, _P(ws), ws.numel(), stream())
-            outs.append(y)
-        h, a = outs
+        h = empty_nhwc(n, c1, 1, 1, p.dtype, p.device)
+        a = empty_nhwc(n, c2, 1, 1, p.dtype, p.device)
+        lib.rtsds_pooled_mlp_fwd(_P(p), _P(wq1), _P(b1), _P(wq2), _P(b2), _P(h), _P(a), n, c0, c1, c2, dcode(p), stream())
         ctx.params = (w1, b1, w2, b2)
         ctx.dims = (n, c0, c1, c2)
         ctx.save_for_backward(p, h, a, wq1, wq2)

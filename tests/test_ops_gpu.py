@@ -1305,3 +1305,40 @@ def test_tapconv_partial_tiles(geo):
     torch.cuda.synchronize()
     _close(dw, dwr, torch.float32, "wgrad", tol=1e-4)
     _close(dwa, dwr + dw0.double().cpu(), torch.float32, "wgrad accumulate", tol=1e-4)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("n,c0,c1,c2,bias", [(2, 19, 19, 19, True), (8, 61, 13, 61, False), (1, 3, 5, 7, True)])
+def test_pooled_mlp_matches_conv_chain(dt, n, c0, c1, c2, bias):
+    """rtsds_pooled_mlp_fwd / _bwd (the FFM attention, build_bisenet.py:67-70, one launch each)
+    equal the pooled 1x1 conv chain (conv + ReLU, conv + sigmoid) bit for bit: outputs, dL/dp
+    and the weight / bias gradients."""
+    g = torch.Generator().manual_seed(n * 100 + c0)
+    p = torch.randn(n, c0, 1, 1, generator=g).to(DEV, dt)
+    w1 = (torch.randn(c1, c0, 1, 1, generator=g) * 0.3).to(DEV)
+    w2 = (torch.randn(c2, c1, 1, 1, generator=g) * 0.3).to(DEV)
+    b1 = torch.randn(c1, generator=g).to(DEV) if bias else None
+    b2 = torch.randn(c2, generator=g).to(DEV) if bias else None
+    da = torch.randn(n, c2, 1, 1, generator=g).to(DEV, dt)
+    assert F.pooled_mlp_ok(p, c1, c2)
+    outs = []
+    for fused in (False, True):
+        ps = p.clone().requires_grad_(True)
+        ws = [t.clone().requires_grad_(True) if t is not None else None for t in (w1, b1, w2, b2)]
+        q1, q2 = _shadow(ws[0], dt), _shadow(ws[2], dt)
+        if fused:
+            a = F.pooled_mlp(ps, ws[0], ws[1], q1, ws[2], ws[3], q2)
+        else:
+            h = F.conv2d(ps, ws[0], ws[1], q1, act=1)
+            a = F.conv2d(h, ws[2], ws[3], q2, act=3)
+        a.backward(da)
+        torch.cuda.synchronize()
+        outs.append([a.detach().float().cpu(), ps.grad.float().cpu()] +
+                    [t.grad.cpu() for t in ws if t is not None])
+    for u, v in zip(*outs):
+        assert torch.equal(u, v)
+    ref = torch.sigmoid(TF.conv2d(torch.relu(TF.conv2d(p.double(), w1.double(), b1.double() if bias else None)),
+                                  w2.double(), b2.double() if bias else None))
+    tol = 2e-2 if dt == torch.bfloat16 else 1e-5
+    assert (outs[1][0].double() - ref.cpu()).abs().max() < tol
