@@ -1357,6 +1357,57 @@ __global__ void __launch_bounds__(256) bilinear_bwd_fused_vec_kernel(const T* __
     *(V16*)(dx + (((long)img * hi + ih) * wi + iw) * c + ch) = o;
   }
 }
+// The same one-pass form for channel counts off the vector width (the supervision heads'
+// 19-class logits): a thread per (input pixel, channel), dY dense (pitch c).  Adjacent lanes
+// read adjacent channels, so each tap's loads stay contiguous across the wave.
+template <typename T, int G>
+__global__ void __launch_bounds__(256) bilinear_bwd_fused_kernel(const T* __restrict__ dy, T* __restrict__ dx, int hi, int wi, int c,
+                                                                 int ho, int wo, float sh, float sw, int maxh, int maxw, long total,
+                                                                 FastDiv f_c, FastDiv f_wi, FastDiv f_hi) {
+  extern __shared__ float tab[];
+  float* wtab = tab;
+  int* wlo = (int*)(wtab + wi * maxw);
+  float* htab = (float*)(wlo + wi);
+  int* hlo = (int*)(htab + hi * maxh);
+  int* wspan = hlo + hi;
+  int* hspan = wspan + wi;
+  bil_table_build(wtab, wlo, wi, wo, sw, maxw);
+  bil_table_build(htab, hlo, hi, ho, sh, maxh);
+  bil_table_span(wtab, wspan, wi, maxw);
+  bil_table_span(htab, hspan, hi, maxh);
+  GRID_STRIDE_XCD(i, total) {  // total < 2^31 (host)
+    const uint32_t q = fdiv((uint32_t)i, f_c), r = fdiv(q, f_wi);
+    const int ch = (int)((uint32_t)i - q * c), iw = (int)(q - r * wi);
+    const uint32_t img = fdiv(r, f_hi);
+    const int ih = (int)(r - img * hi);
+    const float* wx = wtab + iw * maxw;
+    const float* wy = htab + ih * maxh;
+    const T* base = dy + (((long)img * ho + hlo[ih]) * wo + wlo[iw]) * c + ch;
+    const int jx0 = wspan[iw] & 0xffff, jx1 = wspan[iw] >> 16;
+    const int ky0 = hspan[ih] & 0xffff, ky1 = hspan[ih] >> 16;
+    float acc = 0.f;
+    for (int k = ky0; k < ky1; ++k) {
+      const float yk = wy[k];
+      if (yk == 0.f) continue;
+      const T* row = base + (long)k * wo * c;
+      float t = 0.f;
+      for (int j0 = jx0; j0 < jx1; j0 += G) {
+        T v[G];
+        float xw[G];
+#pragma unroll
+        for (int u = 0; u < G; ++u) {
+          const int j = j0 + u;
+          xw[u] = j < jx1 ? wx[j] : 0.f;
+          v[u] = row[(long)min(j, jx1 - 1) * c];
+        }
+#pragma unroll
+        for (int u = 0; u < G; ++u) t = xw[u] != 0.f ? fmaf(xw[u], to_f(v[u]), t) : t;
+      }
+      acc = fmaf(yk, t, acc);
+    }
+    dx[i] = from_f<T>(acc);
+  }
+}
 // most outputs any input index of an axis receives from (bil_wsum_range, host float math)
 static int bil_maxw(int in, int out, float s) {
   int m = 0;
@@ -1386,6 +1437,13 @@ static void bilinear_bwd_launch(const T* dy, float* tmp, T* dx, int n, int hi, i
     auto kern = mw >= 10 ? bilinear_bwd_fused_vec_kernel<T, 8> : bilinear_bwd_fused_vec_kernel<T, 4>;
     hipLaunchKernelGGL(kern, dim3(ew_blocks(tv)), dim3(256), bw + bh + (wi + hi) * 4, st, dy, dx, hi, wi, c, ho, wo, sh, sw, dyld,
                        dyoff, mh, mw, tv, fastdiv_make(c / V), fastdiv_make(wi), fastdiv_make(hi));
+    return;
+  }
+  if (c % V != 0 && dyld == c && dyoff == 0 && th < (1L << 31) && bw + bh + (wi + hi) * 4 <= (size_t)kBilTabLds &&
+      (long)n * ho * wo * c < (1L << 40)) {
+    auto kern = mw >= 10 ? bilinear_bwd_fused_kernel<T, 8> : bilinear_bwd_fused_kernel<T, 4>;
+    hipLaunchKernelGGL(kern, dim3(ew_blocks(th)), dim3(256), bw + bh + (wi + hi) * 4, st, dy, dx, hi, wi, c, ho, wo, sh, sw, mh, mw,
+                       th, fastdiv_make(c), fastdiv_make(wi), fastdiv_make(hi));
     return;
   }
   if (tw < (1L << 31) && bw <= (size_t)kBilTabLds)

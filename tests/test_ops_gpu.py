@@ -423,12 +423,14 @@ def test_bilinear(geo, dt):
 
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("geo", [(16, 32, 64, 128, 64), (32, 64, 64, 128, 256), (13, 17, 97, 129, 16), (8, 8, 8, 8, 8)])
+@pytest.mark.parametrize("geo", [(16, 32, 64, 128, 64), (32, 64, 64, 128, 256), (13, 17, 97, 129, 16), (8, 8, 8, 8, 8),
+                                 (32, 64, 64, 128, 19), (16, 32, 64, 128, 19), (13, 17, 97, 129, 19), (8, 8, 8, 8, 3)])
 def test_bilinear_bwd_fused_bit_identical(geo, dt):
-    """The one-pass vector backward (bilinear_bwd_fused_vec_kernel: channel counts, dY pitch and
-    offset multiples of 16 B) equals the two-pass W / H kernels bit for bit: the same dY read
-    through a row pitch of c + 1 (not a vector multiple) takes the two-pass route.  And both
-    match torch fp64."""
+    """The one-pass backward -- bilinear_bwd_fused_vec_kernel (channel counts, dY pitch and
+    offset multiples of 16 B) or, for channel counts off the vector width with a dense dY,
+    bilinear_bwd_fused_kernel (the supervision heads' 19 classes) -- equals the two-pass W / H
+    kernels bit for bit: the same dY read through a row pitch of c + 1 takes the two-pass
+    route.  And both match torch fp64."""
     import ctypes
     from rtsds_amd._lib import lib
     from rtsds_amd.functional import _P, dcode
