@@ -557,8 +557,6 @@ static bool upce_plan(int n, int hl, int wl, int c, int H, int W, float sh, floa
   // 32 full-res rows per tile: one wave per (tile, head) walks them, so shorter tiles mean more
   // waves in flight (the row loop is latency-bound at ~3 waves per SIMD)
   g.th = std::max(1, std::min(32, (int)(kUpceRows / std::ceil(fy))));
-  g.ntr = (hl + g.th - 1) / g.th;
-  g.ntc = (wl + g.tw - 1) / g.tw;
   g.wmax = (int)std::ceil((g.tw + 1) * fx) + 4;
   g.hmax = (int)std::ceil((g.th + 1) * fy) + 4;
   // kernel limits: two 64-column groups per row, <= 512 owned (column, class) pairs
@@ -567,37 +565,46 @@ static bool upce_plan(int n, int hl, int wl, int c, int H, int W, float sh, floa
     g.wmax = (int)std::ceil((g.tw + 1) * fx) + 4;
   }
   if (g.wmax > 128 || (g.tw + 1) * c > 192) return false;  // <= 3 x-fold pairs per lane
+  // tile counts from the final tile width (the loop above narrows it for small factors)
+  g.ntr = (hl + g.th - 1) / g.th;
+  g.ntc = (wl + g.tw - 1) / g.tw;
   g.nblocks = n * g.ntr * g.ntc;
   return (long)g.nblocks * g.ntr < (1L << 31);
 }
 static int upce_cp(int c) { return (c + 3) / 4 * 4; }
-// the auxiliary wave (upce_fwd_kernel): with fewer heads than waves a workgroup can hold
-static bool upce_aux(int nheads) { return nheads < kUpceMaxHeads; }
-static size_t upce_lds(const UpceGeo& g, int nheads) {
+static size_t upce_lds_with(const UpceGeo& g, int nheads, bool aux) {
   const size_t cp = upce_cp(g.c), tile_el = (size_t)(g.th + 1) * (g.tw + 1) * cp;
   const size_t head = (((size_t)(g.tw + 1) * g.wmax + 4 * (size_t)g.wmax + 2 * (size_t)(g.tw + 1) + 3) & ~(size_t)3);
-  return (head + nheads * (tile_el + 64 * cp) + (upce_aux(nheads) ? 2 * 64 * cp : 0)) * 4 + (size_t)g.hmax * g.wmax;
+  return (head + nheads * (tile_el + 64 * cp) + (aux ? 2 * 64 * cp : 0)) * 4 + (size_t)g.hmax * g.wmax;
 }
+static const size_t kUpceLdsCap = 64 * 1024;
+// the auxiliary wave (upce_fwd_kernel): with fewer heads than waves a workgroup can hold, and
+// only when its two fold rows still fit the LDS cap -- otherwise the head waves take its roles
+// (the AX = false instantiation), so the aux rows never shrink the supported geometries
+static bool upce_aux(const UpceGeo& g, int nheads) {
+  return nheads < kUpceMaxHeads && upce_lds_with(g, nheads, true) <= kUpceLdsCap;
+}
+static size_t upce_lds(const UpceGeo& g, int nheads) { return upce_lds_with(g, nheads, upce_aux(g, nheads)); }
 static size_t upce_tile_el(const UpceGeo& g) { return (size_t)(g.th + 1) * (g.tw + 1) * g.c; }
 // ws: stat[64] (count, per-head loss sums; offset 0, see the header) | [heads][nblocks][tile_el]
 //     gradient partials | [heads][nblocks] loss partials | [nblocks] counts | (auxiliary wave)
 //     [nblocks][tile_el] one-hot partials | [nblocks] argmax matches
 static const size_t kUpceStat = 64;
 static size_t upce_ws_floats(const UpceGeo& g, int heads) {
-  return kUpceStat + (size_t)(heads + (upce_aux(heads) ? 1 : 0)) * g.nblocks * upce_tile_el(g) + (size_t)heads * g.nblocks +
+  return kUpceStat + (size_t)(heads + (upce_aux(g, heads) ? 1 : 0)) * g.nblocks * upce_tile_el(g) + (size_t)heads * g.nblocks +
          2 * (size_t)g.nblocks;
 }
 static float* upce_kpart(float* f, const UpceGeo& g, int heads) {
-  return f + (size_t)(heads + (upce_aux(heads) ? 1 : 0)) * g.nblocks * upce_tile_el(g) + (size_t)heads * g.nblocks + g.nblocks;
+  return f + (size_t)(heads + (upce_aux(g, heads) ? 1 : 0)) * g.nblocks * upce_tile_el(g) + (size_t)heads * g.nblocks + g.nblocks;
 }
 static float* upce_gcorr(float* f, const UpceGeo& g, int heads) {
-  return upce_aux(heads) ? f + (size_t)heads * g.nblocks * (upce_tile_el(g) + 1) + g.nblocks : nullptr;
+  return upce_aux(g, heads) ? f + (size_t)heads * g.nblocks * (upce_tile_el(g) + 1) + g.nblocks : nullptr;
 }
 
 extern "C" size_t rtsds_upce_workspace(int nheads, int n, int hl, int wl, int c, int H, int W, float scale_h, float scale_w) {
   UpceGeo g;
   if (nheads <= 0 || nheads > kUpceMaxHeads || !upce_plan(n, hl, wl, c, H, W, scale_h, scale_w, g)) return 0;
-  if (upce_lds(g, nheads) > 64 * 1024) return 0;
+  if (upce_lds(g, nheads) > kUpceLdsCap) return 0;
   return upce_ws_floats(g, nheads) * 4 + 256;
 }
 
@@ -629,7 +636,7 @@ extern "C" int rtsds_upce_fwd(int nheads, const void* const* logits, const int64
   a.want_grad = want_grad & 1;
   hipStream_t st = (hipStream_t)stream;
   const size_t lds = upce_lds(g, nheads);
-  const dim3 blk(64 * (nheads + (upce_aux(nheads) ? 1 : 0)));
+  const dim3 blk(64 * (nheads + (upce_aux(g, nheads) ? 1 : 0)));
   if (dtype != RTSDS_BF16 && dtype != RTSDS_F32) return RTSDS_ERR_UNSUPPORTED;
   switch (upce_cp(c)) {
 #define UPCE_CASE(CPV)                                                                                      \

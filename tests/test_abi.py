@@ -55,3 +55,14 @@ def test_errors_raise_without_fallback():
     x = torch.zeros(1, 3, 8, 8)
     with pytest.raises(RuntimeError, match="HIP"):
         F.pack_input(x, torch.float32)
+
+
+def test_upce_workspace_aux_wave_never_shrinks_support():
+    """Host planning of the fused upsample + CE (no GPU call): the auxiliary wave's LDS fold rows
+    are used only where they fit, so 3 heads at a x2 resize (over the LDS cap with them) still
+    take the fused path -- without the auxiliary wave -- and the x8 bench geometry keeps it."""
+    lib = _lib.load()
+    x2 = [lib.rtsds_upce_workspace(h, 2, 8, 16, 19, 16, 32, 0.5, 0.5) for h in (1, 2, 3)]
+    assert all(w > 0 for w in x2), x2
+    x8 = [lib.rtsds_upce_workspace(h, 8, 64, 128, 19, 512, 1024, 0.125, 0.125) for h in (3, 4)]
+    assert x8[0] > 0 and x8[1] > 0

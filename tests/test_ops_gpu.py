@@ -725,6 +725,10 @@ def _upce_reference(heads, t, geo_args, ignore):
     (1, 19, 9, 33, {"size": (72, 264)}, 1),          # several column tiles
     (2, 19, 8, 16, {"scale_factor": 8}, 2, 40.0),    # wide logit ranges (softmax shift, exp
     (2, 19, 8, 16, {"scale_factor": 8}, 1, 12.0),    # underflow of the far classes)
+    (2, 19, 8, 16, {"scale_factor": 2}, 3),          # 3 heads at x2: no auxiliary wave (LDS cap)
+    (2, 19, 8, 16, {"scale_factor": 2}, 2),          # 2 heads at x2: with it
+    (2, 19, 8, 16, {"scale_factor": 4}, 3),          # 19 classes below x8: the tile width narrows
+    (1, 19, 16, 40, {"scale_factor": 3}, 1),         # (several column tiles after narrowing)
 ])
 def test_upsample_cross_entropy_fused(case, dt):
     """Fused resize+CE+accuracy (rtsds_upce_*) vs torch fp64 interpolate -> CrossEntropyLoss."""
