@@ -340,7 +340,12 @@ __global__ void __launch_bounds__(256, 2) hconv_dgrad_nt_kernel(const HconvArgs 
     const int n = 16 * j + fr;
     bslot[j] = (n * 4 + (fc ^ ((n >> 2) & 3))) * 16;
   }
-  constexpr int kSt = 8;  // 8-B stores per lane and tile
+  // vector-memory ops per lane that follow tile j's weight DMA: the 8-B stores of the epilogue
+  // below (kFi pixel fragments x kFj channel halves) -- the count the wait at the top of tile
+  // j + 1 leaves in flight.  With P.accum the epilogue also loads the old values; the compiler's
+  // wait for those drains the prefetched weight DMA as well (vmcnt retires in order), so the
+  // accumulate path runs without the weight double-buffer overlap (correct, slower).
+  constexpr int kFi = 4, kFj = 2, kSt = kFi * kFj;
   for (int j = j0; j < j1; ++j) {
     const int st = (j - j0) & 1;
     // tile j's weights (and, first, the halo) landed -- all but this wave's stores of tile j - 1 --
@@ -385,11 +390,11 @@ __global__ void __launch_bounds__(256, 2) hconv_dgrad_nt_kernel(const HconvArgs 
     // C^T: acc[i][jj][e] = dX[pixel 64 wave + 16 i + fr][channel 32 j + 16 jj + 4 fc + e]
     const int px_r = (64 * wave) / TC;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < kFi; ++i) {  // kFi x kFj stores: keep kSt in step with this loop nest
       const int pc = (64 * wave) % TC + 16 * i + fr;
       const long o = (((long)img * P.h + oh0 + px_r + pc / TC) * P.w + ow0 + pc % TC) * P.k + 32 * j + 4 * fc;
 #pragma unroll
-      for (int jj = 0; jj < 2; ++jj) {
+      for (int jj = 0; jj < kFj; ++jj) {
         bf16x4 t;
         if (P.accum) {
           const bf16x4 old = *(const bf16x4*)(P.y + o + 16 * jj);
