@@ -982,3 +982,34 @@ def test_bisenet_inference_fast_path_matches_general_path(dtype, monkeypatch):
     if general is not None:
         err = (fast - general).abs().max().item() / general.abs().max().item()
         assert err < 1e-4, err
+
+
+def test_bisenet_deferred_wgrad_reduce_bit_identical():
+    """The split-K weight-gradient reductions deferred to the end of backward and batched
+    (functional.DEFER_WGRAD_REDUCE: rtsds_split_reduce_many, up to 32 per launch -- the whole
+    BiSeNet step in one) leave losses, parameters and optimizer state bit-identical to one
+    reduction launch per conv."""
+    from rtsds_amd import functional as Fn
+    g = torch.Generator().manual_seed(17)
+    x = torch.randn(2, 3, 128, 256, generator=g).to(DEV)
+    y = torch.randint(0, 20, (2, 128, 256), generator=g).to(DEV)
+    ce = losses.CrossEntropyLoss(ignore_index=19)
+    runs = []
+    with rtsds_amd.precision(torch.bfloat16):
+        for defer in (False, True):
+            Fn.DEFER_WGRAD_REDUCE = defer
+            try:
+                torch.manual_seed(7)
+                net = BiSeNet(19, "resnet18").to(DEV).train()
+                opt = optim.Adam(net.parameters(), lr=1e-3)
+                ls = [[float(v) for v in rtrain.seg_step(net, ce, opt, x, y)] for _ in range(2)]
+                torch.cuda.synchronize()
+                st = {k: v.detach().float().cpu().clone() for k, v in net.state_dict().items()}
+                st.update({f"m{i}": a.m.cpu() for i, a in enumerate(opt.arenas())})
+                runs.append((ls, st))
+            finally:
+                Fn.DEFER_WGRAD_REDUCE = True
+    (l0, s0), (l1, s1) = runs
+    assert l0 == l1
+    for k in s0:
+        assert torch.equal(s0[k], s1[k]), k
